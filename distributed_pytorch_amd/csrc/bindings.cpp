@@ -1,0 +1,371 @@
+// Python bindings for the gfx950 kernels and the native RCCL communicator.
+// Thin: validate tensors, fetch the caller's current HIP stream, call the extern "C" launchers.
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <torch/extension.h>
+
+#include "runtime/rccl_comm.h"
+
+extern "C" {
+int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd, float gscale,
+                 int first, hipStream_t s);
+int dpa_scale(float* x, long n, float sc, hipStream_t s);
+int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
+int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
+                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st);
+int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int N, int H, int W, int C, int Kout,
+                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st);
+int dpa_wflip(const float* w, float* wd, int K, int R, int S, int C, hipStream_t st);
+int dpa_bn_nchunks(int M);
+int dpa_bn_fwd_stats(const float* z, float* part, int M, int C, const float* gamma, const float* beta,
+                     const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
+                     float* scale, float* shift, float momentum, float eps, hipStream_t st);
+int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
+                       const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st);
+int dpa_bn_apply(const float* z, float* a, const float* scale, const float* shift, int N, int H, int W, int C,
+                 int pool, hipStream_t st);
+int dpa_bn_bwd(const float* g, const float* z, const float* scale, const float* shift, const float* mean,
+               const float* invstd, const float* gamma, float* part, float* coef, float* dgamma, float* dbeta,
+               float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st);
+int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
+                    float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
+                    int Cin, int J, hipStream_t st);
+int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
+                   int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st);
+int dpa_augment(const unsigned char* img, const long long* idx, const long long* labels, float* out,
+                long long* target, int B, int Hs, int Ws, int pad, int train, unsigned long long seed,
+                unsigned long long salt, const float* mean, const float* std, hipStream_t st);
+}
+
+namespace {
+
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void chk(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed: rc=", rc, (rc > 0 ? std::string(" ") + hipGetErrorString((hipError_t)rc) : ""));
+}
+
+void need(const Tensor& t, const char* name, at::ScalarType dt = at::kFloat) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has wrong dtype ", t.scalar_type());
+}
+
+float* fp(const Tensor& t) { return t.data_ptr<float>(); }
+float* ofp(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+
+// ---------------- optimizer / elementwise ----------------
+void sgd_flat(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double wd, double gscale, bool first,
+              int64_t offset, int64_t count) {
+  need(p, "p");
+  need(g, "g");
+  need(buf, "buf");
+  if (count < 0) count = p.numel() - offset;
+  TORCH_CHECK(offset % 4 == 0 && count % 4 == 0, "sgd_flat: offset/count must be multiples of 4");
+  TORCH_CHECK(offset + count <= p.numel() && p.numel() == g.numel() && p.numel() == buf.numel(), "sgd_flat sizes");
+  chk(dpa_sgd_flat(fp(p) + offset, fp(g) + offset, fp(buf) + offset, count, (float)lr, (float)momentum, (float)wd,
+                   (float)gscale, first ? 1 : 0, cur_stream()),
+      "sgd_flat");
+}
+
+void scale_(Tensor x, double s) {
+  need(x, "x");
+  chk(dpa_scale(fp(x), x.numel(), (float)s, cur_stream()), "scale_");
+}
+
+void mean_of_w(Tensor in, Tensor out, int64_t W) {
+  need(in, "in");
+  need(out, "out");
+  TORCH_CHECK(in.numel() == W * out.numel(), "mean_of_w sizes");
+  chk(dpa_mean_of_w(fp(in), fp(out), out.numel(), (int)W, cur_stream()), "mean_of_w");
+}
+
+// ---------------- convolution ----------------
+// x [N,H,W,C], w [K,R,S,C], out [N,P,Q,K]
+void conv_fprop(Tensor x, Tensor w, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile) {
+  need(x, "x");
+  need(w, "w");
+  need(out, "out");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "conv_fprop: 4-d NHWC/KRSC tensors expected");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "conv_fprop: channel mismatch");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(out.size(0) == N && out.size(1) == P && out.size(2) == Q && out.size(3) == K, "conv_fprop: out shape");
+  float* sl = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(slab.has_value(), "conv_fprop: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= splits * (int64_t)N * P * Q * K, "conv_fprop: slab too small");
+    sl = fp(*slab);
+  }
+  chk(dpa_conv_fprop(fp(x), fp(w), fp(out), sl, N, H, W, C, K, R, S, (int)stride, (int)pad, (int)splits, (int)tile,
+                     cur_stream()),
+      "conv_fprop");
+}
+
+// x [N,H,W,C], dz [N,P,Q,K], dw [K,R,S,C]
+void conv_wgrad(Tensor x, Tensor dz, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile) {
+  need(x, "x");
+  need(dz, "dz");
+  need(dw, "dw");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = dw.size(0), R = dw.size(1), S = dw.size(2);
+  TORCH_CHECK(dw.size(3) == C && dz.size(3) == K && dz.size(0) == N, "conv_wgrad: shape mismatch");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dz.size(1) == P && dz.size(2) == Q, "conv_wgrad: dz spatial");
+  float* sl = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(slab.has_value(), "conv_wgrad: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= splits * (int64_t)K * R * S * C, "conv_wgrad: slab too small");
+    sl = fp(*slab);
+  }
+  chk(dpa_conv_wgrad(fp(x), fp(dz), fp(dw), sl, N, H, W, C, K, R, S, (int)stride, (int)pad, (int)splits, (int)tile,
+                     cur_stream()),
+      "conv_wgrad");
+}
+
+void wflip(Tensor w, Tensor wd) {
+  need(w, "w");
+  need(wd, "wd");
+  const int K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(wd.size(0) == C && wd.size(1) == R && wd.size(2) == S && wd.size(3) == K, "wflip: wd shape");
+  chk(dpa_wflip(fp(w), fp(wd), K, R, S, C, cur_stream()), "wflip");
+}
+
+// ---------------- batch norm ----------------
+int64_t bn_nchunks(int64_t M) { return dpa_bn_nchunks((int)M); }
+
+void bn_fwd_stats(Tensor z, Tensor part, Tensor gamma, Tensor beta, OptT bias, OptT rmean, OptT rvar, OptT nbt,
+                  Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum, double eps) {
+  need(z, "z");
+  need(part, "part");
+  const int C = z.size(-1);
+  const int M = z.numel() / C;
+  TORCH_CHECK(part.numel() >= 2L * dpa_bn_nchunks(M) * C, "bn_fwd_stats: part too small");
+  long long* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    need(*nbt, "nbt", at::kLong);
+    nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  chk(dpa_bn_fwd_stats(fp(z), fp(part), M, C, fp(gamma), fp(beta), ofp(bias), ofp(rmean), ofp(rvar), nb, fp(mean),
+                       fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps, cur_stream()),
+      "bn_fwd_stats");
+}
+
+void bn_eval_params(Tensor gamma, Tensor beta, OptT bias, Tensor rmean, Tensor rvar, Tensor scale, Tensor shift,
+                    double eps) {
+  chk(dpa_bn_eval_params(fp(gamma), fp(beta), ofp(bias), fp(rmean), fp(rvar), fp(scale), fp(shift), gamma.numel(),
+                         (float)eps, cur_stream()),
+      "bn_eval_params");
+}
+
+void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool) {
+  need(z, "z");
+  need(a, "a");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  TORCH_CHECK(a.numel() == (int64_t)N * (pool ? (H / 2) * (W / 2) : H * W) * C, "bn_apply: a shape");
+  chk(dpa_bn_apply(fp(z), fp(a), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()), "bn_apply");
+}
+
+void bn_bwd(Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, Tensor gamma, Tensor part,
+            Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool) {
+  need(g, "g");
+  need(z, "z");
+  need(dz, "dz");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
+  TORCH_CHECK(g.numel() == (int64_t)Mo * C, "bn_bwd: g shape");
+  TORCH_CHECK(part.numel() >= 3L * dpa_bn_nchunks(Mo) * C, "bn_bwd: part too small");
+  TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
+  chk(dpa_bn_bwd(fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef), fp(dgamma),
+                 fp(dbeta), ofp(dbias), fp(dz), N, H, W, C, pool ? 1 : 0, cur_stream()),
+      "bn_bwd");
+}
+
+// ---------------- classifier head ----------------
+void fc_ce_train(Tensor x, Tensor w, Tensor b, Tensor target, Tensor loss_row, Tensor dlogits, Tensor dx, Tensor dw,
+                 Tensor db, Tensor loss_out, OptT loss_accum) {
+  need(x, "x");
+  need(target, "target", at::kLong);
+  const int B = x.size(0), Cin = x.size(1), J = w.size(0);
+  chk(dpa_fc_ce_train(fp(x), fp(w), fp(b), reinterpret_cast<const long long*>(target.data_ptr<int64_t>()),
+                      fp(loss_row), fp(dlogits), fp(dx), fp(dw), fp(db), fp(loss_out), ofp(loss_accum), B, Cin, J,
+                      cur_stream()),
+      "fc_ce_train");
+}
+
+void fc_ce_eval(Tensor x, Tensor w, Tensor b, Tensor target, Tensor loss_row, Tensor correct_row, OptT logits,
+                OptT acc) {
+  need(x, "x");
+  need(target, "target", at::kLong);
+  need(correct_row, "correct_row", at::kInt);
+  const int B = x.size(0), Cin = x.size(1), J = w.size(0);
+  chk(dpa_fc_ce_eval(fp(x), fp(w), fp(b), reinterpret_cast<const long long*>(target.data_ptr<int64_t>()),
+                     fp(loss_row), correct_row.data_ptr<int>(), ofp(logits), ofp(acc), B, Cin, J, cur_stream()),
+      "fc_ce_eval");
+}
+
+// ---------------- data ----------------
+void augment(Tensor images, Tensor idx, Tensor labels, Tensor out, OptT target, int64_t pad, bool train,
+             int64_t seed, int64_t salt, std::vector<double> mean, std::vector<double> std_) {
+  need(images, "images", at::kByte);
+  need(idx, "idx", at::kLong);
+  need(labels, "labels", at::kLong);
+  need(out, "out");
+  TORCH_CHECK(images.dim() == 4 && images.size(3) == 3, "augment: images must be [N,H,W,3] uint8");
+  const int B = idx.numel(), Hs = images.size(1), Ws = images.size(2);
+  TORCH_CHECK(out.numel() == (int64_t)B * Hs * Ws * 4, "augment: out must be [B,H,W,4]");
+  float m[3], s[3];
+  for (int c = 0; c < 3; ++c) {
+    m[c] = (float)mean.at(c);
+    s[c] = (float)std_.at(c);
+  }
+  long long* tp = nullptr;
+  if (target.has_value() && target->defined()) {
+    need(*target, "target", at::kLong);
+    tp = reinterpret_cast<long long*>(target->data_ptr<int64_t>());
+  }
+  chk(dpa_augment(images.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()),
+                  reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), fp(out), tp, B, Hs, Ws, (int)pad,
+                  train ? 1 : 0, (unsigned long long)seed, (unsigned long long)salt, m, s, cur_stream()),
+      "augment");
+}
+
+// ---------------- RCCL communicator ----------------
+ncclDataType_t nccl_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat:
+      return ncclFloat32;
+    case at::kBFloat16:
+      return ncclBfloat16;
+    case at::kHalf:
+      return ncclFloat16;
+    case at::kLong:
+      return ncclInt64;
+    case at::kInt:
+      return ncclInt32;
+    case at::kByte:
+      return ncclUint8;
+    case at::kDouble:
+      return ncclFloat64;
+    default:
+      TORCH_CHECK(false, "unsupported dtype for RCCL: ", t.scalar_type());
+  }
+}
+
+ncclRedOp_t nccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  TORCH_CHECK(false, "unknown reduce op ", op);
+}
+
+class PyRcclComm {
+ public:
+  PyRcclComm(int rank, int world, py::bytes uid, int device)
+      : stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)),
+        comm_(rank, world, std::string(uid), device, stream_.stream()) {}
+
+  void track(const Tensor& t) { c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_); }
+
+  void all_reduce(Tensor t, const std::string& op) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce: contiguous GPU tensor expected");
+    track(t);
+    comm_.all_reduce(t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), cur_stream());
+  }
+  void broadcast(Tensor t, int root) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "broadcast: contiguous GPU tensor expected");
+    track(t);
+    comm_.broadcast(t.data_ptr(), t.numel(), nccl_dtype(t), root, cur_stream());
+  }
+  void gather(Tensor send, OptT recv, int root) {
+    TORCH_CHECK(send.is_cuda() && send.is_contiguous(), "gather: contiguous GPU tensor expected");
+    track(send);
+    void* rp = nullptr;
+    if (comm_.rank() == root) {
+      TORCH_CHECK(recv.has_value() && recv->numel() == send.numel() * comm_.world(), "gather: recv must be world*n");
+      track(*recv);
+      rp = recv->data_ptr();
+    }
+    comm_.gather(send.data_ptr(), rp, send.numel(), nccl_dtype(send), root, cur_stream());
+  }
+  void reduce_scatter(Tensor send, Tensor recv, const std::string& op) {
+    TORCH_CHECK(send.numel() == recv.numel() * comm_.world(), "reduce_scatter: send must be world*recv");
+    track(send);
+    track(recv);
+    comm_.reduce_scatter(send.data_ptr(), recv.data_ptr(), recv.numel(), nccl_dtype(recv), nccl_op(op), cur_stream());
+  }
+  void all_gather(Tensor send, Tensor recv) {
+    TORCH_CHECK(recv.numel() == send.numel() * comm_.world(), "all_gather: recv must be world*send");
+    track(send);
+    track(recv);
+    comm_.all_gather(send.data_ptr(), recv.data_ptr(), send.numel(), nccl_dtype(send), cur_stream());
+  }
+  void send(Tensor t, int peer) {
+    track(t);
+    comm_.send(t.data_ptr(), t.numel(), nccl_dtype(t), peer, cur_stream());
+  }
+  void recv(Tensor t, int peer) {
+    track(t);
+    comm_.recv(t.data_ptr(), t.numel(), nccl_dtype(t), peer, cur_stream());
+  }
+  void wait() { comm_.wait(cur_stream()); }
+  void synchronize() { comm_.synchronize(); }
+  std::string async_error() { return comm_.async_error(); }
+  void abort() { comm_.abort(); }
+  int64_t stream_ptr() { return reinterpret_cast<int64_t>(stream_.stream()); }
+  int rank() const { return comm_.rank(); }
+  int world() const { return comm_.world(); }
+
+ private:
+  c10::hip::HIPStream stream_;
+  dpa::RcclComm comm_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "distributed_pytorch_amd native extension (gfx950 HIP kernels + RCCL communicator)";
+  m.def("sgd_flat", &sgd_flat, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
+        py::arg("wd"), py::arg("gscale"), py::arg("first"), py::arg("offset") = 0, py::arg("count") = -1);
+  m.def("scale_", &scale_);
+  m.def("mean_of_w", &mean_of_w);
+  m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
+        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dz"), py::arg("dw"), py::arg("slab"), py::arg("stride"),
+        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0);
+  m.def("wflip", &wflip);
+  m.def("bn_nchunks", &bn_nchunks);
+  m.def("bn_fwd_stats", &bn_fwd_stats);
+  m.def("bn_eval_params", &bn_eval_params);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("fc_ce_train", &fc_ce_train);
+  m.def("fc_ce_eval", &fc_ce_eval);
+  m.def("augment", &augment);
+  m.def("rccl_unique_id", []() { return py::bytes(dpa::RcclComm::unique_id()); });
+  m.def("rccl_version", &dpa::RcclComm::version);
+  py::class_<PyRcclComm>(m, "RcclComm")
+      .def(py::init<int, int, py::bytes, int>(), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+      .def("all_reduce", &PyRcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
+      .def("broadcast", &PyRcclComm::broadcast)
+      .def("gather", &PyRcclComm::gather)
+      .def("reduce_scatter", &PyRcclComm::reduce_scatter, py::arg("send"), py::arg("recv"), py::arg("op") = "sum")
+      .def("all_gather", &PyRcclComm::all_gather)
+      .def("send", &PyRcclComm::send)
+      .def("recv", &PyRcclComm::recv)
+      .def("wait", &PyRcclComm::wait)
+      .def("synchronize", &PyRcclComm::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("async_error", &PyRcclComm::async_error)
+      .def("abort", &PyRcclComm::abort)
+      .def("stream_ptr", &PyRcclComm::stream_ptr)
+      .def_property_readonly("rank", &PyRcclComm::rank)
+      .def_property_readonly("world", &PyRcclComm::world);
+}

@@ -1,0 +1,457 @@
+// K1/K2/K3 — convolution as an implicit GEMM on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the reference's mkldnn conv2d forward and convolution_backward
+// (SURVEY §2.3 rows "conv2d" and "convolution_backward"; model.py:18-23).
+// Layout is NHWC activations and KRSC weights, so every GEMM operand row is a contiguous
+// channel run:
+//   FPROP  out[m][n]  = sum_k  Xcol[m][k] * W[n][k]          m=(img,oh,ow) n=kout  k=(r,s,c)
+//   DGRAD  (stride 1, "same" pad) is FPROP of dZ with Wd[c][r][s][k] = W[k][R-1-r][S-1-s][c]
+//   WGRAD  dW[n][k]   = sum_m  dZ[m][n] * Xcol[m][k]          (split-K over m = N*P*Q)
+//
+// Tiling: BM x BN block tile, BK = 32 k per LDS stage, double-buffered LDS with register-staged
+// prefetch (global loads for tile t+1 are issued before the MFMAs of tile t), one barrier per
+// k-tile.  Waves tile the block WAVES_M x WAVES_N; each wave owns (BM/WAVES_M) x (BN/WAVES_N)
+// as 32x32 MFMA sub-tiles.  The f32 MFMA consumes k=2 per instruction with lane half h=l>>5
+// holding k=h; we permute k inside each 8-wide chunk (MFMA t of chunk q uses k = 8q+4h+t for lane
+// half h) so that one ds_read_b128 feeds 4 MFMAs.  The permutation is applied identically to A
+// and B, so the sum over k is unchanged (and each MFMA is still an exact f32 fma chain).
+//
+// LDS images: a k-contiguous operand is stored [row][BK+4] (16-row b128 lane groups hit 16
+// distinct 16-B slots: conflict-free), a row-contiguous operand (WGRAD) [BK][rows+4].
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int KPAD = 4;
+
+struct FastDiv {  // unsigned division by a runtime constant d (d >= 1), exact for n < 2^31
+  unsigned d, mul, shift;
+};
+
+__host__ FastDiv make_fastdiv(unsigned d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) {
+    f.mul = 0;
+    f.shift = 0;
+    return f;
+  }
+  unsigned s = 0;
+  while ((1u << s) < d) ++s;
+  f.shift = s;
+  f.mul = (unsigned)((((unsigned long long)1 << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+__device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) {
+  if (f.d == 1) return n;
+  unsigned t = __umulhi(n, f.mul);
+  return (t + n) >> f.shift;
+}
+
+struct ConvArgs {
+  const float* x;   // FPROP: input NHWC [N,H,W,C]        WGRAD: input NHWC (B operand)
+  const float* w;   // FPROP: weights [Nout][Ktot]         WGRAD: dZ [M][Kout] (A operand)
+  float* out;       // FPROP: out [M][Nout] or slabs       WGRAD: dW [Kout][Ktot] or slabs
+  int N, H, W, C;   // input dims
+  int P, Q;         // output spatial dims
+  int R, S, stride, pad;
+  int M;            // N*P*Q
+  int Nout;         // FPROP: output channels; WGRAD: Kout
+  int Ktot;         // R*S*C
+  int gm, gn;       // tile grid
+  int kchunk;       // split-K chunk (multiple of BK), reduction index range per split
+  long slab;        // elements per split slab (0 when splitK==1)
+  FastDiv fd_C, fd_S, fd_Q, fd_PQ;
+};
+
+template <int ROWS, int THREADS>
+struct KContigSlots {  // a k-contiguous operand tile ROWS x BK, loaded as float4
+  static constexpr int F4_PER_ROW = BK / 4;
+  static constexpr int NSLOT = ROWS * F4_PER_ROW / THREADS;
+  static constexpr int ROW_STEP = THREADS / F4_PER_ROW;
+  static_assert(ROWS * F4_PER_ROW % THREADS == 0, "tile/threads mismatch");
+};
+
+template <int ROWS, int THREADS>
+struct RowContigSlots {  // a row-contiguous operand tile BK x ROWS, loaded as float4
+  static constexpr int F4_PER_K = ROWS / 4;
+  static constexpr int NSLOT = BK * F4_PER_K / THREADS;
+  static constexpr int K_STEP = THREADS / F4_PER_K;
+  static_assert(BK * F4_PER_K % THREADS == 0, "tile/threads mismatch");
+  static_assert(THREADS % F4_PER_K == 0, "threads must cover whole k rows");
+};
+
+__device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool WGRAD>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvArgs a) {
+  constexpr int THREADS = WAVES_M * WAVES_N * 64;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
+  // LDS sizes (floats) per stage
+  constexpr int A_STAGE = WGRAD ? BK * (BM + KPAD) : BM * (BK + KPAD);
+  constexpr int B_STAGE = WGRAD ? BK * (BN + KPAD) : BN * (BK + KPAD);
+  __shared__ __attribute__((aligned(16))) float lds[2 * (A_STAGE + B_STAGE)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid / WAVES_N, wc = wid % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int nwg = a.gm * a.gn;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int bm = tile / a.gn, bn = tile % a.gn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int split = blockIdx.y;
+  const int kbeg = split * a.kchunk;
+  int kend = kbeg + a.kchunk;
+  const int KRED = WGRAD ? a.M : a.Ktot;  // reduction length
+  if (kend > KRED) kend = KRED;
+  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  // ---------------- per-thread load-slot precomputation ----------------
+  // A operand
+  using ASl = typename std::conditional<WGRAD, RowContigSlots<BM, THREADS>, KContigSlots<BM, THREADS>>::type;
+  using BSl = typename std::conditional<WGRAD, RowContigSlots<BN, THREADS>, KContigSlots<BN, THREADS>>::type;
+  constexpr int NA = ASl::NSLOT, NB = BSl::NSLOT;
+
+  float4 ra[NA], rb[NB];
+
+  // FPROP A slots: rows m, fixed k4
+  int a_img[WGRAD ? 1 : NA], a_ih0[WGRAD ? 1 : NA], a_iw0[WGRAD ? 1 : NA];
+  int a_k4 = 0;
+  // WGRAD A slots: fixed kout column group, k rows vary
+  int a_col = 0, a_krow = 0;
+  // FPROP B slots: rows n (weights), fixed k4
+  int b_k4 = 0, b_row0 = 0;
+  // WGRAD B slots: fixed rsc column group
+  int b_rr = 0, b_ss = 0, b_c = 0, b_colvalid = 0, b_krow = 0;
+
+  if constexpr (!WGRAD) {
+    a_k4 = tid % (BK / 4);
+    const int r0 = tid / (BK / 4);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int m = m0 + r0 + j * ASl::ROW_STEP;
+      if (m < a.M) {
+        const unsigned img = fdiv((unsigned)m, a.fd_PQ);
+        const unsigned rem = (unsigned)m - img * (unsigned)(a.P * a.Q);
+        const unsigned oh = fdiv(rem, a.fd_Q);
+        const unsigned ow = rem - oh * (unsigned)a.Q;
+        a_img[j] = (int)img;
+        a_ih0[j] = (int)oh * a.stride - a.pad;
+        a_iw0[j] = (int)ow * a.stride - a.pad;
+      } else {
+        a_img[j] = -1;
+        a_ih0[j] = 0;
+        a_iw0[j] = 0;
+      }
+    }
+    b_k4 = tid % (BK / 4);
+    b_row0 = tid / (BK / 4);
+  } else {
+    a_col = n0 * 0 + m0 + (tid % ASl::F4_PER_K) * 4;  // kout index (A rows = kout, tile origin m0)
+    a_krow = tid / ASl::F4_PER_K;
+    const int rsc = n0 + (tid % BSl::F4_PER_K) * 4;  // B rows = rsc
+    b_colvalid = rsc < a.Ktot;
+    const unsigned tap = fdiv((unsigned)rsc, a.fd_C);
+    b_c = rsc - (int)tap * a.C;
+    const unsigned rr = fdiv(tap, a.fd_S);
+    b_rr = (int)rr - a.pad;
+    b_ss = (int)(tap - rr * a.S) - a.pad;
+    b_krow = tid / BSl::F4_PER_K;
+  }
+
+  auto load_tile = [&](int kt) {
+    const int kb = kbeg + kt * BK;
+    if constexpr (!WGRAD) {
+      const int k = kb + a_k4 * 4;
+      const bool kval = k < kend;
+      const unsigned tap = fdiv((unsigned)k, a.fd_C);
+      const int c = k - (int)tap * a.C;
+      const unsigned r = fdiv(tap, a.fd_S);
+      const int s = (int)(tap - r * a.S);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int ih = a_ih0[j] + (int)r, iw = a_iw0[j] + s;
+        const bool v = kval && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        ra[j] = v ? ldg4(a.x + (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const int kb4 = kb + b_k4 * 4;
+      const bool kbv = kb4 < kend;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int n = n0 + b_row0 + j * BSl::ROW_STEP;
+        const bool v = kbv && n < a.Nout;
+        rb[j] = v ? ldg4(a.w + (long)n * a.Ktot + kb4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+      // A = dZ^T : element (kout, m) = dZ[m][kout]
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int m = kb + a_krow + j * ASl::K_STEP;
+        const bool v = m < kend && a_col < a.Nout;
+        ra[j] = v ? ldg4(a.w + (long)m * a.Nout + a_col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      // B = Xcol^T : element (rsc, m) = X[img, oh*st-pad+r, ow*st-pad+s, c]
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int m = kb + b_krow + j * BSl::K_STEP;
+        bool v = m < kend && b_colvalid;
+        const unsigned img = fdiv((unsigned)m, a.fd_PQ);
+        const unsigned rem = (unsigned)m - img * (unsigned)(a.P * a.Q);
+        const unsigned oh = fdiv(rem, a.fd_Q);
+        const unsigned ow = rem - oh * (unsigned)a.Q;
+        const int ih = (int)oh * a.stride + b_rr, iw = (int)ow * a.stride + b_ss;
+        v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        rb[j] = v ? ldg4(a.x + (((long)img * a.H + ih) * a.W + iw) * a.C + b_c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+
+  auto store_tile = [&](int stage) {
+    float* As = lds + stage * (A_STAGE + B_STAGE);
+    float* Bs = As + A_STAGE;
+    if constexpr (!WGRAD) {
+      const int r0 = tid / (BK / 4);
+#pragma unroll
+      for (int j = 0; j < NA; ++j)
+        *reinterpret_cast<float4*>(As + (r0 + j * ASl::ROW_STEP) * (BK + KPAD) + a_k4 * 4) = ra[j];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        *reinterpret_cast<float4*>(Bs + (b_row0 + j * BSl::ROW_STEP) * (BK + KPAD) + b_k4 * 4) = rb[j];
+    } else {
+      const int ca = (tid % ASl::F4_PER_K) * 4;
+#pragma unroll
+      for (int j = 0; j < NA; ++j)
+        *reinterpret_cast<float4*>(As + (a_krow + j * ASl::K_STEP) * (BM + KPAD) + ca) = ra[j];
+      const int cb = (tid % BSl::F4_PER_K) * 4;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        *reinterpret_cast<float4*>(Bs + (b_krow + j * BSl::K_STEP) * (BN + KPAD) + cb) = rb[j];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute_tile = [&](int stage) {
+    const float* As = lds + stage * (A_STAGE + B_STAGE);
+    const float* Bs = As + A_STAGE;
+#pragma unroll
+    for (int q = 0; q < BK / 8; ++q) {
+      float4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wr * WTM + i * 32 + li;
+        if constexpr (!WGRAD) {
+          fa[i] = *reinterpret_cast<const float4*>(As + row * (BK + KPAD) + 8 * q + 4 * lh);
+        } else {
+          const float* p = As + (8 * q + 4 * lh) * (BM + KPAD) + row;
+          fa[i] = make_float4(p[0], p[BM + KPAD], p[2 * (BM + KPAD)], p[3 * (BM + KPAD)]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wc * WTN + j * 32 + li;
+        if constexpr (!WGRAD) {
+          fb[j] = *reinterpret_cast<const float4*>(Bs + row * (BK + KPAD) + 8 * q + 4 * lh);
+        } else {
+          const float* p = Bs + (8 * q + 4 * lh) * (BN + KPAD) + row;
+          fb[j] = make_float4(p[0], p[BN + KPAD], p[2 * (BN + KPAD)], p[3 * (BN + KPAD)]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < ntiles) load_tile(kt + 1);
+      compute_tile(cur);
+      if (kt + 1 < ntiles) store_tile(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---------------- epilogue: C[row][col], row over BM (A rows), col over BN (B rows) ----------
+  float* out = a.out + (long)split * a.slab;
+  const int ldc = WGRAD ? a.Ktot : a.Nout;
+  const int nrows = WGRAD ? a.Nout : a.M;
+  const int ncols = WGRAD ? a.Ktot : a.Nout;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc * WTN + j * 32 + li;
+      if (col < ncols) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < nrows) out[(long)row * ldc + col] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+// Sum split-K slabs: out[i] = sum_s slab[s*n + i]  (float4 vectorised; n % 4 == 0)
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ slabs, float* __restrict__ out,
+                                                         long n4, int splits) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(slabs)[i];
+    for (int k = 1; k < splits; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(slabs)[(long)k * n4 + i];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+}
+
+// Dgrad weight transform for stride-1 "same" convs: Wd[c][r][s][k] = W[k][R-1-r][S-1-s][c].
+__global__ __launch_bounds__(256) void wflip_kernel(const float* __restrict__ w, float* __restrict__ wd, int K,
+                                                    int R, int S, int C) {
+  const long total = (long)K * R * S * C;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    // i indexes the OUTPUT wd[c][r][s][k] (k fastest -> coalesced writes)
+    const int k = (int)(i % K);
+    long t = i / K;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int c = (int)(t / R);
+    wd[i] = w[(((long)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c];
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool WG>
+int launch_cfg(const ConvArgs& a, int splits, hipStream_t st) {
+  dim3 grid(a.gm * a.gn, splits);
+  conv_gemm_kernel<BM, BN, WM, WN, WG><<<grid, WM * WN * 64, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+int grid_1d(long n) {
+  long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Common conv geometry. out_or_slab must hold splits * rows * cols floats when splits > 1.
+// tile: 0 -> 128x128 (4 waves, 64x64 each), 1 -> 64x64 (4 waves, 32x32 each)
+int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
+                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st) {
+  ConvArgs a{};
+  a.x = x;
+  a.w = w;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.R = R;
+  a.S = S;
+  a.stride = stride;
+  a.pad = pad;
+  a.P = (H + 2 * pad - R) / stride + 1;
+  a.Q = (W + 2 * pad - S) / stride + 1;
+  a.M = N * a.P * a.Q;
+  a.Nout = Kout;
+  a.Ktot = R * S * C;
+  if (C % 4 || Kout % 4) return -2;
+  const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
+  a.gm = cdiv(a.M, BMv);
+  a.gn = cdiv(Kout, BNv);
+  if (splits < 1) splits = 1;
+  a.kchunk = cdiv(cdiv(a.Ktot, splits), BK) * BK;
+  splits = cdiv(a.Ktot, a.kchunk);
+  a.out = splits > 1 ? slab : out;
+  a.slab = splits > 1 ? (long)a.M * Kout : 0;
+  a.fd_C = make_fastdiv(C);
+  a.fd_S = make_fastdiv(S);
+  a.fd_Q = make_fastdiv(a.Q);
+  a.fd_PQ = make_fastdiv(a.P * a.Q);
+  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, false>(a, splits, st) : launch_cfg<64, 64, 2, 2, false>(a, splits, st);
+  if (rc) return rc;
+  if (splits > 1) {
+    const long n4 = (long)a.M * Kout / 4;
+    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, splits);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
+}
+
+// dW[Kout][R*S*C] = sum_m dZ[m][kout] * Xcol[m][rsc]
+int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int N, int H, int W, int C, int Kout,
+                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st) {
+  ConvArgs a{};
+  a.x = x;
+  a.w = dz;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.R = R;
+  a.S = S;
+  a.stride = stride;
+  a.pad = pad;
+  a.P = (H + 2 * pad - R) / stride + 1;
+  a.Q = (W + 2 * pad - S) / stride + 1;
+  a.M = N * a.P * a.Q;
+  a.Nout = Kout;
+  a.Ktot = R * S * C;
+  if (C % 4 || Kout % 4) return -2;
+  const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
+  a.gm = cdiv(Kout, BMv);
+  a.gn = cdiv(a.Ktot, BNv);
+  if (splits < 1) splits = 1;
+  a.kchunk = cdiv(cdiv(a.M, splits), BK) * BK;
+  splits = cdiv(a.M, a.kchunk);
+  a.out = splits > 1 ? slab : dw;
+  a.slab = splits > 1 ? (long)Kout * a.Ktot : 0;
+  a.fd_C = make_fastdiv(C);
+  a.fd_S = make_fastdiv(S);
+  a.fd_Q = make_fastdiv(a.Q);
+  a.fd_PQ = make_fastdiv(a.P * a.Q);
+  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, true>(a, splits, st) : launch_cfg<64, 64, 2, 2, true>(a, splits, st);
+  if (rc) return rc;
+  if (splits > 1) {
+    const long n4 = (long)Kout * a.Ktot / 4;
+    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, splits);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
+}
+
+int dpa_wflip(const float* w, float* wd, int K, int R, int S, int C, hipStream_t st) {
+  wflip_kernel<<<grid_1d((long)K * R * S * C), 256, 0, st>>>(w, wd, K, R, S, C);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

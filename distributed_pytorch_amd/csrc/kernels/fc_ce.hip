@@ -1,0 +1,174 @@
+// K7/K8 — classifier head: Linear(Cin -> J) + softmax cross-entropy (mean reduction), forward
+// and backward fused.  Replaces addmm / _log_softmax / nll_loss and their backwards
+// (model.py:40,45 and main.py:34,99).
+//
+// fc_ce_rows: one wavefront per sample row: logits (wave reductions over Cin), log-sum-exp,
+//   per-row loss, dlogits = (softmax - onehot)/B, and dx = dlogits @ W  — all in registers.
+// fc_ce_wgrad: dW[j][c] = sum_b dlogits[b][j] * x[b][c], db[j] = sum_b dlogits[b][j], and the
+//   batch-mean loss (fixed summation order -> bitwise reproducible).
+#include "common.h"
+
+namespace {
+constexpr int MAXJ = 16;
+
+template <bool TRAIN>
+__global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ bias,
+                                                         const long long* __restrict__ target,
+                                                         float* __restrict__ loss_row, float* __restrict__ dlogits,
+                                                         float* __restrict__ dx, int* __restrict__ correct_row,
+                                                         float* __restrict__ logits_out, int B, int Cin, int J) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* xr = x + (long)row * Cin;
+  float logit[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j < J) {
+      float s = 0.f;
+      for (int c = lane; c < Cin; c += 64) s += xr[c] * w[(long)j * Cin + c];
+      logit[j] = wave_sum(s) + bias[j];
+    } else {
+      logit[j] = -INFINITY;
+    }
+  }
+  float mx = logit[0];
+  int arg = 0;
+#pragma unroll
+  for (int j = 1; j < MAXJ; ++j)
+    if (j < J && logit[j] > mx) {
+      mx = logit[j];
+      arg = j;
+    }
+  float se = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j)
+    if (j < J) se += expf(logit[j] - mx);
+  const float lse = mx + logf(se);
+  const int t = (int)target[row];
+  float lt = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j)
+    if (j == t) lt = logit[j];
+  if (lane == 0) {
+    loss_row[row] = lse - lt;
+    if (correct_row) correct_row[row] = (arg == t) ? 1 : 0;
+  }
+  if (logits_out && lane < J) {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j)
+      if (j == lane) logits_out[(long)row * J + j] = logit[j];
+  }
+  if (TRAIN) {
+    const float invB = 1.f / (float)B;
+    float dl[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) dl[j] = j < J ? (expf(logit[j] - lse) - (j == t ? 1.f : 0.f)) * invB : 0.f;
+    if (lane < J) {
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j)
+        if (j == lane) dlogits[(long)row * J + j] = dl[j];
+    }
+    for (int c = lane; c < Cin; c += 64) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j)
+        if (j < J) s += dl[j] * w[(long)j * Cin + c];
+      dx[(long)row * Cin + c] = s;
+    }
+  }
+}
+
+// grid: J + 1 blocks.  Block j < J computes dW[j][:] and db[j]; block J reduces the loss.
+__global__ __launch_bounds__(256) void fc_ce_wgrad_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ dlogits,
+                                                          const float* __restrict__ loss_row, float* __restrict__ dw,
+                                                          float* __restrict__ db, float* __restrict__ loss_out,
+                                                          float* __restrict__ loss_accum, int B, int Cin, int J) {
+  const int j = blockIdx.x;
+  __shared__ float sh[256];
+  if (j < J) {
+    for (int c = threadIdx.x; c < Cin; c += 256) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += dlogits[(long)b * J + j] * x[(long)b * Cin + c];
+      dw[(long)j * Cin + c] = s;
+    }
+    float s = 0.f;
+    for (int b = threadIdx.x; b < B; b += 256) s += dlogits[(long)b * J + j];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) db[j] = sh[0];
+  } else {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < B; b += 256) s += loss_row[b];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const float l = sh[0] / (float)B;
+      loss_out[0] = l;
+      if (loss_accum) loss_accum[0] += l;
+    }
+  }
+}
+
+// Eval accumulation: acc[0] += mean loss of this batch, acc[1] += #correct (as float, exact < 2^24)
+__global__ __launch_bounds__(256) void eval_accum_kernel(const float* __restrict__ loss_row,
+                                                         const int* __restrict__ correct_row, float* __restrict__ acc,
+                                                         int B) {
+  __shared__ float sl[256];
+  __shared__ int sc[256];
+  float l = 0.f;
+  int c = 0;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    l += loss_row[b];
+    c += correct_row[b];
+  }
+  sl[threadIdx.x] = l;
+  sc[threadIdx.x] = c;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      sl[threadIdx.x] += sl[threadIdx.x + o];
+      sc[threadIdx.x] += sc[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    acc[0] += sl[0] / (float)B;
+    acc[1] += (float)sc[0];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
+                    float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
+                    int Cin, int J, hipStream_t st) {
+  if (J > MAXJ) return -2;
+  fc_ce_rows_kernel<true><<<cdiv(B, 4), 256, 0, st>>>(x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin,
+                                                      J);
+  fc_ce_wgrad_kernel<<<J + 1, 256, 0, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B, Cin, J);
+  return (int)hipGetLastError();
+}
+
+int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
+                   int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st) {
+  if (J > MAXJ) return -2;
+  fc_ce_rows_kernel<false><<<cdiv(B, 4), 256, 0, st>>>(x, w, b, target, loss_row, nullptr, nullptr, correct_row, logits,
+                                                       B, Cin, J);
+  if (acc) eval_accum_kernel<<<1, 256, 0, st>>>(loss_row, correct_row, acc, B);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

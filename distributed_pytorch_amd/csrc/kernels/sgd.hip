@@ -1,0 +1,82 @@
+// K9 — fused multi-tensor SGD (momentum, weight decay, optional grad scale) over ONE flat fp32
+// arena.  Replaces the reference's torch.optim.SGD for-loop / foreach path
+// (/root/reference/main.py:103-104, per-param add/mul_/add_/add_ — SURVEY §2.3 row "SGD step")
+// with a single streaming kernel: 5 × 4 B per parameter (p, g, buf read; p, buf written).
+//
+// torch semantics (dampening 0, nesterov False):
+//   d = g*scale + wd*p ; buf = first ? d : momentum*buf + d ; p -= lr*buf
+#include "common.h"
+
+__global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ buf, long n4, float lr, float momentum,
+                                                       float wd, float gscale, int first) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 bv;
+    float d0 = gv.x * gscale + wd * pv.x;
+    float d1 = gv.y * gscale + wd * pv.y;
+    float d2 = gv.z * gscale + wd * pv.z;
+    float d3 = gv.w * gscale + wd * pv.w;
+    if (first) {
+      bv = make_float4(d0, d1, d2, d3);
+    } else {
+      bv = reinterpret_cast<float4*>(buf)[i];
+      bv.x = momentum * bv.x + d0;
+      bv.y = momentum * bv.y + d1;
+      bv.z = momentum * bv.z + d2;
+      bv.w = momentum * bv.w + d3;
+    }
+    pv.x -= lr * bv.x;
+    pv.y -= lr * bv.y;
+    pv.z -= lr * bv.z;
+    pv.w -= lr * bv.w;
+    reinterpret_cast<float4*>(buf)[i] = bv;
+    reinterpret_cast<float4*>(p)[i] = pv;
+  }
+}
+
+// Elementwise y = x * s over a flat fp32 range (K12: grad /= W for the all-reduce mode when the
+// scale is not fused into the optimizer).
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, long n, float s) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
+}
+
+// K11 — mean over W stacked copies: out[i] = (sum_w in[w*n + i]) / W   (gather mode, rank 0).
+__global__ __launch_bounds__(256) void mean_of_w_kernel(const float* __restrict__ in, float* __restrict__ out, long n,
+                                                        int W) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const float inv = 1.0f / (float)W;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int w = 0; w < W; ++w) s += in[(long)w * n + i];
+    out[i] = s * inv;
+  }
+}
+
+static int grid_for(long n, int block) {
+  long g = (n + block - 1) / block;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd,
+                            float gscale, int first, hipStream_t s) {
+  if (n % 4) return -1;
+  const long n4 = n / 4;
+  sgd_flat_kernel<<<grid_for(n4, 256), 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dpa_scale(float* x, long n, float sc, hipStream_t s) {
+  scale_kernel<<<grid_for(n, 256), 256, 0, s>>>(x, n, sc);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s) {
+  mean_of_w_kernel<<<grid_for(n, 256), 256, 0, s>>>(in, out, n, W);
+  return (int)hipGetLastError();
+}

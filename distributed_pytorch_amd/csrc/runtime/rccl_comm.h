@@ -1,0 +1,62 @@
+// Native RCCL communicator: one process per MI355X, collectives issued on a dedicated comm HIP
+// stream that is fenced against the caller's compute stream with HIP events (no host sync).
+//
+// Replaces the reference's c10d ProcessGroupGloo usage:
+//   gather/scatter (main_gather.py:49,59)  -> grouped ncclSend/ncclRecv + ncclBroadcast
+//   all_reduce     (main_all_reduce.py:47) -> ncclAllReduce
+//   DDP Reducer buckets / buffer broadcast (main_ddp.py:137) -> ncclAllReduce / ncclBroadcast
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <string>
+#include <vector>
+
+namespace dpa {
+
+class RcclComm {
+ public:
+  // uid: NCCL_UNIQUE_ID_BYTES bytes created by rank 0 (unique_id()) and shared out of band.
+  RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream);
+  ~RcclComm();
+
+  static std::string unique_id();
+  static int version();
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  hipStream_t stream() const { return stream_; }
+
+  // All ops: comm stream waits for everything already queued on `after` (the compute stream),
+  // then runs the collective.  Returns immediately.
+  void all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t after);
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t after);
+  // Rank `root` receives world*count elements into recv (its own contribution copied in place).
+  void gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t after);
+  void reduce_scatter(const void* send, void* recv, size_t recvcount, ncclDataType_t dt, ncclRedOp_t op,
+                      hipStream_t after);
+  void all_gather(const void* send, void* recv, size_t sendcount, ncclDataType_t dt, hipStream_t after);
+  void send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t after);
+  void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t after);
+
+  // `waiter` waits (device-side) for all comm work issued so far.
+  void wait(hipStream_t waiter);
+  // Host blocks until all comm work issued so far completes.
+  void synchronize();
+  // Non-blocking: returns "" if healthy, else an error string (ncclCommGetAsyncError).
+  std::string async_error();
+  void abort();
+
+ private:
+  void fence_after(hipStream_t after);
+  void check(ncclResult_t r, const char* what);
+
+  int rank_, world_, device_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_;
+  hipEvent_t ev_in_, ev_out_;
+  std::atomic<bool> aborted_{false};
+};
+
+}  // namespace dpa

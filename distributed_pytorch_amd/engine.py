@@ -1,0 +1,337 @@
+"""VGGEngine — the hand-scheduled MI355X trainer for the reference's VGG family.
+
+The reference trains ``model.VGG11()`` through PyTorch autograd (main.py:31-37).  Here the whole
+step is a static schedule of native kernels over persistent buffers:
+
+  forward   per conv layer: conv_fprop (MFMA implicit GEMM, NHWC/KRSC) → bn_fwd_stats
+            (batch stats + running-stat update) → bn_apply (+ReLU, +2x2 max-pool)
+  head      fc_ce_train: Linear + softmax-CE loss, dlogits, dW, db, dx in two launches
+  backward  per conv layer (reverse): bn_bwd (max-pool/ReLU routing recomputed from z, BN
+            backward, dgamma/dbeta/dbias) → dgrad (conv_fprop on flipped weights) → wgrad
+            (split-K implicit GEMM) — after each layer a ``grad_ready`` callback lets the
+            gradient-sync strategy launch that bucket's collective on the comm stream while the
+            remaining backward runs
+  update    sgd_flat over the flat parameter/grad/momentum arenas (one launch)
+
+Parameters/grads/momentum are three :class:`~distributed_pytorch_amd.utils.arena.Arena` s with
+identical layout (reference ``named_parameters()`` order; conv weights stored KRSC, the first
+layer's input channels zero-padded 3→4).  ``state_dict()``/``load_state_dict()`` speak the
+reference's 58-key OIHW layout (model.py; SURVEY §2.3 "Model facts").
+
+On a CPU device the same schedule runs on :mod:`distributed_pytorch_amd.ops.cpu_ref` (plain
+torch), which is what the multi-process gloo tests drive.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from . import _ext
+from .models.vgg import VGGSpec
+from .ops import cpu_ref
+from .utils.arena import Arena
+
+
+def _pow2_round(x: float) -> int:
+    p = 1
+    while p * 2 <= x * 1.4142:
+        p *= 2
+    return p
+
+
+def conv_cfg(kind: str, M: int, N: int, K: int):
+    """(tile, splits) heuristic for the implicit-GEMM conv kernels, fitted to per-layer sweeps on
+    MI355X (tools/conv_bench.py; profiles/conv_bench_r1.txt).  kind: 'fprop' | 'wgrad'.
+    fprop/dgrad GEMM: [M x K]·[K x N];  wgrad GEMM: [N(=Kout) x M(=NPQ)]·[M x K(=RSC)]."""
+    cdiv = lambda a, b: (a + b - 1) // b
+    if kind == "wgrad":
+        tiles = cdiv(N, 64) * cdiv(K, 64)
+        s = max(1, min(128, _pow2_round(2048 / tiles)))
+        while s > 1 and M // s < 128:
+            s //= 2
+        return 1, s
+    if N <= 64:
+        tiles = cdiv(M, 64) * cdiv(N, 64)
+        s = 1
+        while tiles * s < 512 and K // (s * 2) >= 256:
+            s *= 2
+        return 1, s
+    tiles = cdiv(M, 128) * cdiv(N, 128)
+    if tiles >= 512:
+        return 0, 1
+    s = max(1, _pow2_round(512 / tiles))
+    while s > 1 and K // s < 256:
+        s //= 2
+    return 0, s
+
+
+class VGGEngine:
+    def __init__(self, name: str = "VGG11", device="cuda", max_batch: int = 256, num_classes: int = 10,
+                 lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4, bn_momentum: float = 0.1,
+                 bn_eps: float = 1e-5, in_hw: int = 32, backend=None):
+        self.device = torch.device(device)
+        self.spec = VGGSpec.from_name(name, num_classes, in_hw)
+        self.K = backend if backend is not None else (_ext.require() if self.device.type == "cuda" else cpu_ref)
+        self.max_batch = max_batch
+        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
+        self.bn_momentum, self.bn_eps = bn_momentum, bn_eps
+        self.num_classes = num_classes
+        self.steps_taken = 0
+        dev = self.device
+        L = self.spec.convs
+        entries = []
+        for l in L:
+            entries += [(f"{l.conv_key}.weight", (l.cout, 3, 3, l.cin_pad)), (f"{l.conv_key}.bias", (l.cout,)),
+                        (f"{l.bn_key}.weight", (l.cout,)), (f"{l.bn_key}.bias", (l.cout,))]
+        entries += [("fc1.weight", (num_classes, self.spec.fc_in)), ("fc1.bias", (num_classes,))]
+        self.params = Arena(entries, dev)
+        self.grads = self.params.like()
+        self.mom = self.params.like()
+        self.buffers = Arena([(f"{l.bn_key}.{b}", (l.cout,)) for l in L for b in ("running_mean", "running_var")],
+                             dev)
+        self.nbt = torch.zeros(len(L), dtype=torch.int64, device=dev)
+        for l in L:
+            self.buffers[f"{l.bn_key}.running_var"].fill_(1.0)
+
+        # ---- workspaces (sized for max_batch) ----
+        N = max_batch
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.x0 = torch.zeros(N, in_hw, in_hw, 4, **f32)
+        self.target = torch.zeros(N, dtype=torch.int64, device=dev)
+        self.z, self.a, self.g, self.dz, self.wflip = [], [], [], [], []
+        self.stats = []  # per layer dict(mean, invstd, scale, shift)
+        self.eval_ss = []
+        slab_need, part_need = 1, 1
+        for l in L:
+            hw, ho = l.hw, (l.hw // 2 if l.pool else l.hw)
+            self.z.append(torch.empty(N, hw, hw, l.cout, **f32))
+            self.a.append(torch.empty(N, ho, ho, l.cout, **f32))
+            self.g.append(torch.empty(N, ho, ho, l.cout, **f32))
+            self.dz.append(torch.empty(N, hw, hw, l.cout, **f32))
+            self.wflip.append(torch.empty(l.cin_pad, 3, 3, l.cout, **f32))
+            self.stats.append({k: torch.zeros(l.cout, **f32) for k in ("mean", "invstd", "scale", "shift")})
+            self.eval_ss.append({k: torch.zeros(l.cout, **f32) for k in ("scale", "shift")})
+            M = N * hw * hw
+            for kind, (m, n, k) in (("fprop", (M, l.cout, 9 * l.cin_pad)), ("dgrad", (M, l.cin_pad, 9 * l.cout)),
+                                    ("wgrad", (M, l.cout, 9 * l.cin_pad))):
+                _, s = conv_cfg("wgrad" if kind == "wgrad" else "fprop", m, n, k)
+                out = m * n if kind != "wgrad" else n * k
+                if s > 1:
+                    slab_need = max(slab_need, s * out)
+            part_need = max(part_need, 3 * ((M + 63) // 64) * l.cout)
+        self.slab = torch.empty(slab_need, **f32)
+        self.part = torch.empty(part_need, **f32)
+        self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
+        self.loss_row = torch.zeros(N, **f32)
+        self.dlogits = torch.zeros(N, num_classes, **f32)
+        self.loss = torch.zeros(1, **f32)
+        self.loss_accum = torch.zeros(1, **f32)
+        self.correct = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.eval_acc = torch.zeros(2, **f32)
+        self._cfg_cache: Dict[tuple, tuple] = {}
+        self._eval_dirty = True
+        self.init_parameters(seed=None)
+
+    # ------------------------------------------------------------------ parameters / state
+    @torch.no_grad()
+    def init_parameters(self, seed: Optional[int] = None, module: Optional[torch.nn.Module] = None):
+        """torch default init of the reference module (seeded like the reference: manual_seed
+        before construction), copied into the arenas."""
+        from .models.vgg import VGG
+
+        if module is None:
+            if seed is not None:
+                torch.manual_seed(seed)
+            module = VGG(self.spec.name, self.num_classes)
+        self.load_state_dict(module.state_dict())
+
+    @torch.no_grad()
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+        seen = set()
+        for l in self.spec.convs:
+            w = sd[f"{l.conv_key}.weight"]  # OIHW
+            dst = self.params[f"{l.conv_key}.weight"]
+            dst.zero_()
+            dst[..., :l.cin].copy_(w.permute(0, 2, 3, 1))
+            for k in (f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"):
+                self.params[k].copy_(sd[k])
+            for b in ("running_mean", "running_var"):
+                self.buffers[f"{l.bn_key}.{b}"].copy_(sd[f"{l.bn_key}.{b}"])
+            self.nbt[self.spec.convs.index(l)] = int(sd.get(f"{l.bn_key}.num_batches_tracked", torch.tensor(0)))
+            seen |= {f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias",
+                     f"{l.bn_key}.running_mean", f"{l.bn_key}.running_var", f"{l.bn_key}.num_batches_tracked"}
+        for k in ("fc1.weight", "fc1.bias"):
+            self.params[k].copy_(sd[k])
+            seen.add(k)
+        if strict:
+            extra = set(sd) - seen
+            if extra:
+                raise KeyError(f"unexpected keys in state_dict: {sorted(extra)[:5]}")
+        self._eval_dirty = True
+
+    @torch.no_grad()
+    def state_dict(self, prefix: str = "") -> "OrderedDict[str, torch.Tensor]":
+        """Reference-layout state_dict (58 keys for VGG-11, OIHW fp32, CPU tensors)."""
+        out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        for i, l in enumerate(self.spec.convs):
+            out[prefix + f"{l.conv_key}.weight"] = (
+                self.params[f"{l.conv_key}.weight"][..., :l.cin].permute(0, 3, 1, 2).contiguous().cpu())
+            out[prefix + f"{l.conv_key}.bias"] = self.params[f"{l.conv_key}.bias"].cpu().clone()
+            out[prefix + f"{l.bn_key}.weight"] = self.params[f"{l.bn_key}.weight"].cpu().clone()
+            out[prefix + f"{l.bn_key}.bias"] = self.params[f"{l.bn_key}.bias"].cpu().clone()
+            out[prefix + f"{l.bn_key}.running_mean"] = self.buffers[f"{l.bn_key}.running_mean"].cpu().clone()
+            out[prefix + f"{l.bn_key}.running_var"] = self.buffers[f"{l.bn_key}.running_var"].cpu().clone()
+            out[prefix + f"{l.bn_key}.num_batches_tracked"] = self.nbt[i].cpu().clone()
+        out[prefix + "fc1.weight"] = self.params["fc1.weight"].cpu().clone()
+        out[prefix + "fc1.bias"] = self.params["fc1.bias"].cpu().clone()
+        return out
+
+    def _to_torch_layout(self, name: str, t: torch.Tensor) -> torch.Tensor:
+        if name.endswith(".weight") and t.dim() == 4:
+            l = next(l for l in self.spec.convs if name == f"{l.conv_key}.weight")
+            return t[..., :l.cin].permute(0, 3, 1, 2).contiguous()
+        return t.clone()
+
+    def _from_torch_layout(self, name: str, t: torch.Tensor, dst: torch.Tensor):
+        if name.endswith(".weight") and dst.dim() == 4:
+            l = next(l for l in self.spec.convs if name == f"{l.conv_key}.weight")
+            dst.zero_()
+            dst[..., :l.cin].copy_(t.permute(0, 2, 3, 1))
+        else:
+            dst.copy_(t)
+
+    @torch.no_grad()
+    def optimizer_state_dict(self) -> dict:
+        """torch.optim.SGD-format state_dict (momentum buffers in OIHW)."""
+        names = self.spec.param_names()
+        state = {}
+        if self.steps_taken > 0:
+            for i, n in enumerate(names):
+                state[i] = {"momentum_buffer": self._to_torch_layout(n, self.mom[n]).cpu()}
+        return {"state": state,
+                "param_groups": [{"lr": self.lr, "momentum": self.momentum, "dampening": 0,
+                                  "weight_decay": self.weight_decay, "nesterov": False, "maximize": False,
+                                  "foreach": None, "differentiable": False, "fused": None,
+                                  "params": list(range(len(names)))}]}
+
+    @torch.no_grad()
+    def load_optimizer_state_dict(self, osd: dict):
+        names = self.spec.param_names()
+        pg = osd["param_groups"][0]
+        self.lr, self.momentum, self.weight_decay = pg["lr"], pg["momentum"], pg["weight_decay"]
+        st = osd.get("state", {})
+        if st:
+            for i, n in enumerate(names):
+                self._from_torch_layout(n, st[i]["momentum_buffer"].to(self.device), self.mom[n])
+            self.steps_taken = max(self.steps_taken, 1)
+        else:
+            self.mom.flat.zero_()
+            self.steps_taken = 0
+
+    def num_parameters(self) -> int:
+        return sum(p.numel() for p in self.state_dict().values() if p.dtype == torch.float32) - sum(
+            self.buffers.numels.values())
+
+    # ------------------------------------------------------------------ kernel configs
+    def _cfg(self, kind, M, N, K):
+        key = (kind, M, N, K)
+        c = self._cfg_cache.get(key)
+        if c is None:
+            c = conv_cfg(kind, M, N, K)
+            self._cfg_cache[key] = c
+        return c
+
+    def _conv(self, x, w, out, l_cin, l_cout, hw, n):
+        M = n * hw * hw
+        tile, s = self._cfg("fprop", M, l_cout, 9 * l_cin)
+        self.K.conv_fprop(x, w, out, self.slab if s > 1 else None, 1, 1, s, tile)
+
+    def _wgrad(self, x, dz, dw, cin, cout, hw, n):
+        M = n * hw * hw
+        tile, s = self._cfg("wgrad", M, cout, 9 * cin)
+        self.K.conv_wgrad(x, dz, dw, self.slab if s > 1 else None, 1, 1, s, tile)
+
+    # ------------------------------------------------------------------ training step
+    def forward_backward(self, x: torch.Tensor, target: torch.Tensor,
+                         grad_ready: Optional[Callable[[List[str]], None]] = None,
+                         pre_forward: Optional[Callable[[], None]] = None) -> torch.Tensor:
+        """One training forward+backward on x [n,H,W,4] (NHWC fp32, 4th channel zero).
+        Gradients land in ``self.grads``; the batch-mean loss in ``self.loss`` (device) and is
+        also accumulated into ``self.loss_accum``.  Returns ``self.loss``."""
+        K, P, G = self.K, self.params, self.grads
+        n = x.shape[0]
+        L = self.spec.convs
+        if pre_forward is not None:
+            pre_forward()
+        inp = x
+        for i, l in enumerate(L):
+            z, a, st = self.z[i][:n], self.a[i][:n], self.stats[i]
+            self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n)
+            K.bn_fwd_stats(z, self.part, P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
+                           self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
+                           self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"], self.bn_momentum,
+                           self.bn_eps)
+            K.bn_apply(z, a, st["scale"], st["shift"], l.pool)
+            inp = a
+        feat = inp.view(n, -1)
+        K.fc_ce_train(feat, P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n], self.dlogits[:n],
+                      self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
+        if grad_ready is not None:
+            grad_ready(["fc1.weight", "fc1.bias"])
+        for i in range(len(L) - 1, -1, -1):
+            l = L[i]
+            st = self.stats[i]
+            z, dz = self.z[i][:n], self.dz[i][:n]
+            K.bn_bwd(self.g[i][:n], z, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
+                     self.part, self.coef, G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"],
+                     dz, l.pool)
+            xin = x if i == 0 else self.a[i - 1][:n]
+            if i > 0:
+                K.wflip(P[f"{l.conv_key}.weight"], self.wflip[i])
+                M = n * l.hw * l.hw
+                tile, s = self._cfg("fprop", M, l.cin_pad, 9 * l.cout)
+                K.conv_fprop(dz, self.wflip[i], self.g[i - 1][:n], self.slab if s > 1 else None, 1, 1, s, tile)
+            self._wgrad(xin, dz, G[f"{l.conv_key}.weight"], l.cin_pad, l.cout, l.hw, n)
+            if grad_ready is not None:
+                grad_ready([f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"])
+        self._eval_dirty = True
+        return self.loss
+
+    def sgd_step(self, grad_scale: float = 1.0, offset: int = 0, count: int = -1):
+        """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
+        self.K.sgd_flat(self.params.flat, self.grads.flat, self.mom.flat, self.lr, self.momentum, self.weight_decay,
+                        grad_scale, self.steps_taken == 0, offset, count)
+
+    def finish_step(self):
+        self.steps_taken += 1
+        self._eval_dirty = True
+
+    # ------------------------------------------------------------------ evaluation
+    def begin_eval(self):
+        for i, l in enumerate(self.spec.convs):
+            self.K.bn_eval_params(self.params[f"{l.bn_key}.weight"], self.params[f"{l.bn_key}.bias"],
+                                  self.params[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
+                                  self.buffers[f"{l.bn_key}.running_var"], self.eval_ss[i]["scale"],
+                                  self.eval_ss[i]["shift"], self.bn_eps)
+        self.eval_acc.zero_()
+        self._eval_dirty = False
+
+    def eval_batch(self, x: torch.Tensor, target: torch.Tensor, logits: Optional[torch.Tensor] = None):
+        """Eval-mode forward (running stats); accumulates [sum of batch-mean losses, #correct]
+        into ``self.eval_acc``."""
+        if self._eval_dirty:
+            raise RuntimeError("call begin_eval() after the last parameter update")
+        n = x.shape[0]
+        P = self.params
+        inp = x
+        for i, l in enumerate(self.spec.convs):
+            z, a = self.z[i][:n], self.a[i][:n]
+            self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n)
+            self.K.bn_apply(z, a, self.eval_ss[i]["scale"], self.eval_ss[i]["shift"], l.pool)
+            inp = a
+        self.K.fc_ce_eval(inp.view(n, -1), P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n],
+                          self.correct[:n], logits, self.eval_acc)
+        return self.eval_acc

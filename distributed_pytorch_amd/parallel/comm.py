@@ -1,0 +1,231 @@
+"""Communicators: the collective layer the gradient-sync strategies run on.
+
+``RcclComm``  — the MI355X path: the native C++ communicator (csrc/runtime/rccl_comm.cpp) straight
+               on RCCL over xGMI, with its own high-priority comm HIP stream.  Bootstrapped by
+               exchanging an ``ncclUniqueId`` through the rendezvous store.
+``TorchComm`` — ``torch.distributed`` (gloo on CPU — the test oracle; nccl=RCCL on GPU for A/B
+               comparison), with a side stream on GPU so collectives overlap compute the same way.
+``NullComm``  — world size 1: every collective is the identity (gather copies).
+
+All share one ordering contract, which is what lets backward overlap communication:
+
+    with comm.region():          # comm stream waits for work queued so far on the compute stream
+        comm.all_reduce(t)       # collectives + any kernels launched here run on the comm stream
+    comm.wait()                  # compute stream waits for everything issued on the comm stream
+
+No host synchronisation happens in any of these calls on GPU.
+"""
+from __future__ import annotations
+
+import contextlib
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    rank: int = 0
+    world: int = 1
+    name = "base"
+
+    @contextlib.contextmanager
+    def region(self):
+        yield
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, root: int = 0):
+        raise NotImplementedError
+
+    def gather(self, send: torch.Tensor, recv: Optional[torch.Tensor], root: int = 0):
+        raise NotImplementedError
+
+    def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, op: str = "sum"):
+        raise NotImplementedError
+
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor):
+        raise NotImplementedError
+
+    def wait(self):
+        pass
+
+    def synchronize(self):
+        pass
+
+    def barrier(self):
+        pass
+
+    def check(self):
+        """Raise if the communicator reported an asynchronous error."""
+
+    def close(self):
+        pass
+
+
+class NullComm(Comm):
+    name = "null"
+
+    def __init__(self):
+        self.rank, self.world = 0, 1
+
+    def all_reduce(self, t, op="sum"):
+        return None
+
+    def broadcast(self, t, root=0):
+        return None
+
+    def gather(self, send, recv, root=0):
+        if recv is not None:
+            recv.view(-1)[: send.numel()].copy_(send.view(-1))
+
+    def reduce_scatter(self, send, recv, op="sum"):
+        recv.copy_(send.view(-1)[: recv.numel()].view_as(recv))
+
+    def all_gather(self, send, recv):
+        recv.view(-1)[: send.numel()].copy_(send.view(-1))
+
+
+_TORCH_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+              "prod": dist.ReduceOp.PRODUCT}
+
+
+class TorchComm(Comm):
+    """torch.distributed process group.  Every op waits on its Work right after issue: on GPU
+    (nccl) that is a device-side wait of the side stream, on CPU (gloo) a host wait."""
+
+    name = "torch"
+
+    def __init__(self, group=None, device: Optional[torch.device] = None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+
+    @contextlib.contextmanager
+    def region(self):
+        if self.side is None:
+            yield
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            yield
+
+    def _w(self, work):
+        if work is not None:
+            work.wait()
+
+    def all_reduce(self, t, op="sum"):
+        if op == "avg":
+            self._w(dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group, async_op=True))
+            t.div_(self.world)
+            return
+        self._w(dist.all_reduce(t, _TORCH_OPS[op], group=self.group, async_op=True))
+
+    def broadcast(self, t, root=0):
+        self._w(dist.broadcast(t, src=root, group=self.group, async_op=True))
+
+    def gather(self, send, recv, root=0):
+        gl = list(recv.view(self.world, -1).unbind(0)) if self.rank == root else None
+        self._w(dist.gather(send.view(-1), gather_list=gl, dst=root, group=self.group, async_op=True))
+
+    def reduce_scatter(self, send, recv, op="sum"):
+        if self.device.type == "cpu":  # gloo has no reduce_scatter: all_reduce a copy, keep own shard
+            tmp = send.clone()
+            self.all_reduce(tmp, op)
+            recv.copy_(tmp.view(self.world, -1)[self.rank].view_as(recv))
+            return
+        self._w(dist.reduce_scatter_tensor(recv, send, _TORCH_OPS[op], group=self.group, async_op=True))
+
+    def all_gather(self, send, recv):
+        self._w(dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True))
+
+    def wait(self):
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+
+    def synchronize(self):
+        if self.side is not None:
+            self.side.synchronize()
+
+    def barrier(self):
+        dist.barrier(group=self.group)
+
+
+class RcclComm(Comm):
+    """Native RCCL communicator (one per process/GPU)."""
+
+    name = "rccl"
+
+    def __init__(self, rank: int, world: int, device: torch.device, store=None, uid: Optional[bytes] = None,
+                 tag: str = "dpa_rccl_uid"):
+        from .. import _ext
+
+        C = _ext.require()
+        self.rank, self.world = rank, world
+        self.device = torch.device(device)
+        if uid is None:
+            if store is None:
+                raise ValueError("RcclComm needs a store (or an explicit unique id) for bootstrap")
+            if rank == 0:
+                uid = C.rccl_unique_id()
+                store.set(tag, uid)
+            else:
+                store.wait([tag], datetime.timedelta(seconds=int(os.environ.get("DPA_RCCL_INIT_TIMEOUT", "600"))))
+                uid = store.get(tag)
+        with torch.cuda.device(self.device):
+            self._c = C.RcclComm(rank, world, bytes(uid), self.device.index or 0)
+        self.stream = torch.cuda.ExternalStream(self._c.stream_ptr(), device=self.device)
+        self._store = store
+
+    @contextlib.contextmanager
+    def region(self):
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            yield
+
+    def all_reduce(self, t, op="sum"):
+        self._c.all_reduce(t, op)
+
+    def broadcast(self, t, root=0):
+        self._c.broadcast(t, root)
+
+    def gather(self, send, recv, root=0):
+        self._c.gather(send, recv, root)
+
+    def reduce_scatter(self, send, recv, op="sum"):
+        self._c.reduce_scatter(send, recv, op)
+
+    def all_gather(self, send, recv):
+        self._c.all_gather(send, recv)
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def synchronize(self):
+        self._c.synchronize()
+
+    def barrier(self):
+        t = torch.zeros(1, device=self.device)
+        with self.region():
+            self.all_reduce(t)
+        self.wait()
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def check(self):
+        err = self._c.async_error()
+        if err:
+            raise RuntimeError(f"RCCL async error on rank {self.rank}: {err}")
+
+    def close(self):
+        try:
+            self._c.synchronize()
+        except Exception:
+            self._c.abort()
+
+    def abort(self):
+        self._c.abort()

@@ -1,0 +1,228 @@
+"""Gradient-synchronisation strategies — the reference's three DP modes, MI355X-first.
+
+  mode "gather"    (main_gather.py:42-59)     grads → rank 0 (grouped send/recv into a W×n
+                   buffer), mean-of-W kernel on rank 0, broadcast back (== scattering W copies).
+  mode "allreduce" (main_all_reduce.py:45-48) all_reduce(SUM) per tensor, /W fused into SGD.
+  mode "ddp"       (main_ddp.py:137)          DDP semantics: initial broadcast of params+buffers
+                   from rank 0, BN buffers broadcast before every training forward, bucketed
+                   all_reduce(SUM) overlapped with backward, /W fused into SGD.
+
+Differences from the reference, all by design:
+* every mode works on contiguous slices of the flat grad arena (no per-step allocation, no
+  stack/copy), and by default issues each bucket's collective on the comm stream as soon as the
+  static backward schedule reports its layer done (``overlap=True``); ``overlap=False`` defers
+  all collectives to after backward (the reference's blocking placement, for A/B comparison);
+* buckets are cut at layer boundaries with an xGMI-sized cap (``bucket_mb``, default 10 MiB: the
+  three 9 MiB [512,512,3,3] weights each get a bucket; the last-ready bucket is kept small so the
+  exposed tail after backward is short) instead of DDP's 25 MiB/1 MiB;
+* all modes broadcast rank 0's parameters and buffers once at start, so replicas
+  cannot silently fork.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from .comm import Comm
+
+
+class Bucket:
+    __slots__ = ("names", "lo", "hi", "pending", "issued")
+
+    def __init__(self, names: List[str], lo: int, hi: int):
+        self.names = list(names)
+        self.lo, self.hi = lo, hi
+        self.pending = set(names)
+        self.issued = False
+
+    @property
+    def numel(self):
+        return self.hi - self.lo
+
+
+def plan_buckets(arena, ready_order: List[List[str]], bucket_mb: float, tail_mb: float = 2.0) -> List[Bucket]:
+    """Greedy layer-aligned buckets in gradient-ready order.  ``bucket_mb <= 0`` → one bucket
+    per tensor (the reference's per-parameter granularity)."""
+    if bucket_mb <= 0:
+        out = []
+        for group in ready_order:
+            for n in group:
+                lo, hi = arena.span([n])
+                out.append(Bucket([n], lo, hi))
+        return out
+    cap = bucket_mb * (1 << 20) / 4
+    tail = tail_mb * (1 << 20) / 4
+    groups = [(g, arena.span(g)) for g in ready_order]
+    # the trailing (last-ready) groups form a small tail bucket
+    tail_groups = []
+    acc = 0
+    while groups and acc + (groups[-1][1][1] - groups[-1][1][0]) <= tail and len(groups) > 1:
+        g = groups.pop()
+        acc += g[1][1] - g[1][0]
+        tail_groups.insert(0, g)
+    buckets, cur, cur_n = [], [], 0
+    for g, (lo, hi) in groups:
+        n = hi - lo
+        if cur and cur_n + n > cap:
+            buckets.append(cur)
+            cur, cur_n = [], 0
+        cur.append((g, (lo, hi)))
+        cur_n += n
+    if cur:
+        buckets.append(cur)
+    if tail_groups:
+        buckets.append(tail_groups)
+    out = []
+    for b in buckets:
+        names = [n for g, _ in b for n in g]
+        lo, hi = arena.span(names)
+        out.append(Bucket(names, lo, hi))
+    # sanity: buckets must tile contiguous, non-overlapping ranges
+    rng = sorted((b.lo, b.hi) for b in out)
+    for (a0, a1), (b0, b1) in zip(rng, rng[1:]):
+        assert a1 <= b0, "bucket ranges overlap"
+    return out
+
+
+class GradSync:
+    mode = "none"
+
+    def __init__(self, engine, comm: Comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
+        self.engine = engine
+        self.comm = comm
+        self.world = comm.world
+        self.overlap = overlap
+        order = [["fc1.weight", "fc1.bias"]] + [
+            [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
+            for l in reversed(engine.spec.convs)]
+        self.buckets = plan_buckets(engine.grads, order, bucket_mb)
+        self._by_name: Dict[str, Bucket] = {n: b for b in self.buckets for n in b.names}
+        self.issued_bytes = 0
+        if broadcast_init and self.world > 1:
+            self.broadcast_state()
+
+    # -- state broadcast (DDP ctor semantics; torch distributed.py:862-871) --
+    def broadcast_state(self):
+        e = self.engine
+        with self.comm.region():
+            self.comm.broadcast(e.params.flat, 0)
+            self.comm.broadcast(e.buffers.flat, 0)
+            self.comm.broadcast(e.nbt, 0)
+            if e.steps_taken > 0:
+                self.comm.broadcast(e.mom.flat, 0)
+        self.comm.wait()
+
+    def pre_forward(self):
+        pass
+
+    def begin_step(self):
+        for b in self.buckets:
+            b.pending = set(b.names)
+            b.issued = False
+
+    def grad_ready(self, names: List[str]):
+        if self.world == 1:
+            return
+        for n in names:
+            b = self._by_name.get(n)
+            if b is None:
+                continue
+            b.pending.discard(n)
+            if not b.pending and self.overlap and not b.issued:
+                self._issue(b)
+
+    def _issue(self, b: Bucket):
+        b.issued = True
+        self.issued_bytes += 4 * b.numel
+        with self.comm.region():
+            self.reduce_bucket(b)
+
+    def reduce_bucket(self, b: Bucket):
+        raise NotImplementedError
+
+    def finish(self) -> float:
+        """Issue whatever is left, make the compute stream wait for the comm stream, and return
+        the scale the optimizer must apply to the synced grads."""
+        if self.world == 1:
+            return 1.0
+        for b in self.buckets:
+            if not b.issued:
+                self._issue(b)
+        self.comm.wait()
+        return self.grad_scale()
+
+    def grad_scale(self) -> float:
+        return 1.0
+
+
+class GatherScatterSync(GradSync):
+    """Mode A: gather → mean on rank 0 → broadcast (main_gather.py:42-59)."""
+
+    mode = "gather"
+
+    def __init__(self, engine, comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
+        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
+        self._recv = None
+        if comm.rank == 0 and comm.world > 1:
+            mx = max(b.numel for b in self.buckets)
+            self._recv = torch.empty(comm.world * mx, device=engine.device, dtype=torch.float32)
+
+    def reduce_bucket(self, b: Bucket):
+        g = self.engine.grads.flat[b.lo:b.hi]
+        recv = self._recv[: self.world * b.numel] if self._recv is not None else None
+        self.comm.gather(g, recv, 0)
+        if self.comm.rank == 0:
+            self.engine.K.mean_of_w(recv, g, self.world)
+        self.comm.broadcast(g, 0)
+
+
+class AllReduceSync(GradSync):
+    """Mode B: per-tensor all_reduce(SUM), then grad /= W (fused into SGD)."""
+
+    mode = "allreduce"
+
+    def reduce_bucket(self, b: Bucket):
+        self.comm.all_reduce(self.engine.grads.flat[b.lo:b.hi], "sum")
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+
+class DDPSync(GradSync):
+    """Mode C: DistributedDataParallel semantics on RCCL."""
+
+    mode = "ddp"
+
+    def __init__(self, engine, comm, bucket_mb: float = 10.0, overlap: bool = True, broadcast_init: bool = True,
+                 broadcast_buffers: bool = True):
+        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
+        self.broadcast_buffers = broadcast_buffers
+
+    def pre_forward(self):
+        # DDP._sync_buffers: rank 0's BN running stats/counters overwrite every replica's before
+        # each training forward (torch nn/parallel/distributed.py:2178).
+        if self.world == 1 or not self.broadcast_buffers:
+            return
+        e = self.engine
+        with self.comm.region():
+            self.comm.broadcast(e.buffers.flat, 0)
+            self.comm.broadcast(e.nbt, 0)
+        self.comm.wait()
+
+    def reduce_bucket(self, b: Bucket):
+        self.comm.all_reduce(self.engine.grads.flat[b.lo:b.hi], "sum")
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+
+MODES = {"gather": GatherScatterSync, "allreduce": AllReduceSync, "ddp": DDPSync}
+DEFAULT_BUCKET_MB = {"gather": 0.0, "allreduce": 0.0, "ddp": 10.0}
+
+
+def make_sync(mode: str, engine, comm: Comm, bucket_mb: Optional[float] = None, overlap: bool = True,
+              broadcast_init: bool = True) -> GradSync:
+    cls = MODES[mode]
+    bmb = DEFAULT_BUCKET_MB[mode] if bucket_mb is None else bucket_mb
+    return cls(engine, comm, bmb, overlap, broadcast_init)

@@ -1,0 +1,212 @@
+"""Training / evaluation loop and the shared CLI behind every entry point.
+
+Mirrors the reference's observable behaviour (main.py:19-66):
+  * ``Epoch: {e}, Iteration: {a}-{b}, Average Loss: {x:.3f}`` every 20 iterations;
+  * ``Avg Time for iteration 2-40: {t} seconds.`` then every 40 (iteration 0 excluded, first
+    window ÷39);
+  * ``Test set: Average loss: {:.4f}, Accuracy: {}/{} ({:.0f}%)`` over the full, unsharded test
+    set on every rank;
+  * every rank prints; seed 1 before model construction; sampler seed 0; batch 256 per rank;
+    SGD(lr 0.1, momentum 0.9, wd 1e-4); 1 epoch.
+Timing is device-accurate: the clock is read after a device synchronize at each window boundary
+(the reference's ``loss.item()`` forced the same synchronisation every step).
+Extra (new scope): images/sec, JSON metrics, per-rank checkpoints + resume, roctx tracing, RCCL
+async-error polling.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from typing import Optional
+
+import torch
+
+from .data import DeviceLoader, ShardSampler, get_datasets
+from .engine import VGGEngine
+from .parallel import DistContext, env_dict, init_cli, init_env, init_single, make_sync
+from .utils import checkpoint
+from .utils.profiling import enable_tracing, trace_range
+
+BATCH_SIZE = 256  # main.py:18 ("batch for one node")
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: DistContext, args,
+                start_batch: int = 0, stats: Optional[dict] = None):
+    dev = engine.device
+    engine.loss_accum.zero_()
+    t_win, win_start = None, None
+    n_iters = 0
+    t_epoch0 = None
+    max_iters = getattr(args, "max_iters", None)
+    ck_every = getattr(args, "checkpoint_every", 0) or 0
+    for batch_idx, (x, target) in enumerate(loader.iterate(start_batch), start=start_batch):
+        with trace_range("step"):
+            sync.begin_step()
+            with trace_range("fwd_bwd"):
+                engine.forward_backward(x, target, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+            with trace_range("sync"):
+                gscale = sync.finish()
+            with trace_range("sgd"):
+                engine.sgd_step(gscale)
+            engine.finish_step()
+        n_iters += 1
+        if batch_idx == start_batch:
+            _sync(dev)
+            t_win = time.perf_counter()
+            t_epoch0 = t_win
+            win_start = batch_idx
+        if batch_idx % 20 == 19:
+            running = float(engine.loss_accum.item())
+            engine.loss_accum.zero_()
+            print(f"Epoch: {epoch + 1}, Iteration: {batch_idx - 18}-{batch_idx + 1}, Average Loss: {running / 20:.3f}",
+                  flush=True)
+        if batch_idx % 40 == 39:
+            _sync(dev)
+            now = time.perf_counter()
+            if batch_idx == 39:
+                print(f"Avg Time for iteration {batch_idx - 37}-{batch_idx + 1}: {(now - t_win) / 39} seconds.",
+                      flush=True)
+            else:
+                print(f"Avg Time for iteration {batch_idx - 38}-{batch_idx + 1}: {(now - t_win) / 40} seconds.",
+                      flush=True)
+            t_win = now
+            ctx.comm.check()
+        if ck_every and args.checkpoint_dir and (batch_idx + 1) % ck_every == 0:
+            checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch, batch_idx + 1, args.sampler_seed, ctx.world,
+                            sync.mode, ddp_prefix=sync.mode == "ddp")
+        if max_iters and n_iters >= max_iters:
+            break
+    _sync(dev)
+    if stats is not None and t_epoch0 is not None and n_iters > 1:
+        el = time.perf_counter() - t_epoch0
+        stats["iters_timed"] = n_iters - 1
+        stats["sec_per_iter"] = el / (n_iters - 1)
+        stats["images_per_sec_rank"] = loader.batch_size / stats["sec_per_iter"]
+        stats["images_per_sec_total"] = stats["images_per_sec_rank"] * ctx.world
+    return None
+
+
+def test_model(engine: VGGEngine, loader: DeviceLoader, sync=None):
+    if sync is not None and sync.mode == "ddp":
+        sync.pre_forward()  # first eval forward under DDP still broadcasts rank 0's buffers
+    engine.begin_eval()
+    nb = 0
+    for x, target in loader:
+        engine.eval_batch(x, target)
+        nb += 1
+    acc = engine.eval_acc.cpu()
+    test_loss = float(acc[0]) / max(nb, 1)
+    correct = int(round(float(acc[1])))
+    n = loader.dataset_len
+    print("Test set: Average loss: {:.4f}, Accuracy: {}/{} ({:.0f}%)\n".format(test_loss, correct, n,
+                                                                              100.0 * correct / n), flush=True)
+    return test_loss, correct
+
+
+def add_common_args(ap: argparse.ArgumentParser):
+    g = ap.add_argument_group("framework options (defaults = reference values)")
+    g.add_argument("--model", default="VGG11", choices=["VGG11", "VGG13", "VGG16", "VGG19"])
+    g.add_argument("--epochs", type=int, default=1)
+    g.add_argument("--batch-size", type=int, default=BATCH_SIZE, help="per-rank batch")
+    g.add_argument("--lr", type=float, default=0.1)
+    g.add_argument("--momentum", type=float, default=0.9)
+    g.add_argument("--weight-decay", type=float, default=1e-4)
+    g.add_argument("--seed", type=int, default=1)
+    g.add_argument("--sampler-seed", type=int, default=0)
+    g.add_argument("--data-root", default="./data")
+    g.add_argument("--synthetic", action="store_true", help="synthetic CIFAR-shaped data (default if no dataset)")
+    g.add_argument("--train-size", type=int, default=50000)
+    g.add_argument("--test-size", type=int, default=10000)
+    g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    g.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    g.add_argument("--bucket-mb", type=float, default=None)
+    g.add_argument("--no-overlap", action="store_true", help="sync after backward (reference placement)")
+    g.add_argument("--checkpoint-dir", default=None)
+    g.add_argument("--checkpoint-every", type=int, default=0)
+    g.add_argument("--resume", action="store_true")
+    g.add_argument("--max-iters", type=int, default=None, help="stop each epoch after this many iterations")
+    g.add_argument("--no-eval", action="store_true")
+    g.add_argument("--trace", action="store_true", help="emit roctx ranges (rocprofv3 --marker-trace)")
+    g.add_argument("--json-metrics", default=None, help="append a JSON metrics line per epoch to this file")
+    g.add_argument("--port", type=int, default=6585)
+    return ap
+
+
+def run(ctx: DistContext, mode: str, args):
+    if args.trace:
+        enable_tracing(True)
+    torch.manual_seed(args.seed)  # main.py:70 — identical init on all ranks (plus a rank-0 broadcast)
+    train_set, test_set = get_datasets(args.data_root, args.synthetic, args.train_size, args.test_size)
+    sampler = ShardSampler(len(train_set), num_replicas=ctx.world, rank=ctx.rank, shuffle=True,
+                           seed=args.sampler_seed, drop_last=False)
+    train_loader = DeviceLoader(train_set, args.batch_size, ctx.device, sampler=sampler, train=True,
+                                seed=args.seed * 7919 + ctx.rank)
+    test_loader = DeviceLoader(test_set, args.batch_size, ctx.device, sampler=None, train=False)
+    engine = VGGEngine(args.model, ctx.device, max_batch=args.batch_size, lr=args.lr, momentum=args.momentum,
+                       weight_decay=args.weight_decay)
+    engine.init_parameters(seed=args.seed)
+    start_epoch, start_batch = 0, 0
+    if args.resume and args.checkpoint_dir:
+        obj = checkpoint.load(args.checkpoint_dir, ctx.rank, engine)
+        if obj is not None:
+            start_epoch, start_batch = obj["epoch"], obj["batch_idx"]
+            if start_batch >= len(train_loader):
+                start_epoch, start_batch = start_epoch + 1, 0
+    sync = make_sync(mode, engine, ctx.comm, bucket_mb=args.bucket_mb, overlap=not args.no_overlap)
+    for epoch in range(start_epoch, args.epochs):
+        train_loader.set_epoch(epoch)
+        stats = {}
+        train_model(engine, train_loader, sync, epoch, ctx, args, start_batch=start_batch, stats=stats)
+        start_batch = 0
+        if args.checkpoint_dir:
+            checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch + 1, 0, args.sampler_seed, ctx.world, mode,
+                            ddp_prefix=mode == "ddp")
+        res = None
+        if not args.no_eval:
+            res = test_model(engine, test_loader, sync)
+        if args.json_metrics and ctx.rank == 0:
+            rec = dict(stats, epoch=epoch + 1, mode=mode, world=ctx.world, model=args.model,
+                       batch_per_rank=args.batch_size)
+            if res:
+                rec["test_loss"], rec["test_correct"] = res
+            with open(args.json_metrics, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+    ctx.shutdown()
+
+
+def main_cli(mode: str, argv=None):
+    """``python main_{gather,all_reduce,part3}.py --master-ip IP --num-nodes N --rank R``"""
+    ap = argparse.ArgumentParser(prog="Input arguments", description="gather ip, nunber of workers, rank")
+    ap.add_argument("--master-ip", required=True)
+    ap.add_argument("--num-nodes", required=True, type=int)
+    ap.add_argument("--rank", required=True, type=int)
+    add_common_args(ap)
+    args = ap.parse_args(argv)
+    ctx = init_cli(args.master_ip, args.num_nodes, args.rank, port=args.port, device=args.device, comm=args.comm)
+    run(ctx, mode, args)
+
+
+def main_env(mode: str = "ddp", argv=None):
+    """``torchrun ... main_ddp.py`` (env:// rendezvous)."""
+    ap = argparse.ArgumentParser(prog="Input arguments", description="gather ip, nunber of workers, rank")
+    add_common_args(ap)
+    args = ap.parse_args(argv)
+    print(f"[{os.getpid()}] Initializing process group with: {env_dict()}", flush=True)
+    ctx = init_env(device=args.device, comm=args.comm)
+    run(ctx, mode, args)
+
+
+def main_single(argv=None):
+    """``python main.py`` — single process, no distribution (main.py:69-108)."""
+    ap = argparse.ArgumentParser(prog="main.py")
+    add_common_args(ap)
+    args = ap.parse_args(argv)
+    ctx = init_single(args.device)
+    run(ctx, "allreduce", args)

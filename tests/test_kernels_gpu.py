@@ -1,0 +1,97 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32/fp64 reference of the same op.
+
+Shapes: the VGG-11 layer shapes of SURVEY §2.3 (with a reduced batch so the fp64 CPU
+reference stays cheap) plus odd shapes exercising masking / split-K / tails.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from distributed_pytorch_amd import _ext
+
+    return _ext.require()
+
+
+def rel_err(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+CONV_SHAPES = [
+    # N, H, W, C, K, R, stride, pad
+    (8, 32, 32, 4, 64, 3, 1, 1),
+    (8, 16, 16, 64, 128, 3, 1, 1),
+    (4, 8, 8, 128, 256, 3, 1, 1),
+    (4, 4, 4, 256, 512, 3, 1, 1),
+    (16, 2, 2, 512, 512, 3, 1, 1),
+    (3, 7, 5, 12, 20, 3, 1, 1),
+    (2, 9, 9, 8, 16, 3, 2, 1),
+    (2, 8, 8, 16, 32, 1, 1, 0),
+    (2, 14, 14, 4, 16, 7, 2, 3),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("tile", [0, 1])
+def test_conv_fprop(shape, splits, tile):
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(K, Cin, R, R, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), stride=st, padding=pd)  # N K P Q
+    xd = x.permute(0, 2, 3, 1).contiguous().cuda()
+    wd = w.permute(0, 2, 3, 1).contiguous().cuda()
+    P, Q = ref.shape[2], ref.shape[3]
+    out = torch.empty(N, P, Q, K, device="cuda")
+    slab = torch.empty(splits * N * P * Q * K, device="cuda") if splits > 1 else None
+    C.conv_fprop(xd, wd, out, slab, st, pd, splits, tile)
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-5
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("splits", [1, 7])
+@pytest.mark.parametrize("tile", [0, 1])
+def test_conv_wgrad(shape, splits, tile):
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64, requires_grad=False)
+    w = (torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1).requires_grad_(True)
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gw,) = torch.autograd.grad(y, w, dy)
+    xd = x.float().permute(0, 2, 3, 1).contiguous().cuda()
+    dzd = dy.float().permute(0, 2, 3, 1).contiguous().cuda()
+    dw = torch.empty(K, R, R, Cin, device="cuda")
+    slab = torch.empty(splits * K * R * R * Cin, device="cuda") if splits > 1 else None
+    C.conv_wgrad(xd, dzd, dw, slab, st, pd, splits, tile)
+    torch.cuda.synchronize()
+    assert rel_err(dw.permute(0, 3, 1, 2), gw) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [s for s in CONV_SHAPES if s[6] == 1 and 2 * s[7] == s[5] - 1])
+def test_conv_dgrad_via_flip(shape):
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(True)
+    w = torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, dy)
+    wk = w.float().permute(0, 2, 3, 1).contiguous().cuda()
+    wflip = torch.empty(Cin, R, R, K, device="cuda")
+    C.wflip(wk, wflip)
+    dzd = dy.float().permute(0, 2, 3, 1).contiguous().cuda()
+    dx = torch.empty(N, H, W, Cin, device="cuda")
+    C.conv_fprop(dzd, wflip, dx, None, 1, pd, 1, 0)
+    torch.cuda.synchronize()
+    assert rel_err(dx.permute(0, 3, 1, 2), gx) < 1e-5
