@@ -1,0 +1,106 @@
+"""Worker functions for the multi-process (gloo, CPU) tests.  Spawned processes import this
+module by name, so it must stay importable (tests/ is on sys.path in the children)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+
+
+def _batches(rank, steps, n=4, seed=100):
+    g = torch.Generator().manual_seed(seed + rank)
+    out = []
+    for _ in range(steps):
+        x = torch.randn(n, 3, 32, 32, generator=g)
+        t = torch.randint(0, 10, (n,), generator=g)
+        out.append((x, t))
+    return out
+
+
+def _x4(x):
+    x4 = torch.zeros(x.shape[0], 32, 32, 4)
+    x4[..., :3] = x.permute(0, 2, 3, 1)
+    return x4
+
+
+def run_engine_mode(rank, world, port, mode, steps, outdir, bucket_mb=None, overlap=True, lr=0.01):
+    from distributed_pytorch_amd.engine import VGGEngine
+    from distributed_pytorch_amd.parallel import TorchComm, make_sync
+
+    _init(rank, world, port)
+    comm = TorchComm(device=torch.device("cpu"))
+    # deliberately different init on rank 1: the start-up broadcast must make replicas identical
+    e = VGGEngine("VGG11", "cpu", max_batch=4, lr=lr)
+    e.init_parameters(seed=1 + rank)
+    sync = make_sync(mode, e, comm, bucket_mb=bucket_mb, overlap=overlap)
+    losses = []
+    for x, t in _batches(rank, steps):
+        sync.begin_step()
+        e.forward_backward(_x4(x), t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+        gs = sync.finish()
+        e.sgd_step(gs)
+        e.finish_step()
+        losses.append(float(e.loss.item()))
+    if mode == "ddp":
+        sync.pre_forward()  # what the first eval forward does
+    torch.save({"params": e.params.flat.clone(), "buffers": e.buffers.flat.clone(), "losses": losses,
+                "sd": e.state_dict()}, os.path.join(outdir, f"{mode}_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_torch_ddp(rank, world, port, steps, outdir, lr=0.01):
+    """Oracle: stock torch DistributedDataParallel on the reference module (main_ddp.py:137)."""
+    from torch.nn.parallel import DistributedDataParallel
+
+    from distributed_pytorch_amd.models import VGG11
+
+    _init(rank, world, port)
+    torch.manual_seed(1)
+    m = DistributedDataParallel(VGG11())
+    opt = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+    losses = []
+    for x, t in _batches(rank, steps):
+        opt.zero_grad()
+        loss = F.cross_entropy(m(x), t)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.item()))
+    m.eval()
+    with torch.no_grad():
+        m(torch.zeros(1, 3, 32, 32))  # first eval forward broadcasts rank 0's buffers
+    torch.save({"sd": m.module.state_dict(), "losses": losses}, os.path.join(outdir, f"torchddp_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_cli_main(rank, world, port, script, args, outfile):
+    """Run one of the CLI entry points in-process (rank from the reference-style CLI flags)."""
+    import contextlib
+    import io
+    import runpy
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    torch.set_num_threads(1)
+    sys.argv = [script, "--master-ip", "127.0.0.1", "--num-nodes", str(world), "--rank", str(rank), "--port",
+                str(port)] + list(args)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        runpy.run_path(os.path.join(root, script), run_name="__main__")
+    with open(outfile, "w") as f:
+        f.write(buf.getvalue())

@@ -1,0 +1,110 @@
+"""Multi-process data-parallel tests on CPU (gloo, world_size 2) — the SURVEY §4 oracle:
+all three sync modes must leave identical parameters on every rank, agree with each other, and
+agree with stock torch DistributedDataParallel on the reference module."""
+import os
+import re
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import dist_helpers as H
+
+WORLD = 2
+STEPS = 3
+
+
+def _spawn(fn, *args):
+    port = H.free_port()
+    mp.start_processes(fn, args=(WORLD, port) + args, nprocs=WORLD, join=True, start_method="spawn")
+
+
+@pytest.fixture(scope="module")
+def mode_results(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("modes"))
+    for mode in ("gather", "allreduce", "ddp"):
+        _spawn(H.run_engine_mode, mode, STEPS, d)
+    _spawn(H.run_torch_ddp, STEPS, d)
+    out = {}
+    for name in ("gather", "allreduce", "ddp", "torchddp"):
+        out[name] = [torch.load(os.path.join(d, f"{name}_{r}.pt"), weights_only=True) for r in range(WORLD)]
+    return out
+
+
+@pytest.mark.parametrize("mode", ["gather", "allreduce", "ddp"])
+def test_replicas_identical(mode_results, mode):
+    r0, r1 = mode_results[mode]
+    assert torch.equal(r0["params"], r1["params"]), f"{mode}: parameters diverged across ranks"
+
+
+def test_modes_agree(mode_results):
+    a = mode_results["gather"][0]["params"]
+    for m in ("allreduce", "ddp"):
+        b = mode_results[m][0]["params"]
+        assert (a - b).abs().max().item() < 1e-5 * max(1.0, a.abs().max().item()), m
+    # per-rank losses identical across modes (same data, same params each step)
+    for r in range(WORLD):
+        la = mode_results["gather"][r]["losses"]
+        for m in ("allreduce", "ddp"):
+            lb = mode_results[m][r]["losses"]
+            assert all(abs(x - y) < 1e-4 for x, y in zip(la, lb))
+
+
+def test_ddp_matches_torch_ddp(mode_results):
+    ours = mode_results["ddp"][0]["sd"]
+    ref = mode_results["torchddp"][0]["sd"]
+    for k, v in ref.items():
+        if v.is_floating_point():
+            d = (ours[k].double() - v.double()).abs().max().item()
+            assert d < 5e-4 * max(1.0, v.abs().max().item()), (k, d)
+        else:
+            assert int(ours[k]) == int(v)
+    lo = mode_results["ddp"][0]["losses"]
+    lr = mode_results["torchddp"][0]["losses"]
+    assert all(abs(x - y) < 1e-3 for x, y in zip(lo, lr)), (lo, lr)
+
+
+def test_ddp_eval_buffers_from_rank0(mode_results):
+    # DDP semantics: the first eval forward broadcasts rank 0's BN buffers
+    b0, b1 = mode_results["ddp"][0]["buffers"], mode_results["ddp"][1]["buffers"]
+    assert torch.equal(b0, b1)
+    # modes A/B keep per-rank BN statistics
+    g0, g1 = mode_results["allreduce"][0]["buffers"], mode_results["allreduce"][1]["buffers"]
+    assert not torch.equal(g0, g1)
+
+
+def test_overlap_and_bucketing_do_not_change_results(tmp_path):
+    d = str(tmp_path)
+    _spawn(H.run_engine_mode, "ddp", 2, d, 1.0, False)
+    a = torch.load(os.path.join(d, "ddp_0.pt"), weights_only=True)["params"]
+    _spawn(H.run_engine_mode, "ddp", 2, d, 0.0, True)
+    b = torch.load(os.path.join(d, "ddp_0.pt"), weights_only=True)["params"]
+    assert torch.equal(a, b)
+
+
+LOSS_RE = re.compile(r"^Epoch: 1, Iteration: (\d+)-(\d+), Average Loss: \d+\.\d{3}$")
+TIME_RE = re.compile(r"^Avg Time for iteration (\d+)-(\d+): [0-9.e-]+ seconds\.$")
+TEST_RE = re.compile(r"^Test set: Average loss: \d+\.\d{4}, Accuracy: \d+/(\d+) \(\d+%\)$")
+
+
+@pytest.mark.parametrize("script", ["main_gather.py", "main_all_reduce.py", "main_part3.py"])
+def test_cli_entrypoints_log_format(tmp_path, script):
+    args = ["--device", "cpu", "--synthetic", "--batch-size", "8", "--max-iters", "41", "--train-size", "2000",
+            "--test-size", "40"]
+    outs = [str(tmp_path / f"out{r}.txt") for r in range(WORLD)]
+    port = H.free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=H.run_cli_main, args=(r, WORLD, port, script, args, outs[r])) for r in range(WORLD)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(600)
+        assert p.exitcode == 0
+    for o in outs:
+        lines = [l for l in open(o).read().splitlines() if l.strip()]
+        loss_lines = [l for l in lines if l.startswith("Epoch:")]
+        time_lines = [l for l in lines if l.startswith("Avg Time")]
+        test_lines = [l for l in lines if l.startswith("Test set:")]
+        assert [LOSS_RE.match(l).groups() for l in loss_lines] == [("1", "20"), ("21", "40")]
+        assert [TIME_RE.match(l).groups() for l in time_lines] == [("2", "40")]
+        assert len(test_lines) == 1 and TEST_RE.match(test_lines[0]).group(1) == "40"

@@ -104,7 +104,8 @@ def test_bn_backward_matches_torch_autograd():
     mean = z.reshape(-1, C).mean(0)
     invstd = torch.rsqrt(z.reshape(-1, C).var(0, unbiased=False) + 1e-5)
     gamma, beta = bn.weight.detach().float(), bn.bias.detach().float()
-    scale, shift = gamma * invstd, beta - mean * scale
+    scale = gamma * invstd
+    shift = beta - mean * scale
     d = lambda t: t.contiguous().cuda()
     out = [torch.zeros(C, device="cuda") for _ in range(3)]
     dz = torch.empty(z.shape, device="cuda")
