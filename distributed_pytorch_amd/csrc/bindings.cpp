@@ -12,21 +12,22 @@ int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float m
 int dpa_scale(float* x, long n, float sc, hipStream_t s);
 int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
-                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st);
+                   int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, hipStream_t st);
+int dpa_conv_splits(int Ktot, int splits);
 int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int N, int H, int W, int C, int Kout,
                    int R, int S, int stride, int pad, int splits, int tile, hipStream_t st);
 int dpa_wflip(const float* w, float* wd, int K, int R, int S, int C, hipStream_t st);
-int dpa_bn_nchunks(int M);
-int dpa_bn_fwd_stats(const float* z, float* part, int M, int C, const float* gamma, const float* beta,
-                     const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
-                     float* scale, float* shift, float momentum, float eps, hipStream_t st);
+long dpa_bn_part_floats(int M, int C, int bwd);
+int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M, int C, const float* gamma,
+                     const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
+                     float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
                        const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st);
 int dpa_bn_apply(const float* z, float* a, const float* scale, const float* shift, int N, int H, int W, int C,
                  int pool, hipStream_t st);
-int dpa_bn_bwd(const float* g, const float* z, const float* scale, const float* shift, const float* mean,
-               const float* invstd, const float* gamma, float* part, float* coef, float* dgamma, float* dbeta,
-               float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st);
+int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
+               const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
+               float* dbeta, float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st);
@@ -84,28 +85,38 @@ void mean_of_w(Tensor in, Tensor out, int64_t W) {
 }
 
 // ---------------- convolution ----------------
-// x [N,H,W,C], w [K,R,S,C], out [N,P,Q,K]
-void conv_fprop(Tensor x, Tensor w, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile) {
+// x [N,H,W,C], w [K,R,S,C] (dgrad: the original conv's weights [C,R,S,K]), out [N,P,Q,K]
+void conv_fprop(Tensor x, Tensor w, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile,
+                bool dgrad, bool reduce) {
   need(x, "x");
   need(w, "w");
   need(out, "out");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "conv_fprop: 4-d NHWC/KRSC tensors expected");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  const int K = w.size(0), R = w.size(1), S = w.size(2);
-  TORCH_CHECK(w.size(3) == C, "conv_fprop: channel mismatch");
+  int K, R, S;
+  if (dgrad) {
+    K = w.size(3), R = w.size(1), S = w.size(2);
+    TORCH_CHECK(w.size(0) == C, "conv_fprop(dgrad): weight [C,R,S,K] expected");
+  } else {
+    K = w.size(0), R = w.size(1), S = w.size(2);
+    TORCH_CHECK(w.size(3) == C, "conv_fprop: channel mismatch");
+  }
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   TORCH_CHECK(out.size(0) == N && out.size(1) == P && out.size(2) == Q && out.size(3) == K, "conv_fprop: out shape");
   float* sl = nullptr;
-  if (splits > 1) {
-    TORCH_CHECK(slab.has_value(), "conv_fprop: split-K needs a slab workspace");
+  const int eff = dpa_conv_splits(R * S * C, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_fprop: split-K needs a slab workspace");
     need(*slab, "slab");
-    TORCH_CHECK(slab->numel() >= splits * (int64_t)N * P * Q * K, "conv_fprop: slab too small");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * P * Q * K, "conv_fprop: slab too small");
     sl = fp(*slab);
   }
   chk(dpa_conv_fprop(fp(x), fp(w), fp(out), sl, N, H, W, C, K, R, S, (int)stride, (int)pad, (int)splits, (int)tile,
-                     cur_stream()),
+                     dgrad ? 1 : 0, reduce ? 1 : 0, cur_stream()),
       "conv_fprop");
 }
+
+int64_t conv_splits(int64_t Ktot, int64_t splits) { return dpa_conv_splits((int)Ktot, (int)splits); }
 
 // x [N,H,W,C], dz [N,P,Q,K], dw [K,R,S,C]
 void conv_wgrad(Tensor x, Tensor dz, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile) {
@@ -138,22 +149,27 @@ void wflip(Tensor w, Tensor wd) {
 }
 
 // ---------------- batch norm ----------------
-int64_t bn_nchunks(int64_t M) { return dpa_bn_nchunks((int)M); }
+int64_t bn_part_floats(int64_t M, int64_t C, bool bwd) { return dpa_bn_part_floats((int)M, (int)C, bwd ? 1 : 0); }
 
-void bn_fwd_stats(Tensor z, Tensor part, Tensor gamma, Tensor beta, OptT bias, OptT rmean, OptT rvar, OptT nbt,
-                  Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum, double eps) {
+// src: z [M][C], or nsplit slabs of it (then the summed z is written to z)
+void bn_fwd_stats(Tensor src, int64_t nsplit, Tensor z, Tensor part, Tensor gamma, Tensor beta, OptT bias, OptT rmean,
+                  OptT rvar, OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum,
+                  double eps) {
+  need(src, "src");
   need(z, "z");
   need(part, "part");
   const int C = z.size(-1);
   const int M = z.numel() / C;
-  TORCH_CHECK(part.numel() >= 2L * dpa_bn_nchunks(M) * C, "bn_fwd_stats: part too small");
+  TORCH_CHECK(src.numel() >= nsplit * (int64_t)M * C, "bn_fwd_stats: src too small");
+  TORCH_CHECK(part.numel() >= dpa_bn_part_floats(M, C, 0), "bn_fwd_stats: part too small");
   long long* nb = nullptr;
   if (nbt.has_value() && nbt->defined()) {
     need(*nbt, "nbt", at::kLong);
     nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
   }
-  chk(dpa_bn_fwd_stats(fp(z), fp(part), M, C, fp(gamma), fp(beta), ofp(bias), ofp(rmean), ofp(rvar), nb, fp(mean),
-                       fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps, cur_stream()),
+  chk(dpa_bn_fwd_stats(fp(src), (int)nsplit, fp(z), fp(part), M, C, fp(gamma), fp(beta), ofp(bias), ofp(rmean),
+                       ofp(rvar), nb, fp(mean), fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps,
+                       cur_stream()),
       "bn_fwd_stats");
 }
 
@@ -172,18 +188,22 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool) {
   chk(dpa_bn_apply(fp(z), fp(a), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()), "bn_apply");
 }
 
-void bn_bwd(Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, Tensor gamma, Tensor part,
-            Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool) {
+// gsrc: grad wrt the layer output (pooled shape if pool) or nsplit slabs of it (then the sum is
+// written to g).
+void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
+            Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool) {
+  need(gsrc, "gsrc");
   need(g, "g");
   need(z, "z");
   need(dz, "dz");
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   TORCH_CHECK(g.numel() == (int64_t)Mo * C, "bn_bwd: g shape");
-  TORCH_CHECK(part.numel() >= 3L * dpa_bn_nchunks(Mo) * C, "bn_bwd: part too small");
+  TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_bwd: gsrc too small");
+  TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd: part too small");
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
-  chk(dpa_bn_bwd(fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef), fp(dgamma),
-                 fp(dbeta), ofp(dbias), fp(dz), N, H, W, C, pool ? 1 : 0, cur_stream()),
+  chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
+                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), fp(dz), N, H, W, C, pool ? 1 : 0, cur_stream()),
       "bn_bwd");
 }
 
@@ -338,11 +358,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("scale_", &scale_);
   m.def("mean_of_w", &mean_of_w);
   m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
-        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0);
+        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("dgrad") = false, py::arg("reduce") = true);
+  m.def("conv_splits", &conv_splits);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dz"), py::arg("dw"), py::arg("slab"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0);
   m.def("wflip", &wflip);
-  m.def("bn_nchunks", &bn_nchunks);
+  m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);
   m.def("bn_apply", &bn_apply);

@@ -8,49 +8,104 @@
 // finalize kernel) and the eval-mode shift.  Its gradient (mathematically 0) is produced from
 // the same per-channel sums PyTorch would reduce (see bn_bwd_finalize).
 //
-// Forward:  stats partials (shifted sums per 64-row chunk) -> finalize (Chan merge, running-stat
-//           update with unbiased var, momentum, num_batches_tracked) -> apply+relu(+pool).
-// Backward: nothing but z (the conv output) is stored; y = relu(z*scale+shift), the pool argmax
-//           (first max in window scan order, as torch's CPU kernel) and x_hat are recomputed:
-//           reduce pass (sum dy, sum dy*xhat, sum xhat) -> finalize -> apply pass writing dz.
+// Forward:  stats partials per row-block (shifted sums, optionally summing split-K conv slabs
+//           on the fly and writing z) -> finalize (Chan merge, running-stat update with unbiased
+//           var, momentum, num_batches_tracked) -> apply+relu(+pool).
+// Backward: only z (the conv output) is stored; y = relu(z*scale+shift), the pool argmax (first
+//           max in window scan order, as torch's CPU kernel) and x_hat are recomputed:
+//           reduce pass (sum dy, sum dy*xhat, sum xhat; optionally summing split-K dgrad slabs
+//           of g and writing g) -> finalize -> apply pass writing dz.
+//
+// Reductions: a 256-thread block covers RPB rows x all channels (threads per row = C/4 float4
+// lanes, 256/(C/4) rows in flight), keeps per-thread partials in registers, combines them through
+// LDS, and writes ONE partial per (block, channel) — deterministic, no atomics.
 #include "common.h"
 
 namespace {
-constexpr int CHUNK = 64;  // rows per stats partial
 
-// ---- forward statistics: per (chunk, channel) shifted sums -> (mean, M2) ----
-__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ z, float2* __restrict__ part, int M,
-                                                       int C) {
-  const int C4 = C >> 2;
-  const int per_block = 256 / C4;  // chunks per block (C4 <= 256 divides 256 for C in {4..1024} powers of 2)
+struct RedGeom {
+  int C4, TPR, RPI, CG;  // float4 lanes per row, threads per row, rows per iteration, channel groups/thread
+};
+
+__host__ __device__ inline RedGeom red_geom(int C) {
+  RedGeom g;
+  g.C4 = C >> 2;
+  g.TPR = g.C4 < 256 ? g.C4 : 256;
+  g.RPI = 256 / g.TPR;
+  g.CG = (g.C4 + g.TPR - 1) / g.TPR;
+  return g;
+}
+
+// rows per block so that the grid has ~2048 blocks (at least one full iteration per block)
+__host__ inline int red_rows_per_block(int M, int C) {
+  const RedGeom g = red_geom(C);
+  int rpb = (M + 2047) / 2048;
+  rpb = ((rpb + g.RPI - 1) / g.RPI) * g.RPI;
+  return rpb < g.RPI ? g.RPI : rpb;
+}
+
+#define F4GET(v, k) ((k) == 0 ? (v).x : (k) == 1 ? (v).y : (k) == 2 ? (v).z : (v).w)
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// ---- forward statistics: per (row-block, channel) (mean, M2) via sums shifted by the block's
+// first row.  If nsplit > 1, src holds nsplit slabs of [M][C] that are summed here and written
+// to z (the split-K reduction of the producing conv, fused).
+__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ src, float* __restrict__ z,
+                                                       int nsplit, float2* __restrict__ part, int M, int C,
+                                                       int rpb) {
+  const RedGeom g = red_geom(C);
   const int t = threadIdx.x;
-  if (t >= per_block * C4) return;
-  const int c4 = t % C4;
-  const int chunk = blockIdx.x * per_block + t / C4;
-  const int r0 = chunk * CHUNK;
-  if (r0 >= M) return;
-  const int r1 = min(M, r0 + CHUNK);
-  const float4* zp = reinterpret_cast<const float4*>(z) + (long)r0 * C4 + c4;
-  const float4 x0 = zp[0];
-  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
-  for (int r = r0; r < r1; ++r) {
-    const float4 v = zp[(long)(r - r0) * C4];
-    const float d0 = v.x - x0.x, d1 = v.y - x0.y, d2 = v.z - x0.z, d3 = v.w - x0.w;
-    s1.x += d0;
-    s1.y += d1;
-    s1.z += d2;
-    s1.w += d3;
-    s2.x += d0 * d0;
-    s2.y += d1 * d1;
-    s2.z += d2 * d2;
-    s2.w += d3 * d3;
+  const int lane_c = t % g.TPR, lane_r = t / g.TPR;
+  const bool active = lane_r < g.RPI;
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(M, r0 + rpb);
+  const long slab4 = (long)M * g.C4;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  __shared__ float4 sh1[256], sh2[256];
+  for (int cg = 0; cg < g.CG; ++cg) {
+    const int c4 = lane_c + cg * g.TPR;
+    const bool cval = active && c4 < g.C4;
+    float4 K = make_float4(0.f, 0.f, 0.f, 0.f), a1 = K, a2 = K;
+    if (cval) {
+      // shift = the block's first row (summed over splits)
+      K = s4[(long)r0 * g.C4 + c4];
+      for (int s = 1; s < nsplit; ++s) K = f4add(K, s4[s * slab4 + (long)r0 * g.C4 + c4]);
+      for (int r = r0 + lane_r; r < r1; r += g.RPI) {
+        const long i = (long)r * g.C4 + c4;
+        float4 v = s4[i];
+        for (int s = 1; s < nsplit; ++s) v = f4add(v, s4[s * slab4 + i]);
+        if (nsplit > 1) reinterpret_cast<float4*>(z)[i] = v;
+        const float d0 = v.x - K.x, d1 = v.y - K.y, d2 = v.z - K.z, d3 = v.w - K.w;
+        a1.x += d0;
+        a1.y += d1;
+        a1.z += d2;
+        a1.w += d3;
+        a2.x = fmaf(d0, d0, a2.x);
+        a2.y = fmaf(d1, d1, a2.y);
+        a2.z = fmaf(d2, d2, a2.z);
+        a2.w = fmaf(d3, d3, a2.w);
+      }
+    }
+    sh1[t] = a1;
+    sh2[t] = a2;
+    __syncthreads();
+    if (cval && lane_r == 0) {
+      for (int k = 1; k < g.RPI; ++k) {
+        a1 = f4add(a1, sh1[t + k * g.TPR]);
+        a2 = f4add(a2, sh2[t + k * g.TPR]);
+      }
+      const float n = (float)(r1 - r0), inv = 1.f / n;
+      float2* o = part + (long)blockIdx.x * C + c4 * 4;
+      o[0] = make_float2(K.x + a1.x * inv, fmaxf(a2.x - a1.x * a1.x * inv, 0.f));
+      o[1] = make_float2(K.y + a1.y * inv, fmaxf(a2.y - a1.y * a1.y * inv, 0.f));
+      o[2] = make_float2(K.z + a1.z * inv, fmaxf(a2.z - a1.z * a1.z * inv, 0.f));
+      o[3] = make_float2(K.w + a1.w * inv, fmaxf(a2.w - a1.w * a1.w * inv, 0.f));
+    }
+    __syncthreads();
   }
-  const float n = (float)(r1 - r0), inv = 1.f / n;
-  float2* o = part + (long)chunk * C + c4 * 4;
-  o[0] = make_float2(x0.x + s1.x * inv, fmaxf(s2.x - s1.x * s1.x * inv, 0.f));
-  o[1] = make_float2(x0.y + s1.y * inv, fmaxf(s2.y - s1.y * s1.y * inv, 0.f));
-  o[2] = make_float2(x0.z + s1.z * inv, fmaxf(s2.z - s1.z * s1.z * inv, 0.f));
-  o[3] = make_float2(x0.w + s1.w * inv, fmaxf(s2.w - s1.w * s1.w * inv, 0.f));
 }
 
 struct Welford {
@@ -70,38 +125,42 @@ __device__ __forceinline__ Welford merge(Welford a, Welford b) {
   return r;
 }
 
-// One block per channel: Chan-merge the chunk partials, derive scale/shift, update running stats.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restrict__ part, int nchunks, int M, int C,
-                                                          const float* __restrict__ gamma,
+// 16 channels x 16 partial-groups per block: coalesced 128-B reads of the partials, Chan merge,
+// then scale/shift + running-stat update.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restrict__ part, int nblk, int rpb, int M,
+                                                          int C, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta,
                                                           const float* __restrict__ bias, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, long long* __restrict__ nbt,
                                                           float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float momentum, float eps) {
-  const int c = blockIdx.x;
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   Welford acc{0.f, 0.f, 0.f};
-  for (int k = threadIdx.x; k < nchunks; k += 256) {
-    const float2 p = part[(long)k * C + c];
-    const int cnt = min(CHUNK, M - k * CHUNK);
-    acc = merge(acc, Welford{(float)cnt, p.x, p.y});
+  if (c < C) {
+    for (int k = grp; k < nblk; k += 16) {
+      const float2 p = part[(long)k * C + c];
+      const int cnt = min(rpb, M - k * rpb);
+      acc = merge(acc, Welford{(float)cnt, p.x, p.y});
+    }
   }
   __shared__ Welford sh[256];
   sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = 128; o >= 16; o >>= 1) {
     if ((int)threadIdx.x < o) sh[threadIdx.x] = merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const Welford w = sh[0];
+  if (grp == 0 && c < C) {
+    const Welford w = sh[cl];
     const float var = w.m2 / w.n;
     const float inv = rsqrtf(var + eps);
-    const float g = gamma[c];
+    const float gm = gamma[c];
     mean_out[c] = w.mean;
     invstd_out[c] = inv;
-    scale[c] = g * inv;
-    shift[c] = beta[c] - w.mean * g * inv;
+    scale[c] = gm * inv;
+    shift[c] = beta[c] - w.mean * gm * inv;
     if (rmean) {
       const float b = bias ? bias[c] : 0.f;
       const float unb = w.n > 1.f ? w.m2 / (w.n - 1.f) : var;
@@ -163,8 +222,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   }
 }
 
-// --- backward helpers: per scalar channel, route pooled grad to the first max, apply relu mask ---
-// returns dy for the 4 window positions (00,01,10,11)
+// route the pooled grad to the first max of the window (scan order 00,01,10,11), relu mask
 __device__ __forceinline__ void route1(float z00, float z01, float z10, float z11, float sc, float sh, float g,
                                        float& d00, float& d01, float& d10, float& d11) {
   const float y00 = fmaxf(fmaf(z00, sc, sh), 0.f), y01 = fmaxf(fmaf(z01, sc, sh), 0.f);
@@ -174,108 +232,129 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
   if (y01 > mx) { mx = y01; arg = 1; }
   if (y10 > mx) { mx = y10; arg = 2; }
   if (y11 > mx) { mx = y11; arg = 3; }
-  // relu backward: gradient passes where the relu output is > 0
   d00 = (arg == 0 && y00 > 0.f) ? g : 0.f;
   d01 = (arg == 1 && y01 > 0.f) ? g : 0.f;
   d10 = (arg == 2 && y10 > 0.f) ? g : 0.f;
   d11 = (arg == 3 && y11 > 0.f) ? g : 0.f;
 }
 
-#define F4GET(v, k) ((k) == 0 ? (v).x : (k) == 1 ? (v).y : (k) == 2 ? (v).z : (v).w)
-
-// Reduce pass: per (row chunk, c4) sums of dy, dy*xhat, xhat.  For POOL, rows are pooled positions
-// (each covers 4 full-resolution rows).  part layout: [chunk][3][C]
+// Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat.  Rows are OUTPUT rows of
+// the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
+// the summed g is written to gout (consumed by the apply pass).  part layout: [block][3][C]
 template <bool POOL>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ z,
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ gsrc, float* __restrict__ gout,
+                                                            int nsplit, const float* __restrict__ z,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
-                                                            float* __restrict__ part, int N, int H, int W, int C) {
-  const int C4 = C >> 2;
-  const int per_block = 256 / C4;
+                                                            float* __restrict__ part, int N, int H, int W, int C,
+                                                            int rpb) {
+  const RedGeom gg = red_geom(C);
   const int t = threadIdx.x;
-  if (t >= per_block * C4) return;
-  const int c4 = t % C4;
-  const int chunk = blockIdx.x * per_block + t / C4;
+  const int lane_c = t % gg.TPR, lane_r = t / gg.TPR;
+  const bool active = lane_r < gg.RPI;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const int Mo = N * Ho * Wo;
-  const int r0 = chunk * CHUNK;
-  if (r0 >= Mo) return;
-  const int r1 = min(Mo, r0 + CHUNK);
-  const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
-  const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
-  const float4 mu = reinterpret_cast<const float4*>(mean)[c4];
-  const float4 is = reinterpret_cast<const float4*>(invstd)[c4];
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(Mo, r0 + rpb);
+  const long slab4 = (long)Mo * gg.C4;
   const float4* z4 = reinterpret_cast<const float4*>(z);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  float sdy[4] = {0, 0, 0, 0}, sdx[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
-  for (int r = r0; r < r1; ++r) {
-    const float4 gv = g4[(long)r * C4 + c4];
-    if (!POOL) {
-      const float4 zv = z4[(long)r * C4 + c4];
+  const float4* g4 = reinterpret_cast<const float4*>(gsrc);
+  __shared__ float4 shA[256], shB[256], shX[256];
+  for (int cg = 0; cg < gg.CG; ++cg) {
+    const int c4 = lane_c + cg * gg.TPR;
+    const bool cval = active && c4 < gg.C4;
+    float sdy[4] = {0, 0, 0, 0}, sdx[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
+    if (cval) {
+      const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
+      const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
+      const float4 mu = reinterpret_cast<const float4*>(mean)[c4];
+      const float4 is = reinterpret_cast<const float4*>(invstd)[c4];
+      for (int r = r0 + lane_r; r < r1; r += gg.RPI) {
+        const long gi = (long)r * gg.C4 + c4;
+        float4 gv = g4[gi];
+        for (int s = 1; s < nsplit; ++s) gv = f4add(gv, g4[s * slab4 + gi]);
+        if (nsplit > 1) reinterpret_cast<float4*>(gout)[gi] = gv;
+        if (!POOL) {
+          const float4 zv = z4[gi];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float zz = F4GET(zv, k);
-        const float y = fmaf(zz, F4GET(sc, k), F4GET(sh, k));
-        const float dy = y > 0.f ? F4GET(gv, k) : 0.f;
-        const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
-        sdy[k] += dy;
-        sdx[k] += dy * xh;
-        sx[k] += xh;
-      }
-    } else {
-      const int ow = r % Wo;
-      const int tt = r / Wo;
-      const int oh = tt % Ho;
-      const int n = tt / Ho;
-      const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * C4 + c4;
-      const float4 z00 = z4[base], z01 = z4[base + C4], z10 = z4[base + (long)W * C4], z11 = z4[base + (long)W * C4 + C4];
+          for (int k = 0; k < 4; ++k) {
+            const float zz = F4GET(zv, k);
+            const float dy = fmaf(zz, F4GET(sc, k), F4GET(sh, k)) > 0.f ? F4GET(gv, k) : 0.f;
+            const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
+            sdy[k] += dy;
+            sdx[k] = fmaf(dy, xh, sdx[k]);
+            sx[k] += xh;
+          }
+        } else {
+          const int ow = r % Wo;
+          const int tt = r / Wo;
+          const int oh = tt % Ho;
+          const int n = tt / Ho;
+          const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * gg.C4 + c4;
+          const float4 z00 = z4[base], z01 = z4[base + gg.C4], z10 = z4[base + (long)W * gg.C4],
+                       z11 = z4[base + (long)W * gg.C4 + gg.C4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float d00, d01, d10, d11;
-        route1(F4GET(z00, k), F4GET(z01, k), F4GET(z10, k), F4GET(z11, k), F4GET(sc, k), F4GET(sh, k), F4GET(gv, k),
-               d00, d01, d10, d11);
-        const float m = F4GET(mu, k), iv = F4GET(is, k);
-        const float x00 = (F4GET(z00, k) - m) * iv, x01 = (F4GET(z01, k) - m) * iv;
-        const float x10 = (F4GET(z10, k) - m) * iv, x11 = (F4GET(z11, k) - m) * iv;
-        sdy[k] += (d00 + d01) + (d10 + d11);
-        sdx[k] += (d00 * x00 + d01 * x01) + (d10 * x10 + d11 * x11);
-        sx[k] += (x00 + x01) + (x10 + x11);
+          for (int k = 0; k < 4; ++k) {
+            float d00, d01, d10, d11;
+            route1(F4GET(z00, k), F4GET(z01, k), F4GET(z10, k), F4GET(z11, k), F4GET(sc, k), F4GET(sh, k),
+                   F4GET(gv, k), d00, d01, d10, d11);
+            const float m = F4GET(mu, k), iv = F4GET(is, k);
+            const float x00 = (F4GET(z00, k) - m) * iv, x01 = (F4GET(z01, k) - m) * iv;
+            const float x10 = (F4GET(z10, k) - m) * iv, x11 = (F4GET(z11, k) - m) * iv;
+            sdy[k] += (d00 + d01) + (d10 + d11);
+            sdx[k] += (d00 * x00 + d01 * x01) + (d10 * x10 + d11 * x11);
+            sx[k] += (x00 + x01) + (x10 + x11);
+          }
+        }
       }
     }
-  }
-  float* o = part + (long)chunk * 3 * C + c4 * 4;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    o[k] = sdy[k];
-    o[C + k] = sdx[k];
-    o[2 * C + k] = sx[k];
+    shA[t] = make_float4(sdy[0], sdy[1], sdy[2], sdy[3]);
+    shB[t] = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
+    shX[t] = make_float4(sx[0], sx[1], sx[2], sx[3]);
+    __syncthreads();
+    if (cval && lane_r == 0) {
+      float4 a = shA[t], b = shB[t], x = shX[t];
+      for (int k = 1; k < gg.RPI; ++k) {
+        a = f4add(a, shA[t + k * gg.TPR]);
+        b = f4add(b, shB[t + k * gg.TPR]);
+        x = f4add(x, shX[t + k * gg.TPR]);
+      }
+      float* o = part + (long)blockIdx.x * 3 * C + c4 * 4;
+      *reinterpret_cast<float4*>(o) = a;
+      *reinterpret_cast<float4*>(o + C) = b;
+      *reinterpret_cast<float4*>(o + 2 * C) = x;
+    }
+    __syncthreads();
   }
 }
 
-// Per channel: sum the chunk partials (fixed order -> deterministic), emit dgamma, dbeta, dbias and
-// the dz coefficients: dz = k1*dy + k2*z + k3.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nchunks, int C,
+// Per channel: sum the block partials (fixed order -> deterministic), emit dgamma, dbeta, dbias and
+// the dz coefficients: dz = k1*dy + k2*z + k3.   16 channels x 16 groups per block.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                               float Mfull, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ dbias, float* __restrict__ coef) {
-  const int c = blockIdx.x;
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float a = 0.f, b = 0.f, x = 0.f;
-  for (int k = threadIdx.x; k < nchunks; k += 256) {
-    const float* p = part + (long)k * 3 * C + c;
-    a += p[0];
-    b += p[C];
-    x += p[2 * C];
+  if (c < C) {
+    for (int k = grp; k < nblk; k += 16) {
+      const float* p = part + (long)k * 3 * C + c;
+      a += p[0];
+      b += p[C];
+      x += p[2 * C];
+    }
   }
   __shared__ float sh[3][256];
   sh[0][threadIdx.x] = a;
   sh[1][threadIdx.x] = b;
   sh[2][threadIdx.x] = x;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = 128; o >= 16; o >>= 1) {
     if ((int)threadIdx.x < o) {
       sh[0][threadIdx.x] += sh[0][threadIdx.x + o];
       sh[1][threadIdx.x] += sh[1][threadIdx.x + o];
@@ -283,17 +362,17 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const float sdy = sh[0][0], sdx = sh[1][0], sx = sh[2][0];
-    const float iv = invstd[c], g = gamma[c];
-    const float k1 = g * iv;
+  if (grp == 0 && c < C) {
+    const float sdy = sh[0][cl], sdx = sh[1][cl], sx = sh[2][cl];
+    const float iv = invstd[c], gm = gamma[c];
+    const float k1 = gm * iv;
     const float k2x = -k1 * sdx / Mfull;  // coefficient of xhat
     const float k3 = -k1 * sdy / Mfull;
     dgamma[c] = sdx;
     dbeta[c] = sdy;
-    if (dbias) dbias[c] = k1 * (sdy - sdy) + k2x * sx;  // = sum over rows of dz
+    if (dbias) dbias[c] = k2x * sx;  // = sum over rows of dz (analytically 0)
     coef[c] = k1;
-    coef[C + c] = k2x * iv;                   // coefficient of z
+    coef[C + c] = k2x * iv;                     // coefficient of z
     coef[2 * C + c] = k3 - k2x * iv * mean[c];  // constant
   }
 }
@@ -365,18 +444,23 @@ int grid_1d(long n) {
 
 extern "C" {
 
-int dpa_bn_nchunks(int M) { return (M + CHUNK - 1) / CHUNK; }
+// floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (3 per ...)
+long dpa_bn_part_floats(int M, int C, int bwd) {
+  const int rpb = red_rows_per_block(M, C);
+  const long nblk = (M + rpb - 1) / rpb;
+  return nblk * C * (bwd ? 3 : 2);
+}
 
-// z [M][C] -> partials [nchunks][C] float2 -> finalize
-int dpa_bn_fwd_stats(const float* z, float* part, int M, int C, const float* gamma, const float* beta,
-                     const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
-                     float* scale, float* shift, float momentum, float eps, hipStream_t st) {
-  if (C % 4 || (256 % (C / 4)) != 0) return -2;
-  const int nchunks = (M + CHUNK - 1) / CHUNK;
-  const int per_block = 256 / (C / 4);
-  bn_stats_kernel<<<cdiv(nchunks, per_block), 256, 0, st>>>(z, reinterpret_cast<float2*>(part), M, C);
-  bn_finalize_kernel<<<C, 256, 0, st>>>(reinterpret_cast<const float2*>(part), nchunks, M, C, gamma, beta, bias, rmean,
-                                        rvar, nbt, mean, invstd, scale, shift, momentum, eps);
+// z [M][C] (or nsplit slabs of it in src; then z is written) -> partials -> finalize
+int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M, int C, const float* gamma,
+                     const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
+                     float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st) {
+  if (C % 4) return -2;
+  const int rpb = red_rows_per_block(M, C);
+  const int nblk = (M + rpb - 1) / rpb;
+  bn_stats_kernel<<<nblk, 256, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C, rpb);
+  bn_finalize_kernel<<<cdiv(C, 16), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
+                                                  bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
   return (int)hipGetLastError();
 }
 
@@ -397,28 +481,31 @@ int dpa_bn_apply(const float* z, float* a, const float* scale, const float* shif
   return (int)hipGetLastError();
 }
 
-// g: grad of the layer output (pooled shape if pool).  Writes dz [N,H,W,C] and dgamma/dbeta/dbias.
-int dpa_bn_bwd(const float* g, const float* z, const float* scale, const float* shift, const float* mean,
-               const float* invstd, const float* gamma, float* part, float* coef, float* dgamma, float* dbeta,
-               float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st) {
-  if (C % 4 || (256 % (C / 4)) != 0) return -2;
+// gsrc: grad of the layer output (pooled shape if pool), or nsplit slabs of it (then the sum is
+// written to g).  Writes dz [N,H,W,C] and dgamma/dbeta/dbias.
+int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
+               const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
+               float* dbeta, float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st) {
+  if (C % 4) return -2;
+  if (nsplit < 1) nsplit = 1;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
-  const int nchunks = (Mo + CHUNK - 1) / CHUNK;
-  const int per_block = 256 / (C / 4);
+  const int rpb = red_rows_per_block(Mo, C);
+  const int nblk = (Mo + rpb - 1) / rpb;
   if (pool)
-    bn_bwd_reduce_kernel<true><<<cdiv(nchunks, per_block), 256, 0, st>>>(g, z, scale, shift, mean, invstd, part, N, H,
-                                                                        W, C);
+    bn_bwd_reduce_kernel<true><<<nblk, 256, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W, C,
+                                                     rpb);
   else
-    bn_bwd_reduce_kernel<false><<<cdiv(nchunks, per_block), 256, 0, st>>>(g, z, scale, shift, mean, invstd, part, N,
-                                                                         H, W, C);
-  bn_bwd_finalize_kernel<<<C, 256, 0, st>>>(part, nchunks, C, (float)N * H * W, gamma, mean, invstd, dgamma, dbeta,
-                                            dbias, coef);
+    bn_bwd_reduce_kernel<false><<<nblk, 256, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W,
+                                                      C, rpb);
+  bn_bwd_finalize_kernel<<<cdiv(C, 16), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
+                                                      dbeta, dbias, coef);
+  const float* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
   if (pool)
-    bn_bwd_apply_kernel<true><<<grid_1d(total), 256, 0, st>>>(g, z, scale, shift, coef, dz, N, H, W, C);
+    bn_bwd_apply_kernel<true><<<grid_1d(total), 256, 0, st>>>(gg, z, scale, shift, coef, dz, N, H, W, C);
   else
-    bn_bwd_apply_kernel<false><<<grid_1d(total), 256, 0, st>>>(g, z, scale, shift, coef, dz, N, H, W, C);
+    bn_bwd_apply_kernel<false><<<grid_1d(total), 256, 0, st>>>(gg, z, scale, shift, coef, dz, N, H, W, C);
   return (int)hipGetLastError();
 }
 

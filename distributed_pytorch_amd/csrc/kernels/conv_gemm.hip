@@ -5,7 +5,8 @@
 // Layout is NHWC activations and KRSC weights, so every GEMM operand row is a contiguous
 // channel run:
 //   FPROP  out[m][n]  = sum_k  Xcol[m][k] * W[n][k]          m=(img,oh,ow) n=kout  k=(r,s,c)
-//   DGRAD  (stride 1, "same" pad) is FPROP of dZ with Wd[c][r][s][k] = W[k][R-1-r][S-1-s][c]
+//   DGRAD  (stride 1, "same" pad) = FPROP of dZ with Wd[c][r][s][k] = W[k][R-1-r][S-1-s][c]; the B
+//          loader reads W with the flipped tap index directly (no transposed weight copy)
 //   WGRAD  dW[n][k]   = sum_m  dZ[m][n] * Xcol[m][k]          (split-K over m = N*P*Q)
 //
 // Tiling: BM x BN block tile, BK = 32 k per LDS stage, double-buffered LDS with register-staged
@@ -17,7 +18,7 @@
 // and B, so the sum over k is unchanged (and each MFMA is still an exact f32 fma chain).
 //
 // LDS images: a k-contiguous operand is stored [row][BK+4] (16-row b128 lane groups hit 16
-// distinct 16-B slots: conflict-free), a row-contiguous operand (WGRAD) [BK][rows+4].
+// distinct 16-B slots: conflict-free), a row-contiguous operand (WGRAD A/B, DGRAD B) [BK][rows+4].
 #include "common.h"
 
 namespace {
@@ -85,15 +86,19 @@ struct RowContigSlots {  // a row-contiguous operand tile BK x ROWS, loaded as f
 
 __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool WGRAD>
+enum { MODE_FPROP = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvArgs a) {
+  constexpr bool WGRAD = MODE == MODE_WGRAD;
+  constexpr bool B_ROWC = MODE != MODE_FPROP;  // B operand row-contiguous in global memory
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
   // LDS sizes (floats) per stage
   constexpr int A_STAGE = WGRAD ? BK * (BM + KPAD) : BM * (BK + KPAD);
-  constexpr int B_STAGE = WGRAD ? BK * (BN + KPAD) : BN * (BK + KPAD);
+  constexpr int B_STAGE = B_ROWC ? BK * (BN + KPAD) : BN * (BK + KPAD);
   __shared__ __attribute__((aligned(16))) float lds[2 * (A_STAGE + B_STAGE)];
 
   const int tid = threadIdx.x;
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
   // ---------------- per-thread load-slot precomputation ----------------
   // A operand
   using ASl = typename std::conditional<WGRAD, RowContigSlots<BM, THREADS>, KContigSlots<BM, THREADS>>::type;
-  using BSl = typename std::conditional<WGRAD, RowContigSlots<BN, THREADS>, KContigSlots<BN, THREADS>>::type;
+  using BSl = typename std::conditional<B_ROWC, RowContigSlots<BN, THREADS>, KContigSlots<BN, THREADS>>::type;
   constexpr int NA = ASl::NSLOT, NB = BSl::NSLOT;
 
   float4 ra[NA], rb[NB];
@@ -151,10 +156,16 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         a_iw0[j] = 0;
       }
     }
-    b_k4 = tid % (BK / 4);
-    b_row0 = tid / (BK / 4);
+    if constexpr (MODE == MODE_FPROP) {
+      b_k4 = tid % (BK / 4);
+      b_row0 = tid / (BK / 4);
+    } else {
+      b_c = n0 + (tid % BSl::F4_PER_K) * 4;  // output channel of the dgrad GEMM = input channel of W
+      b_colvalid = b_c < a.Nout;
+      b_krow = tid / BSl::F4_PER_K;
+    }
   } else {
-    a_col = n0 * 0 + m0 + (tid % ASl::F4_PER_K) * 4;  // kout index (A rows = kout, tile origin m0)
+    a_col = m0 + (tid % ASl::F4_PER_K) * 4;  // kout index (A rows = kout, tile origin m0)
     a_krow = tid / ASl::F4_PER_K;
     const int rsc = n0 + (tid % BSl::F4_PER_K) * 4;  // B rows = rsc
     b_colvalid = rsc < a.Ktot;
@@ -181,13 +192,28 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         const bool v = kval && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         ra[j] = v ? ldg4(a.x + (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      const int kb4 = kb + b_k4 * 4;
-      const bool kbv = kb4 < kend;
+      if constexpr (MODE == MODE_FPROP) {
+        const int kb4 = kb + b_k4 * 4;
+        const bool kbv = kb4 < kend;
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int n = n0 + b_row0 + j * BSl::ROW_STEP;
-        const bool v = kbv && n < a.Nout;
-        rb[j] = v ? ldg4(a.w + (long)n * a.Ktot + kb4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < NB; ++j) {
+          const int n = n0 + b_row0 + j * BSl::ROW_STEP;
+          const bool v = kbv && n < a.Nout;
+          rb[j] = v ? ldg4(a.w + (long)n * a.Ktot + kb4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      } else {
+        // DGRAD: B[n=c][k=(r',s',kk)] = W[kk][R-1-r'][S-1-s'][c], W stored [Kout=a.C][R][S][Nout]
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int k = kb + b_krow + j * BSl::K_STEP;
+          const unsigned tp = fdiv((unsigned)k, a.fd_C);
+          const int kk = k - (int)tp * a.C;
+          const unsigned rr = fdiv(tp, a.fd_S);
+          const int ss = (int)(tp - rr * a.S);
+          const bool v = k < kend && b_colvalid;
+          rb[j] = v ? ldg4(a.w + (((long)kk * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + b_c)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
     } else {
       // A = dZ^T : element (kout, m) = dZ[m][kout]
@@ -221,9 +247,16 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
 #pragma unroll
       for (int j = 0; j < NA; ++j)
         *reinterpret_cast<float4*>(As + (r0 + j * ASl::ROW_STEP) * (BK + KPAD) + a_k4 * 4) = ra[j];
+      if constexpr (MODE == MODE_FPROP) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
-        *reinterpret_cast<float4*>(Bs + (b_row0 + j * BSl::ROW_STEP) * (BK + KPAD) + b_k4 * 4) = rb[j];
+        for (int j = 0; j < NB; ++j)
+          *reinterpret_cast<float4*>(Bs + (b_row0 + j * BSl::ROW_STEP) * (BK + KPAD) + b_k4 * 4) = rb[j];
+      } else {
+        const int cb = (tid % BSl::F4_PER_K) * 4;
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          *reinterpret_cast<float4*>(Bs + (b_krow + j * BSl::K_STEP) * (BN + KPAD) + cb) = rb[j];
+      }
     } else {
       const int ca = (tid % ASl::F4_PER_K) * 4;
 #pragma unroll
@@ -263,7 +296,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wc * WTN + j * 32 + li;
-        if constexpr (!WGRAD) {
+        if constexpr (!B_ROWC) {
           fb[j] = *reinterpret_cast<const float4*>(Bs + row * (BK + KPAD) + 8 * q + 4 * lh);
         } else {
           const float* p = Bs + (8 * q + 4 * lh) * (BN + KPAD) + row;
@@ -347,10 +380,10 @@ __global__ __launch_bounds__(256) void wflip_kernel(const float* __restrict__ w,
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool WG>
+template <int BM, int BN, int WM, int WN, int MODE>
 int launch_cfg(const ConvArgs& a, int splits, hipStream_t st) {
   dim3 grid(a.gm * a.gn, splits);
-  conv_gemm_kernel<BM, BN, WM, WN, WG><<<grid, WM * WN * 64, 0, st>>>(a);
+  conv_gemm_kernel<BM, BN, WM, WN, MODE><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -362,15 +395,7 @@ int grid_1d(long n) {
 
 }  // namespace
 
-extern "C" {
-
-// Common conv geometry. out_or_slab must hold splits * rows * cols floats when splits > 1.
-// tile: 0 -> 128x128 (4 waves, 64x64 each), 1 -> 64x64 (4 waves, 32x32 each)
-int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
-                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st) {
-  ConvArgs a{};
-  a.x = x;
-  a.w = w;
+static void fill_geom(ConvArgs& a, int N, int H, int W, int C, int R, int S, int stride, int pad) {
   a.N = N;
   a.H = H;
   a.W = W;
@@ -382,9 +407,30 @@ int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int 
   a.P = (H + 2 * pad - R) / stride + 1;
   a.Q = (W + 2 * pad - S) / stride + 1;
   a.M = N * a.P * a.Q;
-  a.Nout = Kout;
   a.Ktot = R * S * C;
+  a.fd_C = make_fastdiv(C);
+  a.fd_S = make_fastdiv(S);
+  a.fd_Q = make_fastdiv(a.Q);
+  a.fd_PQ = make_fastdiv(a.P * a.Q);
+}
+
+extern "C" {
+
+// Forward conv (and, with dgrad=1, the stride-1 "same" data-gradient conv reading the ORIGINAL
+// weights with flipped taps).  x: NHWC [N,H,W,C]; w: fprop [Kout][R][S][C], dgrad [C][R][S][Kout]
+// (the original conv's weights, whose input channels Kout are this GEMM's outputs); out
+// [N,P,Q,Kout].  splits > 1: partial sums go to slab[splits][M][Kout]; reduce=1 sums them into
+// out here, reduce=0 leaves them for a consumer that sums on the fly (bn_fwd_stats / bn_bwd).
+// tile: 0 -> 128x128 (4 waves, 64x64 each), 1 -> 64x64 (4 waves, 32x32 each)
+int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
+                   int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, hipStream_t st) {
+  ConvArgs a{};
+  a.x = x;
+  a.w = w;
+  fill_geom(a, N, H, W, C, R, S, stride, pad);
+  a.Nout = Kout;
   if (C % 4 || Kout % 4) return -2;
+  if (dgrad && (stride != 1 || a.P != H || a.Q != W)) return -3;
   const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
   a.gm = cdiv(a.M, BMv);
   a.gn = cdiv(Kout, BNv);
@@ -393,18 +439,27 @@ int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int 
   splits = cdiv(a.Ktot, a.kchunk);
   a.out = splits > 1 ? slab : out;
   a.slab = splits > 1 ? (long)a.M * Kout : 0;
-  a.fd_C = make_fastdiv(C);
-  a.fd_S = make_fastdiv(S);
-  a.fd_Q = make_fastdiv(a.Q);
-  a.fd_PQ = make_fastdiv(a.P * a.Q);
-  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, false>(a, splits, st) : launch_cfg<64, 64, 2, 2, false>(a, splits, st);
+  int rc;
+  if (dgrad)
+    rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_DGRAD>(a, splits, st)
+                   : launch_cfg<64, 64, 2, 2, MODE_DGRAD>(a, splits, st);
+  else
+    rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_FPROP>(a, splits, st)
+                   : launch_cfg<64, 64, 2, 2, MODE_FPROP>(a, splits, st);
   if (rc) return rc;
-  if (splits > 1) {
+  if (splits > 1 && reduce) {
     const long n4 = (long)a.M * Kout / 4;
     splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, splits);
     rc = (int)hipGetLastError();
   }
   return rc;
+}
+
+// effective split count the launcher will use (the K range is rounded to BK multiples)
+int dpa_conv_splits(int Ktot, int splits) {
+  if (splits < 1) splits = 1;
+  const int kchunk = cdiv(cdiv(Ktot, splits), BK) * BK;
+  return cdiv(Ktot, kchunk);
 }
 
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] * Xcol[m][rsc]
@@ -413,19 +468,8 @@ int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int 
   ConvArgs a{};
   a.x = x;
   a.w = dz;
-  a.N = N;
-  a.H = H;
-  a.W = W;
-  a.C = C;
-  a.R = R;
-  a.S = S;
-  a.stride = stride;
-  a.pad = pad;
-  a.P = (H + 2 * pad - R) / stride + 1;
-  a.Q = (W + 2 * pad - S) / stride + 1;
-  a.M = N * a.P * a.Q;
+  fill_geom(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
-  a.Ktot = R * S * C;
   if (C % 4 || Kout % 4) return -2;
   const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
   a.gm = cdiv(Kout, BMv);
@@ -435,11 +479,8 @@ int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int 
   splits = cdiv(a.M, a.kchunk);
   a.out = splits > 1 ? slab : dw;
   a.slab = splits > 1 ? (long)Kout * a.Ktot : 0;
-  a.fd_C = make_fastdiv(C);
-  a.fd_S = make_fastdiv(S);
-  a.fd_Q = make_fastdiv(a.Q);
-  a.fd_PQ = make_fastdiv(a.P * a.Q);
-  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, true>(a, splits, st) : launch_cfg<64, 64, 2, 2, true>(a, splits, st);
+  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_WGRAD>(a, splits, st)
+                     : launch_cfg<64, 64, 2, 2, MODE_WGRAD>(a, splits, st);
   if (rc) return rc;
   if (splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;

@@ -80,42 +80,66 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
   }
 }
 
-// grid: J + 1 blocks.  Block j < J computes dW[j][:] and db[j]; block J reduces the loss.
+// grid: cdiv(Cin,256) + 1 blocks.  Column blocks compute dW[:, c] for one c per thread (dlogits
+// staged through LDS 64 rows at a time, x read coalesced); the last block reduces db and the loss.
 __global__ __launch_bounds__(256) void fc_ce_wgrad_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ dlogits,
                                                           const float* __restrict__ loss_row, float* __restrict__ dw,
                                                           float* __restrict__ db, float* __restrict__ loss_out,
                                                           float* __restrict__ loss_accum, int B, int Cin, int J) {
-  const int j = blockIdx.x;
-  __shared__ float sh[256];
-  if (j < J) {
-    for (int c = threadIdx.x; c < Cin; c += 256) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += dlogits[(long)b * J + j] * x[(long)b * Cin + c];
-      dw[(long)j * Cin + c] = s;
-    }
-    float s = 0.f;
-    for (int b = threadIdx.x; b < B; b += 256) s += dlogits[(long)b * J + j];
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+  const int ncb = (Cin + 255) / 256;
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x < ncb) {
+    __shared__ float sdl[64 * MAXJ];
+    const int c = blockIdx.x * 256 + t;
+    float acc[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) acc[j] = 0.f;
+    for (int b0 = 0; b0 < B; b0 += 64) {
+      const int nb = min(64, B - b0);
+      for (int e = t; e < nb * J; e += 256) sdl[(e / J) * MAXJ + e % J] = dlogits[(long)b0 * J + e];
+      __syncthreads();
+      if (c < Cin) {
+        for (int b = 0; b < nb; ++b) {
+          const float xv = x[(long)(b0 + b) * Cin + c];
+#pragma unroll
+          for (int j = 0; j < MAXJ; ++j)
+            if (j < J) acc[j] = fmaf(sdl[b * MAXJ + j], xv, acc[j]);
+        }
+      }
       __syncthreads();
     }
-    if (threadIdx.x == 0) db[j] = sh[0];
+    if (c < Cin) {
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j)
+        if (j < J) dw[(long)j * Cin + c] = acc[j];
+    }
   } else {
+    __shared__ float sh[256];
+    __shared__ float sj[16][MAXJ + 1];
+    // db: thread (j = t % 16, g = t / 16) sums rows g, g+16, ...
+    const int jj = t % 16, g = t / 16;
     float s = 0.f;
-    for (int b = threadIdx.x; b < B; b += 256) s += loss_row[b];
-    sh[threadIdx.x] = s;
+    if (jj < J)
+      for (int b = g; b < B; b += 16) s += dlogits[(long)b * J + jj];
+    sj[g][jj] = s;
+    float l = 0.f;
+    for (int b = t; b < B; b += 256) l += loss_row[b];
+    sh[t] = l;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+      if (t < o) sh[t] += sh[t + o];
       __syncthreads();
     }
-    if (threadIdx.x == 0) {
-      const float l = sh[0] / (float)B;
-      loss_out[0] = l;
-      if (loss_accum) loss_accum[0] += l;
+    if (t < J) {
+      float d = 0.f;
+      for (int k = 0; k < 16; ++k) d += sj[k][t];
+      db[t] = d;
+    }
+    if (t == 0) {
+      const float lm = sh[0] / (float)B;
+      loss_out[0] = lm;
+      if (loss_accum) loss_accum[0] += lm;
     }
   }
 }
@@ -158,7 +182,7 @@ int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long l
   if (J > MAXJ) return -2;
   fc_ce_rows_kernel<true><<<cdiv(B, 4), 256, 0, st>>>(x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin,
                                                       J);
-  fc_ce_wgrad_kernel<<<J + 1, 256, 0, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B, Cin, J);
+  fc_ce_wgrad_kernel<<<cdiv(Cin, 256) + 1, 256, 0, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B, Cin, J);
   return (int)hipGetLastError();
 }
 

@@ -7,10 +7,12 @@ step is a static schedule of native kernels over persistent buffers:
             (batch stats + running-stat update) → bn_apply (+ReLU, +2x2 max-pool)
   head      fc_ce_train: Linear + softmax-CE loss, dlogits, dW, db, dx in two launches
   backward  per conv layer (reverse): bn_bwd (max-pool/ReLU routing recomputed from z, BN
-            backward, dgamma/dbeta/dbias) → dgrad (conv_fprop on flipped weights) → wgrad
-            (split-K implicit GEMM) — after each layer a ``grad_ready`` callback lets the
-            gradient-sync strategy launch that bucket's collective on the comm stream while the
-            remaining backward runs
+            backward, dgamma/dbeta/dbias) → wgrad (split-K implicit GEMM) → ``grad_ready``
+            callback (the gradient-sync strategy launches that bucket's collective on the comm
+            stream while the remaining backward runs) → dgrad (implicit GEMM reading the weights
+            with flipped taps; its split-K slabs are summed inside the next bn_bwd)
+  split-K   forward/dgrad partial slabs are never reduced by a separate pass: bn_fwd_stats /
+            bn_bwd sum them while computing their statistics
   update    sgd_flat over the flat parameter/grad/momentum arenas (one launch)
 
 Parameters/grads/momentum are three :class:`~distributed_pytorch_amd.utils.arena.Arena` s with
@@ -75,6 +77,7 @@ class VGGEngine:
         self.spec = VGGSpec.from_name(name, num_classes, in_hw)
         self.K = backend if backend is not None else (_ext.require() if self.device.type == "cuda" else cpu_ref)
         self.max_batch = max_batch
+        self._cfg_cache: Dict[tuple, tuple] = {}
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
         self.bn_momentum, self.bn_eps = bn_momentum, bn_eps
         self.num_classes = num_classes
@@ -100,7 +103,7 @@ class VGGEngine:
         f32 = dict(device=dev, dtype=torch.float32)
         self.x0 = torch.zeros(N, in_hw, in_hw, 4, **f32)
         self.target = torch.zeros(N, dtype=torch.int64, device=dev)
-        self.z, self.a, self.g, self.dz, self.wflip = [], [], [], [], []
+        self.z, self.a, self.g, self.dz = [], [], [], []
         self.stats = []  # per layer dict(mean, invstd, scale, shift)
         self.eval_ss = []
         slab_need, part_need = 1, 1
@@ -110,17 +113,18 @@ class VGGEngine:
             self.a.append(torch.empty(N, ho, ho, l.cout, **f32))
             self.g.append(torch.empty(N, ho, ho, l.cout, **f32))
             self.dz.append(torch.empty(N, hw, hw, l.cout, **f32))
-            self.wflip.append(torch.empty(l.cin_pad, 3, 3, l.cout, **f32))
             self.stats.append({k: torch.zeros(l.cout, **f32) for k in ("mean", "invstd", "scale", "shift")})
             self.eval_ss.append({k: torch.zeros(l.cout, **f32) for k in ("scale", "shift")})
             M = N * hw * hw
             for kind, (m, n, k) in (("fprop", (M, l.cout, 9 * l.cin_pad)), ("dgrad", (M, l.cin_pad, 9 * l.cout)),
                                     ("wgrad", (M, l.cout, 9 * l.cin_pad))):
-                _, s = conv_cfg("wgrad" if kind == "wgrad" else "fprop", m, n, k)
+                _, s = self._cfg("wgrad" if kind == "wgrad" else "fprop", m, n, k)
                 out = m * n if kind != "wgrad" else n * k
                 if s > 1:
                     slab_need = max(slab_need, s * out)
-            part_need = max(part_need, 3 * ((M + 63) // 64) * l.cout)
+            Mo = N * ho * ho
+            part_need = max(part_need, 3 * ((M + 63) // 64) * l.cout, self.K.bn_part_floats(M, l.cout, False),
+                            self.K.bn_part_floats(Mo, l.cout, True))
         self.slab = torch.empty(slab_need, **f32)
         self.part = torch.empty(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -130,7 +134,6 @@ class VGGEngine:
         self.loss_accum = torch.zeros(1, **f32)
         self.correct = torch.zeros(N, dtype=torch.int32, device=dev)
         self.eval_acc = torch.zeros(2, **f32)
-        self._cfg_cache: Dict[tuple, tuple] = {}
         self._eval_dirty = True
         self.init_parameters(seed=None)
 
@@ -237,17 +240,23 @@ class VGGEngine:
 
     # ------------------------------------------------------------------ kernel configs
     def _cfg(self, kind, M, N, K):
+        """(tile, effective split count) for a conv GEMM."""
         key = (kind, M, N, K)
         c = self._cfg_cache.get(key)
         if c is None:
-            c = conv_cfg(kind, M, N, K)
+            tile, s = conv_cfg(kind, M, N, K)
+            if kind != "wgrad":
+                s = self.K.conv_splits(K, s)
+            c = (tile, s)
             self._cfg_cache[key] = c
         return c
 
-    def _conv(self, x, w, out, l_cin, l_cout, hw, n):
+    def _conv(self, x, w, out, l_cin, l_cout, hw, n, reduce=True):
+        """Forward conv; returns the split count left UNREDUCED in self.slab (1 = result in out)."""
         M = n * hw * hw
         tile, s = self._cfg("fprop", M, l_cout, 9 * l_cin)
-        self.K.conv_fprop(x, w, out, self.slab if s > 1 else None, 1, 1, s, tile)
+        self.K.conv_fprop(x, w, out, self.slab if s > 1 else None, 1, 1, s, tile, False, reduce)
+        return 1 if (reduce or s == 1) else s
 
     def _wgrad(self, x, dz, dw, cin, cout, hw, n):
         M = n * hw * hw
@@ -269,8 +278,9 @@ class VGGEngine:
         inp = x
         for i, l in enumerate(L):
             z, a, st = self.z[i][:n], self.a[i][:n], self.stats[i]
-            self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n)
-            K.bn_fwd_stats(z, self.part, P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
+            ns = self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n, reduce=False)
+            K.bn_fwd_stats(self.slab if ns > 1 else z, ns, z, self.part, P[f"{l.bn_key}.weight"],
+                           P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                            self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"], self.bn_momentum,
                            self.bn_eps)
@@ -281,22 +291,27 @@ class VGGEngine:
                       self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
         if grad_ready is not None:
             grad_ready(["fc1.weight", "fc1.bias"])
+        gsplit = 1  # split-K slabs of g[i] left unreduced by the previous dgrad (summed inside bn_bwd)
         for i in range(len(L) - 1, -1, -1):
             l = L[i]
             st = self.stats[i]
             z, dz = self.z[i][:n], self.dz[i][:n]
-            K.bn_bwd(self.g[i][:n], z, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
-                     self.part, self.coef, G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"],
-                     dz, l.pool)
+            g = self.g[i][:n]
+            K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
+                     st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
+                     G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dz, l.pool)
             xin = x if i == 0 else self.a[i - 1][:n]
-            if i > 0:
-                K.wflip(P[f"{l.conv_key}.weight"], self.wflip[i])
-                M = n * l.hw * l.hw
-                tile, s = self._cfg("fprop", M, l.cin_pad, 9 * l.cout)
-                K.conv_fprop(dz, self.wflip[i], self.g[i - 1][:n], self.slab if s > 1 else None, 1, 1, s, tile)
+            # wgrad first: it must consume the slab workspace-free dz before the dgrad's split-K
+            # slabs (which bn_bwd of layer i-1 reads) are written
             self._wgrad(xin, dz, G[f"{l.conv_key}.weight"], l.cin_pad, l.cout, l.hw, n)
             if grad_ready is not None:
                 grad_ready([f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"])
+            if i > 0:
+                M = n * l.hw * l.hw
+                tile, s = self._cfg("fprop", M, l.cin_pad, 9 * l.cout)
+                K.conv_fprop(dz, P[f"{l.conv_key}.weight"], self.g[i - 1][:n], self.slab if s > 1 else None, 1, 1, s,
+                             tile, True, False)
+                gsplit = s
         self._eval_dirty = True
         return self.loss
 
@@ -329,7 +344,7 @@ class VGGEngine:
         inp = x
         for i, l in enumerate(self.spec.convs):
             z, a = self.z[i][:n], self.a[i][:n]
-            self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n)
+            self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n, reduce=True)
             self.K.bn_apply(z, a, self.eval_ss[i]["scale"], self.eval_ss[i]["shift"], l.pool)
             inp = a
         self.K.fc_ce_eval(inp.view(n, -1), P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n],

@@ -47,9 +47,23 @@ def mean_of_w(inp, out, W):
 
 
 # ---------------------------------------------------------------- convolution
-def conv_fprop(x, w, out, slab, stride, pad, splits=1, tile=0):
-    y = F.conv2d(_nchw(x), _nchw(w), stride=stride, padding=pad)
-    out.copy_(_nhwc(y))
+def conv_splits(Ktot, splits):
+    splits = max(1, splits)
+    kchunk = -(-(-(-Ktot // splits)) // 32) * 32
+    return -(-Ktot // kchunk)
+
+
+def conv_fprop(x, w, out, slab, stride, pad, splits=1, tile=0, dgrad=False, reduce=True):
+    if dgrad:  # w: the original conv's weights [C_in_of_this_gemm=K_orig, R, S, C_orig]
+        w = w.flip(1, 2).permute(3, 1, 2, 0)
+    y = _nhwc(F.conv2d(_nchw(x), _nchw(w), stride=stride, padding=pad))
+    eff = conv_splits(w.shape[1] * w.shape[2] * w.shape[3], splits)
+    if eff > 1 and not reduce:  # mirror the native contract: the slabs sum to the result
+        n = y.numel()
+        slab[:eff * n].zero_()
+        slab[:n].copy_(y.reshape(-1))
+        return
+    out.copy_(y)
 
 
 def conv_wgrad(x, dz, dw, slab, stride, pad, splits=1, tile=0):
@@ -63,12 +77,15 @@ def wflip(w, wd):
 
 
 # ---------------------------------------------------------------- batch norm
-def bn_nchunks(M):
-    return (M + CHUNK - 1) // CHUNK
+def bn_part_floats(M, C, bwd):
+    return (3 if bwd else 2) * C * ((M + CHUNK - 1) // CHUNK)
 
 
-def bn_fwd_stats(z, part, gamma, beta, bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps):
+def bn_fwd_stats(src, nsplit, z, part, gamma, beta, bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum,
+                 eps):
     C = z.shape[-1]
+    if nsplit > 1:
+        z.copy_(src[:nsplit * z.numel()].view(nsplit, -1).sum(0).view(z.shape))
     zz = z.reshape(-1, C).double()
     n = zz.shape[0]
     mu = zz.mean(0)
@@ -101,8 +118,12 @@ def bn_apply(z, a, scale, shift, pool):
     a.copy_(y.reshape(a.shape))
 
 
-def bn_bwd(g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool):
+def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool):
     N, H, W, C = z.shape
+    if nsplit > 1:
+        g.copy_(gsrc[:nsplit * g.numel()].view(nsplit, -1).sum(0).view(g.shape))
+    else:
+        g = gsrc
     with torch.enable_grad():
         u = (z * scale + shift).detach().requires_grad_(True)  # BN output, pre-ReLU
         y = torch.relu(u)

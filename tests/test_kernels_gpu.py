@@ -95,3 +95,28 @@ def test_conv_dgrad_via_flip(shape):
     C.conv_fprop(dzd, wflip, dx, None, 1, pd, 1, 0)
     torch.cuda.synchronize()
     assert rel_err(dx.permute(0, 3, 1, 2), gx) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [s for s in CONV_SHAPES if s[6] == 1 and 2 * s[7] == s[5] - 1])
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("tile", [0, 1])
+def test_conv_dgrad_mode(shape, splits, tile):
+    """dgrad=True reads the original KRSC weights with flipped taps (no transposed copy); with
+    reduce=False the split-K slabs must sum to the result."""
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(True)
+    w = torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, dy)
+    wk = w.float().permute(0, 2, 3, 1).contiguous().cuda()
+    dzd = dy.float().permute(0, 2, 3, 1).contiguous().cuda()
+    dx = torch.zeros(N, H, W, Cin, device="cuda")
+    eff = C.conv_splits(R * R * K, splits)
+    slab = torch.empty(eff * N * H * W * Cin, device="cuda") if eff > 1 else None
+    C.conv_fprop(dzd, wk, dx, slab, 1, pd, splits, tile, True, False)
+    torch.cuda.synchronize()
+    res = slab.view(eff, N, H, W, Cin).sum(0) if eff > 1 else dx
+    assert rel_err(res.permute(0, 3, 1, 2), gx) < 1e-5

@@ -40,14 +40,18 @@ def test_bn_forward(shape):
     Ho = H // 2 if pool else H
     a_ref = torch.empty(N, Ho, Ho if pool else W, C)
     rm_r, rv_r = rm.clone(), rv.clone()
-    cpu_ref.bn_fwd_stats(z, None, gamma, beta, bias, rm_r, rv_r, nbt, *outs_ref, 0.1, 1e-5)
+    cpu_ref.bn_fwd_stats(z, 1, z, None, gamma, beta, bias, rm_r, rv_r, nbt, *outs_ref, 0.1, 1e-5)
     cpu_ref.bn_apply(z, a_ref, outs_ref[2], outs_ref[3], pool)
     d = lambda t: t.cuda()
-    zd = d(z)
-    part = torch.empty(2 * C_.bn_nchunks(N * H * W) * C, device="cuda")
+    # exercise the fused split-K path: z arrives as 3 slabs that sum to it
+    sl = torch.randn(3, *z.shape, generator=g)
+    sl[2] = z - sl[0] - sl[1]
+    zd = torch.empty(z.shape, device="cuda")
+    part = torch.empty(C_.bn_part_floats(N * H * W, C, False), device="cuda")
     outs = [torch.zeros(C, device="cuda") for _ in range(4)]
     rm_d, rv_d, nbt_d = d(rm), d(rv), torch.zeros(1, dtype=torch.int64, device="cuda")
-    C_.bn_fwd_stats(zd, part, d(gamma), d(beta), d(bias), rm_d, rv_d, nbt_d, *outs, 0.1, 1e-5)
+    C_.bn_fwd_stats(d(sl.reshape(-1)), 3, zd, part, d(gamma), d(beta), d(bias), rm_d, rv_d, nbt_d, *outs, 0.1, 1e-5)
+    close(zd, z, 1e-5)
     a = torch.empty(a_ref.shape, device="cuda")
     C_.bn_apply(zd, a, outs[2], outs[3], pool)
     torch.cuda.synchronize()
@@ -72,15 +76,30 @@ def test_bn_backward(shape):
     gout = torch.randn(N, Ho, Wo, C, generator=g)
     ref = [torch.zeros(C) for _ in range(3)]
     dz_ref = torch.empty_like(z)
-    cpu_ref.bn_bwd(gout, z, scale, shift, mean, invstd, gamma, None, None, ref[0], ref[1], ref[2], dz_ref, pool)
+    cpu_ref.bn_bwd(gout, 1, gout, z, scale, shift, mean, invstd, gamma, None, None, ref[0], ref[1], ref[2], dz_ref,
+                   pool)
     d = lambda t: t.cuda()
-    out = [torch.zeros(C, device="cuda") for _ in range(3)]
-    dz = torch.empty(z.shape, device="cuda")
-    part = torch.empty(3 * C_.bn_nchunks(N * Ho * Wo) * C, device="cuda")
+    part = torch.empty(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
     coef = torch.empty(3 * C, device="cuda")
-    C_.bn_bwd(d(gout), d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, out[0], out[1], out[2], dz,
-              pool)
-    torch.cuda.synchronize()
+    for nsplit in (1, 2):
+        out = [torch.zeros(C, device="cuda") for _ in range(3)]
+        dz = torch.empty(z.shape, device="cuda")
+        gbuf = torch.empty(gout.shape, device="cuda")
+        if nsplit == 1:
+            src = d(gout)
+            gbuf = src
+        else:
+            half = torch.randn(gout.shape, generator=g)
+            src = d(torch.stack([half, gout - half]).reshape(-1))
+        C_.bn_bwd(src, nsplit, gbuf, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, out[0],
+                  out[1], out[2], dz, pool)
+        torch.cuda.synchronize()
+        close(gbuf, gout, 1e-5)
+        close(dz, dz_ref, 2e-5)
+        close(out[0], ref[0], 2e-5)
+        close(out[1], ref[1], 2e-5)
+        assert out[2].abs().max().item() < 1e-3 * ref[0].abs().max().item() + 1e-4  # dbias ~ 0
+    return
     close(dz, dz_ref, 2e-5)
     close(out[0], ref[0], 2e-5)
     close(out[1], ref[1], 2e-5)
@@ -109,9 +128,10 @@ def test_bn_backward_matches_torch_autograd():
     d = lambda t: t.contiguous().cuda()
     out = [torch.zeros(C, device="cuda") for _ in range(3)]
     dz = torch.empty(z.shape, device="cuda")
-    part = torch.empty(3 * C_.bn_nchunks(N * H * W // 4) * C, device="cuda")
+    part = torch.empty(C_.bn_part_floats(N * H * W // 4, C, True), device="cuda")
     coef = torch.empty(3 * C, device="cuda")
-    C_.bn_bwd(d(gy.float().permute(0, 2, 3, 1)), d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef,
+    gg = d(gy.float().permute(0, 2, 3, 1))
+    C_.bn_bwd(gg, 1, gg, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef,
               out[0], out[1], out[2], dz, True)
     torch.cuda.synchronize()
     close(dz.permute(0, 3, 1, 2), gx, 1e-4)
