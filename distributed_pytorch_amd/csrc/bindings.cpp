@@ -12,10 +12,11 @@ int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float m
 int dpa_scale(float* x, long n, float sc, hipStream_t s);
 int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
-                   int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, hipStream_t st);
-int dpa_conv_splits(int Ktot, int splits);
+                   int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, int posmajor,
+                   hipStream_t st);
+int dpa_conv_splits(int Kred, int splits);
 int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int N, int H, int W, int C, int Kout,
-                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st);
+                   int R, int S, int stride, int pad, int splits, int tile, int posmajor, hipStream_t st);
 int dpa_wflip(const float* w, float* wd, int K, int R, int S, int C, hipStream_t st);
 long dpa_bn_part_floats(int M, int C, int bwd);
 int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M, int C, const float* gamma,
@@ -87,7 +88,7 @@ void mean_of_w(Tensor in, Tensor out, int64_t W) {
 // ---------------- convolution ----------------
 // x [N,H,W,C], w [K,R,S,C] (dgrad: the original conv's weights [C,R,S,K]), out [N,P,Q,K]
 void conv_fprop(Tensor x, Tensor w, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile,
-                bool dgrad, bool reduce) {
+                bool dgrad, bool reduce, bool posmajor) {
   need(x, "x");
   need(w, "w");
   need(out, "out");
@@ -112,14 +113,15 @@ void conv_fprop(Tensor x, Tensor w, Tensor out, OptT slab, int64_t stride, int64
     sl = fp(*slab);
   }
   chk(dpa_conv_fprop(fp(x), fp(w), fp(out), sl, N, H, W, C, K, R, S, (int)stride, (int)pad, (int)splits, (int)tile,
-                     dgrad ? 1 : 0, reduce ? 1 : 0, cur_stream()),
+                     dgrad ? 1 : 0, reduce ? 1 : 0, posmajor ? 1 : 0, cur_stream()),
       "conv_fprop");
 }
 
-int64_t conv_splits(int64_t Ktot, int64_t splits) { return dpa_conv_splits((int)Ktot, (int)splits); }
+int64_t conv_splits(int64_t Kred, int64_t splits) { return dpa_conv_splits((int)Kred, (int)splits); }
 
 // x [N,H,W,C], dz [N,P,Q,K], dw [K,R,S,C]
-void conv_wgrad(Tensor x, Tensor dz, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile) {
+void conv_wgrad(Tensor x, Tensor dz, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits, int64_t tile,
+                bool posmajor) {
   need(x, "x");
   need(dz, "dz");
   need(dw, "dw");
@@ -129,14 +131,15 @@ void conv_wgrad(Tensor x, Tensor dz, Tensor dw, OptT slab, int64_t stride, int64
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   TORCH_CHECK(dz.size(1) == P && dz.size(2) == Q, "conv_wgrad: dz spatial");
   float* sl = nullptr;
-  if (splits > 1) {
-    TORCH_CHECK(slab.has_value(), "conv_wgrad: split-K needs a slab workspace");
+  const int eff = dpa_conv_splits(N * P * Q, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_wgrad: split-K needs a slab workspace");
     need(*slab, "slab");
-    TORCH_CHECK(slab->numel() >= splits * (int64_t)K * R * S * C, "conv_wgrad: slab too small");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * K * R * S * C, "conv_wgrad: slab too small");
     sl = fp(*slab);
   }
   chk(dpa_conv_wgrad(fp(x), fp(dz), fp(dw), sl, N, H, W, C, K, R, S, (int)stride, (int)pad, (int)splits, (int)tile,
-                     cur_stream()),
+                     posmajor ? 1 : 0, cur_stream()),
       "conv_wgrad");
 }
 
@@ -358,10 +361,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("scale_", &scale_);
   m.def("mean_of_w", &mean_of_w);
   m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
-        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("dgrad") = false, py::arg("reduce") = true);
+        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("dgrad") = false, py::arg("reduce") = true,
+        py::arg("posmajor") = false);
   m.def("conv_splits", &conv_splits);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dz"), py::arg("dw"), py::arg("slab"), py::arg("stride"),
-        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0);
+        py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
   m.def("wflip", &wflip);
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);

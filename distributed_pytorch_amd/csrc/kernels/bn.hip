@@ -36,10 +36,10 @@ __host__ __device__ inline RedGeom red_geom(int C) {
   return g;
 }
 
-// rows per block so that the grid has ~2048 blocks (at least one full iteration per block)
+// rows per block so that the grid has ~1024 blocks (at least one full iteration per block)
 __host__ inline int red_rows_per_block(int M, int C) {
   const RedGeom g = red_geom(C);
-  int rpb = (M + 2047) / 2048;
+  int rpb = (M + 1023) / 1024;
   rpb = ((rpb + g.RPI - 1) / g.RPI) * g.RPI;
   return rpb < g.RPI ? g.RPI : rpb;
 }
@@ -125,8 +125,8 @@ __device__ __forceinline__ Welford merge(Welford a, Welford b) {
   return r;
 }
 
-// 16 channels x 16 partial-groups per block: coalesced 128-B reads of the partials, Chan merge,
-// then scale/shift + running-stat update.
+// 8 channels x 32 partial-groups per block (32-B coalesced partial reads, 4 loads in flight per
+// thread), Chan merge, then scale/shift + running-stat update.
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restrict__ part, int nblk, int rpb, int M,
                                                           int C, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta,
@@ -135,20 +135,30 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
                                                           float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float momentum, float eps) {
-  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int cl = threadIdx.x & 7, grp = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
   Welford acc{0.f, 0.f, 0.f};
   if (c < C) {
-    for (int k = grp; k < nblk; k += 16) {
+    int k = grp;
+    for (; k + 96 < nblk; k += 128) {
+      float2 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p[u] = part[(long)(k + 32 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kk = k + 32 * u;
+        acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
+      }
+    }
+    for (; k < nblk; k += 32) {
       const float2 p = part[(long)k * C + c];
-      const int cnt = min(rpb, M - k * rpb);
-      acc = merge(acc, Welford{(float)cnt, p.x, p.y});
+      acc = merge(acc, Welford{(float)min(rpb, M - k * rpb), p.x, p.y});
     }
   }
   __shared__ Welford sh[256];
   sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int o = 128; o >= 16; o >>= 1) {
+  for (int o = 128; o >= 8; o >>= 1) {
     if ((int)threadIdx.x < o) sh[threadIdx.x] = merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
@@ -331,18 +341,35 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 }
 
 // Per channel: sum the block partials (fixed order -> deterministic), emit dgamma, dbeta, dbias and
-// the dz coefficients: dz = k1*dy + k2*z + k3.   16 channels x 16 groups per block.
+// the dz coefficients: dz = k1*dy + k2*z + k3.   8 channels x 32 groups per block.
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                               float Mfull, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ dbias, float* __restrict__ coef) {
-  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int cl = threadIdx.x & 7, grp = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
   float a = 0.f, b = 0.f, x = 0.f;
   if (c < C) {
-    for (int k = grp; k < nblk; k += 16) {
+    int k = grp;
+    for (; k + 96 < nblk; k += 128) {
+      float pa[4], pb[4], px[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* p = part + (long)(k + 32 * u) * 3 * C + c;
+        pa[u] = p[0];
+        pb[u] = p[C];
+        px[u] = p[2 * C];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a += pa[u];
+        b += pb[u];
+        x += px[u];
+      }
+    }
+    for (; k < nblk; k += 32) {
       const float* p = part + (long)k * 3 * C + c;
       a += p[0];
       b += p[C];
@@ -354,7 +381,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   sh[1][threadIdx.x] = b;
   sh[2][threadIdx.x] = x;
   __syncthreads();
-  for (int o = 128; o >= 16; o >>= 1) {
+  for (int o = 128; o >= 8; o >>= 1) {
     if ((int)threadIdx.x < o) {
       sh[0][threadIdx.x] += sh[0][threadIdx.x + o];
       sh[1][threadIdx.x] += sh[1][threadIdx.x + o];
@@ -459,7 +486,7 @@ int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M,
   const int rpb = red_rows_per_block(M, C);
   const int nblk = (M + rpb - 1) / rpb;
   bn_stats_kernel<<<nblk, 256, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C, rpb);
-  bn_finalize_kernel<<<cdiv(C, 16), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
+  bn_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
                                                   bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
   return (int)hipGetLastError();
 }
@@ -498,7 +525,7 @@ int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const fl
   else
     bn_bwd_reduce_kernel<false><<<nblk, 256, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W,
                                                       C, rpb);
-  bn_bwd_finalize_kernel<<<cdiv(C, 16), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
+  bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
                                                       dbeta, dbias, coef);
   const float* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);

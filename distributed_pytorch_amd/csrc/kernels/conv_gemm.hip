@@ -17,6 +17,14 @@
 // half h) so that one ds_read_b128 feeds 4 MFMAs.  The permutation is applied identically to A
 // and B, so the sum over k is unchanged (and each MFMA is still an exact f32 fma chain).
 //
+// Position-major rows + tap skipping (posmajor=1).  The GEMM row index m is ordered
+// (oh, ow, img) instead of (img, oh, ow), so a BM-row tile holds ONE output pixel position of BM
+// images.  Every row of the tile then has the same set of in-bounds filter taps, and k-tiles of
+// taps that fall entirely into the zero padding are skipped instead of multiplied by zeros: on
+// 2x2 feature maps only 4 of 9 taps are real (2.25x less MFMA work), 4x4 → 0.69, 8x8 → 0.84.
+// WGRAD skips the (position, tap) pairs the same way over its m reduction.  Results are written
+// in NHWC memory order whatever the row order, so consumers never see the permutation.
+//
 // LDS images: a k-contiguous operand is stored [row][BK+4] (16-row b128 lane groups hit 16
 // distinct 16-B slots: conflict-free), a row-contiguous operand (WGRAD A/B, DGRAD B) [BK][rows+4].
 #include "common.h"
@@ -52,19 +60,20 @@ __device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) {
 }
 
 struct ConvArgs {
-  const float* x;   // FPROP: input NHWC [N,H,W,C]        WGRAD: input NHWC (B operand)
-  const float* w;   // FPROP: weights [Nout][Ktot]         WGRAD: dZ [M][Kout] (A operand)
-  float* out;       // FPROP: out [M][Nout] or slabs       WGRAD: dW [Kout][Ktot] or slabs
+  const float* x;   // FPROP/DGRAD: GEMM input NHWC [N,H,W,C]     WGRAD: input NHWC (B operand)
+  const float* w;   // FPROP: weights [Nout][Ktot]; DGRAD: orig weights [C][R][S][Nout]; WGRAD: dZ [N,P,Q,Kout]
+  float* out;       // FPROP/DGRAD: out NHWC [N,P,Q,Nout] or slabs    WGRAD: dW [Kout][Ktot] or slabs
   int N, H, W, C;   // input dims
   int P, Q;         // output spatial dims
   int R, S, stride, pad;
   int M;            // N*P*Q
-  int Nout;         // FPROP: output channels; WGRAD: Kout
+  int Nout;         // FPROP/DGRAD: output channels; WGRAD: Kout
   int Ktot;         // R*S*C
   int gm, gn;       // tile grid
-  int kchunk;       // split-K chunk (multiple of BK), reduction index range per split
-  long slab;        // elements per split slab (0 when splitK==1)
-  FastDiv fd_C, fd_S, fd_Q, fd_PQ;
+  int splits;       // split-K factor (tiles of the reduction are partitioned over blockIdx.y)
+  int posmajor;     // row order (oh,ow,img) + tap skipping (see header)
+  long slab;        // elements per split slab (0 when splits==1)
+  FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
 };
 
 template <int ROWS, int THREADS>
@@ -85,6 +94,21 @@ struct RowContigSlots {  // a row-contiguous operand tile BK x ROWS, loaded as f
 };
 
 __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// logical GEMM row m -> (img, oh, ow)
+__device__ __forceinline__ void decode_row(const ConvArgs& a, unsigned m, unsigned& img, unsigned& oh,
+                                           unsigned& ow) {
+  unsigned pos;
+  if (a.posmajor) {
+    pos = fdiv(m, a.fd_N);
+    img = m - pos * (unsigned)a.N;
+  } else {
+    img = fdiv(m, a.fd_PQ);
+    pos = m - img * (unsigned)(a.P * a.Q);
+  }
+  oh = fdiv(pos, a.fd_Q);
+  ow = pos - oh * (unsigned)a.Q;
+}
 
 enum { MODE_FPROP = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -112,28 +136,77 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
   const int bm = tile / a.gn, bn = tile % a.gn;
   const int m0 = bm * BM, n0 = bn * BN;
   const int split = blockIdx.y;
-  const int kbeg = split * a.kchunk;
-  int kend = kbeg + a.kchunk;
-  const int KRED = WGRAD ? a.M : a.Ktot;  // reduction length
-  if (kend > KRED) kend = KRED;
-  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  // ---------------- reduction tile iterator (virtual tile v -> reduction offset) ----------------
+  // FPROP/DGRAD reduce over k=(r,s,c); WGRAD over m.  With tap skipping the virtual tiles
+  // enumerate only the (tap x c-chunk) [FPROP/DGRAD] or (position x img-chunk) [WGRAD]
+  // combinations that can be non-zero for this block.
+  bool skip = false;
+  int lo0 = 0, lo1 = 0, span1 = 1, per = 1;  // rectangle origin, inner span, tiles per cell
+  int ntot;
+  if constexpr (!WGRAD) {
+    ntot = (a.Ktot + BK - 1) / BK;
+    if (a.posmajor && a.C % BK == 0 && a.N % BM == 0) {
+      const int pos = m0 / a.N;
+      const int oh = pos / a.Q, ow = pos - (pos / a.Q) * a.Q;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      const int r_lo = max(0, -ih0), r_hi = min(a.R, a.H - ih0);
+      const int s_lo = max(0, -iw0), s_hi = min(a.S, a.W - iw0);
+      skip = true;
+      lo0 = r_lo;
+      lo1 = s_lo;
+      span1 = max(0, s_hi - s_lo);
+      per = a.C / BK;
+      ntot = max(0, r_hi - r_lo) * span1 * per;
+    }
+  } else {
+    ntot = (a.M + BK - 1) / BK;
+    if (a.posmajor && a.C % BN == 0 && a.N % BK == 0) {
+      const int tap = n0 / a.C;  // the block's rsc columns share one tap
+      const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
+      // positions with ih = oh*st - pad + r in [0, H)
+      const int oh_lo = max(0, (a.pad - r + a.stride - 1) / a.stride);
+      const int oh_hi = min(a.P, (a.H - 1 + a.pad - r) / a.stride + 1);
+      const int ow_lo = max(0, (a.pad - s + a.stride - 1) / a.stride);
+      const int ow_hi = min(a.Q, (a.W - 1 + a.pad - s) / a.stride + 1);
+      skip = true;
+      lo0 = oh_lo;
+      lo1 = ow_lo;
+      span1 = max(0, ow_hi - ow_lo);
+      per = a.N / BK;
+      ntot = max(0, oh_hi - oh_lo) * span1 * per;
+    }
+  }
+  const int tchunk = (ntot + a.splits - 1) / a.splits;
+  const int vbeg = split * tchunk;
+  const int vend = min(ntot, vbeg + tchunk);
+  const int ntiles = max(0, vend - vbeg);
+  auto tile_off = [&](int v) -> int {  // reduction offset (k for FPROP/DGRAD, m for WGRAD)
+    if (!skip) return v * BK;
+    const int cell = v / per, sub = v - (v / per) * per;
+    const int i0 = lo0 + cell / span1, i1 = lo1 + cell % span1;
+    if constexpr (!WGRAD)
+      return (i0 * a.S + i1) * a.C + sub * BK;  // (r, s, c-chunk)
+    else
+      return (i0 * a.Q + i1) * a.N + sub * BK;  // (oh, ow, img-chunk), posmajor m order
+  };
+  const int KMAX = WGRAD ? a.M : a.Ktot;
 
   // ---------------- per-thread load-slot precomputation ----------------
-  // A operand
   using ASl = typename std::conditional<WGRAD, RowContigSlots<BM, THREADS>, KContigSlots<BM, THREADS>>::type;
   using BSl = typename std::conditional<B_ROWC, RowContigSlots<BN, THREADS>, KContigSlots<BN, THREADS>>::type;
   constexpr int NA = ASl::NSLOT, NB = BSl::NSLOT;
 
   float4 ra[NA], rb[NB];
 
-  // FPROP A slots: rows m, fixed k4
+  // FPROP/DGRAD A slots: rows m, fixed k4
   int a_img[WGRAD ? 1 : NA], a_ih0[WGRAD ? 1 : NA], a_iw0[WGRAD ? 1 : NA];
   int a_k4 = 0;
   // WGRAD A slots: fixed kout column group, k rows vary
   int a_col = 0, a_krow = 0;
   // FPROP B slots: rows n (weights), fixed k4
   int b_k4 = 0, b_row0 = 0;
-  // WGRAD B slots: fixed rsc column group
+  // WGRAD/DGRAD B slots: fixed column group
   int b_rr = 0, b_ss = 0, b_c = 0, b_colvalid = 0, b_krow = 0;
 
   if constexpr (!WGRAD) {
@@ -143,10 +216,8 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
     for (int j = 0; j < NA; ++j) {
       const int m = m0 + r0 + j * ASl::ROW_STEP;
       if (m < a.M) {
-        const unsigned img = fdiv((unsigned)m, a.fd_PQ);
-        const unsigned rem = (unsigned)m - img * (unsigned)(a.P * a.Q);
-        const unsigned oh = fdiv(rem, a.fd_Q);
-        const unsigned ow = rem - oh * (unsigned)a.Q;
+        unsigned img, oh, ow;
+        decode_row(a, (unsigned)m, img, oh, ow);
         a_img[j] = (int)img;
         a_ih0[j] = (int)oh * a.stride - a.pad;
         a_iw0[j] = (int)ow * a.stride - a.pad;
@@ -177,11 +248,11 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
     b_krow = tid / BSl::F4_PER_K;
   }
 
-  auto load_tile = [&](int kt) {
-    const int kb = kbeg + kt * BK;
+  auto load_tile = [&](int v) {
+    const int kb = tile_off(vbeg + v);
     if constexpr (!WGRAD) {
       const int k = kb + a_k4 * 4;
-      const bool kval = k < kend;
+      const bool kval = k < KMAX;
       const unsigned tap = fdiv((unsigned)k, a.fd_C);
       const int c = k - (int)tap * a.C;
       const unsigned r = fdiv(tap, a.fd_S);
@@ -194,7 +265,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
       }
       if constexpr (MODE == MODE_FPROP) {
         const int kb4 = kb + b_k4 * 4;
-        const bool kbv = kb4 < kend;
+        const bool kbv = kb4 < KMAX;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           const int n = n0 + b_row0 + j * BSl::ROW_STEP;
@@ -210,28 +281,28 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
           const int kk = k - (int)tp * a.C;
           const unsigned rr = fdiv(tp, a.fd_S);
           const int ss = (int)(tp - rr * a.S);
-          const bool v = k < kend && b_colvalid;
+          const bool v = k < KMAX && b_colvalid;
           rb[j] = v ? ldg4(a.w + (((long)kk * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + b_c)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
     } else {
-      // A = dZ^T : element (kout, m) = dZ[m][kout]
+      // A = dZ^T : element (kout, m) = dZ[row(m)][kout];  B = Xcol^T : (rsc, m) = X[img, ih, iw, c]
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
         const int m = kb + a_krow + j * ASl::K_STEP;
-        const bool v = m < kend && a_col < a.Nout;
-        ra[j] = v ? ldg4(a.w + (long)m * a.Nout + a_col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bool v = m < KMAX && a_col < a.Nout;
+        unsigned img = 0, oh = 0, ow = 0;
+        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        const long row = ((long)img * a.P + oh) * a.Q + ow;
+        ra[j] = v ? ldg4(a.w + row * a.Nout + a_col) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      // B = Xcol^T : element (rsc, m) = X[img, oh*st-pad+r, ow*st-pad+s, c]
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int m = kb + b_krow + j * BSl::K_STEP;
-        bool v = m < kend && b_colvalid;
-        const unsigned img = fdiv((unsigned)m, a.fd_PQ);
-        const unsigned rem = (unsigned)m - img * (unsigned)(a.P * a.Q);
-        const unsigned oh = fdiv(rem, a.fd_Q);
-        const unsigned ow = rem - oh * (unsigned)a.Q;
+        bool v = m < KMAX && b_colvalid;
+        unsigned img = 0, oh = 0, ow = 0;
+        if (v) decode_row(a, (unsigned)m, img, oh, ow);
         const int ih = (int)oh * a.stride + b_rr, iw = (int)ow * a.stride + b_ss;
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         rb[j] = v ? ldg4(a.x + (((long)img * a.H + ih) * a.W + iw) * a.C + b_c) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -327,10 +398,13 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
   }
 
   // ---------------- epilogue: C[row][col], row over BM (A rows), col over BN (B rows) ----------
+  // FPROP/DGRAD rows are logical GEMM rows, stored at their NHWC memory row.
   float* out = a.out + (long)split * a.slab;
   const int ldc = WGRAD ? a.Ktot : a.Nout;
   const int nrows = WGRAD ? a.Nout : a.M;
   const int ncols = WGRAD ? a.Ktot : a.Nout;
+  const bool remap = !WGRAD && a.posmajor;
+  const int PQ = a.P * a.Q;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -340,7 +414,14 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < nrows) out[(long)row * ldc + col] = acc[i][j][r];
+          if (row < nrows) {
+            long mrow = row;
+            if (remap) {
+              const unsigned pos = fdiv((unsigned)row, a.fd_N);
+              mrow = (long)(row - (int)pos * a.N) * PQ + pos;
+            }
+            out[mrow * ldc + col] = acc[i][j][r];
+          }
         }
       }
     }
@@ -381,8 +462,8 @@ __global__ __launch_bounds__(256) void wflip_kernel(const float* __restrict__ w,
 }
 
 template <int BM, int BN, int WM, int WN, int MODE>
-int launch_cfg(const ConvArgs& a, int splits, hipStream_t st) {
-  dim3 grid(a.gm * a.gn, splits);
+int launch_cfg(const ConvArgs& a, hipStream_t st) {
+  dim3 grid(a.gm * a.gn, a.splits);
   conv_gemm_kernel<BM, BN, WM, WN, MODE><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
@@ -412,18 +493,29 @@ static void fill_geom(ConvArgs& a, int N, int H, int W, int C, int R, int S, int
   a.fd_S = make_fastdiv(S);
   a.fd_Q = make_fastdiv(a.Q);
   a.fd_PQ = make_fastdiv(a.P * a.Q);
+  a.fd_N = make_fastdiv(N);
 }
 
 extern "C" {
 
+// effective split count the launcher will use for a reduction of `ntiles_k` BK-tiles
+int dpa_conv_splits(int Kred, int splits) {
+  const int nt = cdiv(Kred, BK);
+  if (splits < 1) splits = 1;
+  if (splits > nt) splits = nt;
+  return splits < 1 ? 1 : splits;
+}
+
 // Forward conv (and, with dgrad=1, the stride-1 "same" data-gradient conv reading the ORIGINAL
 // weights with flipped taps).  x: NHWC [N,H,W,C]; w: fprop [Kout][R][S][C], dgrad [C][R][S][Kout]
 // (the original conv's weights, whose input channels Kout are this GEMM's outputs); out
-// [N,P,Q,Kout].  splits > 1: partial sums go to slab[splits][M][Kout]; reduce=1 sums them into
+// [N,P,Q,Kout].  splits > 1: partial sums go to slab[splits][N,P,Q,Kout]; reduce=1 sums them into
 // out here, reduce=0 leaves them for a consumer that sums on the fly (bn_fwd_stats / bn_bwd).
 // tile: 0 -> 128x128 (4 waves, 64x64 each), 1 -> 64x64 (4 waves, 32x32 each)
+// posmajor: position-major row order + tap skipping (any value is correct; 1 is faster on small maps)
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
-                   int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, hipStream_t st) {
+                   int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, int posmajor,
+                   hipStream_t st) {
   ConvArgs a{};
   a.x = x;
   a.w = w;
@@ -434,37 +526,27 @@ int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int 
   const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
   a.gm = cdiv(a.M, BMv);
   a.gn = cdiv(Kout, BNv);
-  if (splits < 1) splits = 1;
-  a.kchunk = cdiv(cdiv(a.Ktot, splits), BK) * BK;
-  splits = cdiv(a.Ktot, a.kchunk);
-  a.out = splits > 1 ? slab : out;
-  a.slab = splits > 1 ? (long)a.M * Kout : 0;
+  a.splits = dpa_conv_splits(a.Ktot, splits);
+  a.posmajor = posmajor ? 1 : 0;
+  a.out = a.splits > 1 ? slab : out;
+  a.slab = a.splits > 1 ? (long)a.M * Kout : 0;
   int rc;
   if (dgrad)
-    rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_DGRAD>(a, splits, st)
-                   : launch_cfg<64, 64, 2, 2, MODE_DGRAD>(a, splits, st);
+    rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_DGRAD>(a, st) : launch_cfg<64, 64, 2, 2, MODE_DGRAD>(a, st);
   else
-    rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_FPROP>(a, splits, st)
-                   : launch_cfg<64, 64, 2, 2, MODE_FPROP>(a, splits, st);
+    rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_FPROP>(a, st) : launch_cfg<64, 64, 2, 2, MODE_FPROP>(a, st);
   if (rc) return rc;
-  if (splits > 1 && reduce) {
+  if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * Kout / 4;
-    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, splits);
+    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, a.splits);
     rc = (int)hipGetLastError();
   }
   return rc;
 }
 
-// effective split count the launcher will use (the K range is rounded to BK multiples)
-int dpa_conv_splits(int Ktot, int splits) {
-  if (splits < 1) splits = 1;
-  const int kchunk = cdiv(cdiv(Ktot, splits), BK) * BK;
-  return cdiv(Ktot, kchunk);
-}
-
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] * Xcol[m][rsc]
 int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int N, int H, int W, int C, int Kout,
-                   int R, int S, int stride, int pad, int splits, int tile, hipStream_t st) {
+                   int R, int S, int stride, int pad, int splits, int tile, int posmajor, hipStream_t st) {
   ConvArgs a{};
   a.x = x;
   a.w = dz;
@@ -474,17 +556,15 @@ int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int 
   const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
   a.gm = cdiv(Kout, BMv);
   a.gn = cdiv(a.Ktot, BNv);
-  if (splits < 1) splits = 1;
-  a.kchunk = cdiv(cdiv(a.M, splits), BK) * BK;
-  splits = cdiv(a.M, a.kchunk);
-  a.out = splits > 1 ? slab : dw;
-  a.slab = splits > 1 ? (long)Kout * a.Ktot : 0;
-  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_WGRAD>(a, splits, st)
-                     : launch_cfg<64, 64, 2, 2, MODE_WGRAD>(a, splits, st);
+  a.splits = dpa_conv_splits(a.M, splits);
+  a.posmajor = posmajor ? 1 : 0;
+  a.out = a.splits > 1 ? slab : dw;
+  a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
+  int rc = tile == 0 ? launch_cfg<128, 128, 2, 2, MODE_WGRAD>(a, st) : launch_cfg<64, 64, 2, 2, MODE_WGRAD>(a, st);
   if (rc) return rc;
-  if (splits > 1) {
+  if (a.splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;
-    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, splits);
+    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, a.splits);
     rc = (int)hipGetLastError();
   }
   return rc;

@@ -80,39 +80,42 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
   }
 }
 
-// grid: cdiv(Cin,256) + 1 blocks.  Column blocks compute dW[:, c] for one c per thread (dlogits
-// staged through LDS 64 rows at a time, x read coalesced); the last block reduces db and the loss.
+// grid: cdiv(Cin,16) + 1 blocks of 256 threads = 16 columns x 16 row-groups.  Each thread sums
+// its rows (independent loads in flight), the row-groups are combined through LDS in a fixed order
+// (deterministic).  The last block reduces db and the batch-mean loss.
 __global__ __launch_bounds__(256) void fc_ce_wgrad_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ dlogits,
                                                           const float* __restrict__ loss_row, float* __restrict__ dw,
                                                           float* __restrict__ db, float* __restrict__ loss_out,
                                                           float* __restrict__ loss_accum, int B, int Cin, int J) {
-  const int ncb = (Cin + 255) / 256;
+  const int ncb = (Cin + 15) / 16;
   const int t = threadIdx.x;
   if ((int)blockIdx.x < ncb) {
-    __shared__ float sdl[64 * MAXJ];
-    const int c = blockIdx.x * 256 + t;
+    __shared__ float red[16][16][MAXJ + 1];
+    const int cl = t & 15, rg = t >> 4;
+    const int c = blockIdx.x * 16 + cl;
     float acc[MAXJ];
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) acc[j] = 0.f;
-    for (int b0 = 0; b0 < B; b0 += 64) {
-      const int nb = min(64, B - b0);
-      for (int e = t; e < nb * J; e += 256) sdl[(e / J) * MAXJ + e % J] = dlogits[(long)b0 * J + e];
-      __syncthreads();
-      if (c < Cin) {
-        for (int b = 0; b < nb; ++b) {
-          const float xv = x[(long)(b0 + b) * Cin + c];
-#pragma unroll
-          for (int j = 0; j < MAXJ; ++j)
-            if (j < J) acc[j] = fmaf(sdl[b * MAXJ + j], xv, acc[j]);
-        }
-      }
-      __syncthreads();
-    }
     if (c < Cin) {
+#pragma unroll 4
+      for (int b = rg; b < B; b += 16) {
+        const float xv = x[(long)b * Cin + c];
+        const float* dl = dlogits + (long)b * J;
 #pragma unroll
-      for (int j = 0; j < MAXJ; ++j)
-        if (j < J) dw[(long)j * Cin + c] = acc[j];
+        for (int j = 0; j < MAXJ; ++j)
+          if (j < J) acc[j] = fmaf(dl[j], xv, acc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) red[rg][cl][j] = acc[j];
+    __syncthreads();
+    if (t < 16 * J) {
+      const int j = t / 16, cc = t % 16;
+      float s = 0.f;
+      for (int k = 0; k < 16; ++k) s += red[k][cc][j];
+      const int col = blockIdx.x * 16 + cc;
+      if (col < Cin) dw[(long)j * Cin + col] = s;
     }
   } else {
     __shared__ float sh[256];
@@ -182,7 +185,7 @@ int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long l
   if (J > MAXJ) return -2;
   fc_ce_rows_kernel<true><<<cdiv(B, 4), 256, 0, st>>>(x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin,
                                                       J);
-  fc_ce_wgrad_kernel<<<cdiv(Cin, 256) + 1, 256, 0, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B, Cin, J);
+  fc_ce_wgrad_kernel<<<cdiv(Cin, 16) + 1, 256, 0, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B, Cin, J);
   return (int)hipGetLastError();
 }
 

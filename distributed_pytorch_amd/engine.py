@@ -245,23 +245,28 @@ class VGGEngine:
         c = self._cfg_cache.get(key)
         if c is None:
             tile, s = conv_cfg(kind, M, N, K)
-            if kind != "wgrad":
-                s = self.K.conv_splits(K, s)
+            s = self.K.conv_splits(M if kind == "wgrad" else K, s)
             c = (tile, s)
             self._cfg_cache[key] = c
         return c
+
+    @staticmethod
+    def _posmajor(hw: int) -> bool:
+        """Position-major GEMM rows + padding-tap skipping pays on small feature maps
+        (conv_gemm.hip header: 2x2 maps do 4/9 of the taps)."""
+        return hw <= 8
 
     def _conv(self, x, w, out, l_cin, l_cout, hw, n, reduce=True):
         """Forward conv; returns the split count left UNREDUCED in self.slab (1 = result in out)."""
         M = n * hw * hw
         tile, s = self._cfg("fprop", M, l_cout, 9 * l_cin)
-        self.K.conv_fprop(x, w, out, self.slab if s > 1 else None, 1, 1, s, tile, False, reduce)
+        self.K.conv_fprop(x, w, out, self.slab if s > 1 else None, 1, 1, s, tile, False, reduce, self._posmajor(hw))
         return 1 if (reduce or s == 1) else s
 
     def _wgrad(self, x, dz, dw, cin, cout, hw, n):
         M = n * hw * hw
         tile, s = self._cfg("wgrad", M, cout, 9 * cin)
-        self.K.conv_wgrad(x, dz, dw, self.slab if s > 1 else None, 1, 1, s, tile)
+        self.K.conv_wgrad(x, dz, dw, self.slab if s > 1 else None, 1, 1, s, tile, self._posmajor(hw))
 
     # ------------------------------------------------------------------ training step
     def forward_backward(self, x: torch.Tensor, target: torch.Tensor,
@@ -310,7 +315,7 @@ class VGGEngine:
                 M = n * l.hw * l.hw
                 tile, s = self._cfg("fprop", M, l.cin_pad, 9 * l.cout)
                 K.conv_fprop(dz, P[f"{l.conv_key}.weight"], self.g[i - 1][:n], self.slab if s > 1 else None, 1, 1, s,
-                             tile, True, False)
+                             tile, True, False, self._posmajor(l.hw))
                 gsplit = s
         self._eval_dirty = True
         return self.loss

@@ -47,13 +47,11 @@ def mean_of_w(inp, out, W):
 
 
 # ---------------------------------------------------------------- convolution
-def conv_splits(Ktot, splits):
-    splits = max(1, splits)
-    kchunk = -(-(-(-Ktot // splits)) // 32) * 32
-    return -(-Ktot // kchunk)
+def conv_splits(Kred, splits):
+    return max(1, min(max(1, splits), -(-Kred // 32)))
 
 
-def conv_fprop(x, w, out, slab, stride, pad, splits=1, tile=0, dgrad=False, reduce=True):
+def conv_fprop(x, w, out, slab, stride, pad, splits=1, tile=0, dgrad=False, reduce=True, posmajor=False):
     if dgrad:  # w: the original conv's weights [C_in_of_this_gemm=K_orig, R, S, C_orig]
         w = w.flip(1, 2).permute(3, 1, 2, 0)
     y = _nhwc(F.conv2d(_nchw(x), _nchw(w), stride=stride, padding=pad))
@@ -66,7 +64,7 @@ def conv_fprop(x, w, out, slab, stride, pad, splits=1, tile=0, dgrad=False, redu
     out.copy_(y)
 
 
-def conv_wgrad(x, dz, dw, slab, stride, pad, splits=1, tile=0):
+def conv_wgrad(x, dz, dw, slab, stride, pad, splits=1, tile=0, posmajor=False):
     K, R, S, C = dw.shape
     gw = torch.nn.grad.conv2d_weight(_nchw(x), (K, C, R, S), _nchw(dz), stride=stride, padding=pad)
     dw.copy_(_nhwc(gw))

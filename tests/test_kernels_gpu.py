@@ -36,10 +36,15 @@ CONV_SHAPES = [
 ]
 
 
+CONV_SHAPES += [(128, 4, 4, 32, 64, 3, 1, 1), (64, 2, 2, 64, 32, 3, 1, 1), (128, 8, 8, 32, 32, 3, 1, 1),
+                (64, 5, 5, 64, 64, 3, 2, 1)]
+
+
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
 @pytest.mark.parametrize("tile", [0, 1])
-def test_conv_fprop(shape, splits, tile):
+@pytest.mark.parametrize("posmajor", [False, True])
+def test_conv_fprop(shape, splits, tile, posmajor):
     C = _C()
     N, H, W, Cin, K, R, st, pd = shape
     g = torch.Generator().manual_seed(0)
@@ -51,7 +56,7 @@ def test_conv_fprop(shape, splits, tile):
     P, Q = ref.shape[2], ref.shape[3]
     out = torch.empty(N, P, Q, K, device="cuda")
     slab = torch.empty(splits * N * P * Q * K, device="cuda") if splits > 1 else None
-    C.conv_fprop(xd, wd, out, slab, st, pd, splits, tile)
+    C.conv_fprop(xd, wd, out, slab, st, pd, splits, tile, False, True, posmajor)
     torch.cuda.synchronize()
     assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-5
 
@@ -59,7 +64,8 @@ def test_conv_fprop(shape, splits, tile):
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 @pytest.mark.parametrize("splits", [1, 7])
 @pytest.mark.parametrize("tile", [0, 1])
-def test_conv_wgrad(shape, splits, tile):
+@pytest.mark.parametrize("posmajor", [False, True])
+def test_conv_wgrad(shape, splits, tile, posmajor):
     C = _C()
     N, H, W, Cin, K, R, st, pd = shape
     g = torch.Generator().manual_seed(1)
@@ -72,7 +78,7 @@ def test_conv_wgrad(shape, splits, tile):
     dzd = dy.float().permute(0, 2, 3, 1).contiguous().cuda()
     dw = torch.empty(K, R, R, Cin, device="cuda")
     slab = torch.empty(splits * K * R * R * Cin, device="cuda") if splits > 1 else None
-    C.conv_wgrad(xd, dzd, dw, slab, st, pd, splits, tile)
+    C.conv_wgrad(xd, dzd, dw, slab, st, pd, splits, tile, posmajor)
     torch.cuda.synchronize()
     assert rel_err(dw.permute(0, 3, 1, 2), gw) < 1e-5
 
@@ -100,7 +106,8 @@ def test_conv_dgrad_via_flip(shape):
 @pytest.mark.parametrize("shape", [s for s in CONV_SHAPES if s[6] == 1 and 2 * s[7] == s[5] - 1])
 @pytest.mark.parametrize("splits", [1, 4])
 @pytest.mark.parametrize("tile", [0, 1])
-def test_conv_dgrad_mode(shape, splits, tile):
+@pytest.mark.parametrize("posmajor", [False, True])
+def test_conv_dgrad_mode(shape, splits, tile, posmajor):
     """dgrad=True reads the original KRSC weights with flipped taps (no transposed copy); with
     reduce=False the split-K slabs must sum to the result."""
     C = _C()
@@ -116,7 +123,7 @@ def test_conv_dgrad_mode(shape, splits, tile):
     dx = torch.zeros(N, H, W, Cin, device="cuda")
     eff = C.conv_splits(R * R * K, splits)
     slab = torch.empty(eff * N * H * W * Cin, device="cuda") if eff > 1 else None
-    C.conv_fprop(dzd, wk, dx, slab, 1, pd, splits, tile, True, False)
+    C.conv_fprop(dzd, wk, dx, slab, 1, pd, splits, tile, True, False, posmajor)
     torch.cuda.synchronize()
     res = slab.view(eff, N, H, W, Cin).sum(0) if eff > 1 else dx
     assert rel_err(res.permute(0, 3, 1, 2), gx) < 1e-5

@@ -55,24 +55,24 @@ def main():
         best = {}
         for kind in ("fprop", "dgrad", "wgrad"):
             res = []
-            for tile in (0, 1):
+            for tile, pm in ((0, False), (1, False), (0, True), (1, True)):
                 for splits in (1, 2, 4, 8, 16, 32, 64, 128):
                     if kind == "fprop":
                         need = splits * M * K
                         slab = torch.empty(need, device="cuda") if splits > 1 else None
-                        fn = lambda: C.conv_fprop(x, w, z, slab, 1, 1, splits, tile)
+                        fn = lambda: C.conv_fprop(x, w, z, slab, 1, 1, splits, tile, False, True, pm)
                     elif kind == "dgrad":
                         need = splits * M * Cin
                         slab = torch.empty(need, device="cuda") if splits > 1 else None
-                        fn = lambda: (C.wflip(w, wf), C.conv_fprop(dz, wf, dx, slab, 1, 1, splits, tile))
+                        fn = lambda: C.conv_fprop(dz, w, dx, slab, 1, 1, splits, tile, True, True, pm)
                     else:
                         need = splits * K * 9 * Cin
                         slab = torch.empty(need, device="cuda") if splits > 1 else None
-                        fn = lambda: C.conv_wgrad(x, dz, dw, slab, 1, 1, splits, tile)
+                        fn = lambda: C.conv_wgrad(x, dz, dw, slab, 1, 1, splits, tile, pm)
                     if kind != "wgrad" and splits > 16:
                         continue
                     ms = timeit(fn, a.iters)
-                    res.append((ms, tile, splits))
+                    res.append((ms, tile, splits, pm))
             res.sort()
             best[kind] = res[0]
         # MIOpen reference (NCHW-logical, channels_last memory)
@@ -88,7 +88,7 @@ def main():
         tot["ours"] += ours
         tot["miopen"] += mi_f + mi_b
         print(json.dumps({"H": H, "Cin": Cin, "K": K, "gflop": flops / 1e9,
-                          "best": {k: {"ms": round(v[0], 4), "tile": v[1], "splits": v[2],
+                          "best": {k: {"ms": round(v[0], 4), "tile": v[1], "splits": v[2], "posmajor": v[3],
                                        "tflops": round(flops / v[0] / 1e9, 1)} for k, v in best.items()},
                           "miopen_fwd_ms": round(mi_f, 4), "miopen_bwd_ms": round(mi_b, 4)}), flush=True)
     print(json.dumps({"total_ms": {k: round(v, 3) for k, v in tot.items()}}))
