@@ -34,6 +34,16 @@ int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long l
                     int Cin, int J, hipStream_t st);
 int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                    int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st);
+int dpa_x3_splits(int Kred, int splits);
+int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w, long wps, float* out, float* slab,
+                      int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
+                      int reduce, int posmajor, int np, hipStream_t st);
+int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* dz, long dzps, float* dw, float* slab,
+                      int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
+                      int posmajor, int np, hipStream_t st);
+int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
+int dpa_split_weights(const float* w, unsigned short* w3, unsigned short* wd3, int K, int R, int S, int C, int np,
+                      hipStream_t st);
 int dpa_augment(const unsigned char* img, const long long* idx, const long long* labels, float* out,
                 long long* target, int B, int Hs, int Ws, int pad, int train, unsigned long long seed,
                 unsigned long long salt, const float* mean, const float* std, hipStream_t st);
@@ -149,6 +159,92 @@ void wflip(Tensor w, Tensor wd) {
   const int K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
   TORCH_CHECK(wd.size(0) == C && wd.size(1) == R && wd.size(2) == S && wd.size(3) == K, "wflip: wd shape");
   chk(dpa_wflip(fp(w), fp(wd), K, R, S, C, cur_stream()), "wflip");
+}
+
+// ---------------- bf16-plane (fp32 via bf16x6, or plain bf16) convolution ----------------
+// Plane tensors are bfloat16 [NP, ...] (NP = 1 or 3), contiguous.
+using u16 = unsigned short;
+u16* up(const Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr<at::BFloat16>()); }
+
+void need_planes(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16 planes");
+  TORCH_CHECK(t.size(0) == 1 || t.size(0) == 3, name, " must have 1 or 3 planes in dim 0");
+}
+
+int64_t x3_splits(int64_t Kred, int64_t splits) { return dpa_x3_splits((int)Kred, (int)splits); }
+
+// x3 [NP,N,H,W,C], w3 [NP,K,R,S,C], out [N,P,Q,K] fp32
+void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits,
+                   int64_t tile, bool reduce, bool posmajor) {
+  need_planes(x3, "x3");
+  need_planes(w3, "w3");
+  need(out, "out");
+  const int np = x3.size(0);
+  TORCH_CHECK(w3.size(0) == np, "plane count mismatch");
+  const int N = x3.size(1), H = x3.size(2), W = x3.size(3), C = x3.size(4);
+  const int K = w3.size(1), R = w3.size(2), S = w3.size(3);
+  TORCH_CHECK(w3.size(4) == C, "conv_x3_fprop: channel mismatch");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(out.size(0) == N && out.size(1) == P && out.size(2) == Q && out.size(3) == K, "conv_x3_fprop: out shape");
+  float* sl = nullptr;
+  const int eff = dpa_x3_splits(R * S * C, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_fprop: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * P * Q * K, "conv_x3_fprop: slab too small");
+    sl = fp(*slab);
+  }
+  chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), fp(out), sl, N, H, W, C, K, R, S, (int)stride,
+                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, cur_stream()),
+      "conv_x3_fprop");
+}
+
+// x3 [NP,N,H,W,C], dz3 [NP,N,P,Q,K], dw [K,R,S,C] fp32
+void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits,
+                   int64_t tile, bool posmajor) {
+  need_planes(x3, "x3");
+  need_planes(dz3, "dz3");
+  need(dw, "dw");
+  const int np = x3.size(0);
+  TORCH_CHECK(dz3.size(0) == np, "plane count mismatch");
+  const int N = x3.size(1), H = x3.size(2), W = x3.size(3), C = x3.size(4);
+  const int K = dw.size(0), R = dw.size(1), S = dw.size(2);
+  TORCH_CHECK(dw.size(3) == C && dz3.size(4) == K && dz3.size(1) == N, "conv_x3_wgrad: shape mismatch");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dz3.size(2) == P && dz3.size(3) == Q, "conv_x3_wgrad: dz spatial");
+  float* sl = nullptr;
+  const int eff = dpa_x3_splits(N * P * Q, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_wgrad: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * K * R * S * C, "conv_x3_wgrad: slab too small");
+    sl = fp(*slab);
+  }
+  chk(dpa_conv_x3_wgrad(up(x3), x3.stride(0), up(dz3), dz3.stride(0), fp(dw), sl, N, H, W, C, K, R, S, (int)stride,
+                        (int)pad, (int)splits, (int)tile, posmajor ? 1 : 0, np, cur_stream()),
+      "conv_x3_wgrad");
+}
+
+// x fp32 (any shape) -> out [NP, *x.shape] bf16 planes
+void split_planes(Tensor x, Tensor out) {
+  need(x, "x");
+  need_planes(out, "out");
+  TORCH_CHECK(out.numel() == out.size(0) * x.numel(), "split_planes: out must be [NP, *x.shape]");
+  chk(dpa_split_planes(fp(x), up(out), x.numel(), out.stride(0), out.size(0), cur_stream()), "split_planes");
+}
+
+// w [K,R,S,C] fp32 -> w3 [NP,K,R,S,C] and (optional) wd3 [NP,C,R,S,K] (flipped, for the data gradient)
+void split_weights(Tensor w, Tensor w3, OptT wd3) {
+  need(w, "w");
+  need_planes(w3, "w3");
+  u16* wdp = nullptr;
+  if (wd3.has_value() && wd3->defined()) {
+    need_planes(*wd3, "wd3");
+    wdp = up(*wd3);
+  }
+  chk(dpa_split_weights(fp(w), up(w3), wdp, w.size(0), w.size(1), w.size(2), w.size(3), w3.size(0), cur_stream()),
+      "split_weights");
 }
 
 // ---------------- batch norm ----------------
@@ -367,6 +463,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dz"), py::arg("dw"), py::arg("slab"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
   m.def("wflip", &wflip);
+  m.def("x3_splits", &x3_splits);
+  m.def("conv_x3_fprop", &conv_x3_fprop, py::arg("x3"), py::arg("w3"), py::arg("out"), py::arg("slab"),
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
+        py::arg("posmajor") = false);
+  m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
+  m.def("split_planes", &split_planes);
+  m.def("split_weights", &split_weights);
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);

@@ -1,0 +1,581 @@
+// K1/K2/K3 (fast path) — implicit-GEMM convolution on gfx950 bf16 MFMA with fp32-grade accuracy.
+//
+// gfx950's bf16 matrix rate is 16x its fp32 matrix rate (v_mfma_f32_32x32x16_bf16 does 32x32x16
+// in 32 cycles; v_mfma_f32_32x32x2_f32 does 32x32x2 in 64).  Every fp32 operand x is stored as
+// three bf16 planes x = x0 + x1 + x2 (x0 = rne(x), x1 = rne(x - x0), x2 = rne(x - x0 - x1): 24
+// significant bits, i.e. the full fp32 mantissa), and a product is formed from the six plane
+// products whose magnitude can reach 2^-24 of a*b:
+//        a*b ~= a2*b0 + a1*b1 + a0*b2 + a1*b0 + a0*b1 + a0*b0
+// Each bf16 x bf16 product is exact in the fp32 MFMA accumulator, the three dropped products are
+// below 2^-24 relative, so results carry fp32 rounding-level error (tests compare against fp64),
+// at 6/16 of the fp32-MFMA matrix time.  NP=1 gives the plain bf16 path (one plane, one product).
+//
+// The operand planes are written by their producers (conv_split / bn_apply / bn_bwd_apply / the
+// per-step weight split), so this kernel never converts: it streams bf16 planes global -> LDS
+// (register-staged, double-buffered, one barrier per 16-deep k step) and feeds MFMAs.
+//
+// Modes (same GEMM formulations and position-major tap skipping as conv_gemm.hip):
+//   FPROP  out[m][n] = sum_k Xcol[m][k] W[n][k]      (dgrad = FPROP of dZ with the flipped,
+//                                                     transposed weight planes Wd[c][r][s][k])
+//   WGRAD  dW[n][k]  = sum_m dZ[m][n] Xcol[m][k]     (operands are m-major in memory: the LDS
+//          images keep the loaded [m][col] order and the MFMA fragments are fetched with the
+//          gfx950 transpose read ds_read_b64_tr_b16)
+// Tiles: T128 = 128x128 block, 2x2 waves of 64x64 (2x2 32x32 sub-tiles); T64 = 64x64 block, 1x2
+// waves of 64x32.  Each thread stages one 16-byte chunk per plane per operand per k step.
+#include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+namespace {
+
+constexpr int BK = 16;
+constexpr int KCP = 24;  // k-contiguous LDS row pitch in bf16 (16 data + 8 pad = 48 B: conflict-free b128 reads)
+
+struct FastDiv {
+  unsigned d, mul, shift;
+};
+
+__host__ FastDiv make_fastdiv(unsigned d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) {
+    f.mul = 0;
+    f.shift = 0;
+    return f;
+  }
+  unsigned s = 0;
+  while ((1u << s) < d) ++s;
+  f.shift = s;
+  f.mul = (unsigned)((((unsigned long long)1 << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+__device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) {
+  if (f.d == 1) return n;
+  unsigned t = __umulhi(n, f.mul);
+  return (t + n) >> f.shift;
+}
+
+struct Args {
+  const u16* x;     // FPROP: GEMM input planes NHWC [N,H,W,C]; WGRAD: conv input planes (B operand)
+  long xps;         // plane stride (elements)
+  const u16* w;     // FPROP: weight planes [Nout][R][S][C]; WGRAD: dZ planes [N,P,Q,Kout]
+  long wps;
+  float* out;       // FPROP: NHWC [N,P,Q,Nout] or slabs; WGRAD: dW [Kout][R*S*C] or slabs
+  long slab;
+  int N, H, W, C, P, Q, R, S, stride, pad;
+  int M, Nout, Ktot;
+  int gm, gn, splits, posmajor;
+  FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
+};
+
+__device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& img, unsigned& oh, unsigned& ow) {
+  unsigned pos;
+  if (a.posmajor) {
+    pos = fdiv(m, a.fd_N);
+    img = m - pos * (unsigned)a.N;
+  } else {
+    img = fdiv(m, a.fd_PQ);
+    pos = m - img * (unsigned)(a.P * a.Q);
+  }
+  oh = fdiv(pos, a.fd_Q);
+  ow = pos - oh * (unsigned)a.Q;
+}
+
+__device__ __forceinline__ uint4 ld16(const u16* p) { return *reinterpret_cast<const uint4*>(p); }
+
+enum { XM_FPROP = 0, XM_WGRAD = 2 };
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
+  constexpr bool WG = MODE == XM_WGRAD;
+  constexpr int THREADS = WAVES_M * WAVES_N * 64;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
+  // one 16-B chunk per plane per operand per thread per k step
+  static_assert(WG ? (BK * BM / 8 == THREADS && BK * BN / 8 == THREADS) : (2 * BM == THREADS && 2 * BN == THREADS),
+                "tile/threads mismatch");
+  constexpr int APITCH = WG ? BM + 32 : KCP;  // bf16 per LDS row
+  constexpr int BPITCH = WG ? BN + 32 : KCP;
+  constexpr int AROWS = WG ? BK : BM, BROWS = WG ? BK : BN;
+  constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
+  constexpr int STAGE = NP * (A_PLANE + B_PLANE);
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid / WAVES_N, wc = wid % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int nwg = a.gm * a.gn;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int bm = tile / a.gn, bn = tile % a.gn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int split = blockIdx.y;
+
+  // ---------------- reduction tile iterator with padding-tap skipping ----------------
+  bool skip = false;
+  int lo0 = 0, lo1 = 0, span1 = 1, per = 1, ntot;
+  if constexpr (!WG) {
+    ntot = (a.Ktot + BK - 1) / BK;
+    if (a.posmajor && a.C % BK == 0 && a.N % BM == 0) {
+      const int pos = m0 / a.N;
+      const int oh = pos / a.Q, ow = pos - (pos / a.Q) * a.Q;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      const int r_lo = max(0, -ih0), r_hi = min(a.R, a.H - ih0);
+      const int s_lo = max(0, -iw0), s_hi = min(a.S, a.W - iw0);
+      skip = true;
+      lo0 = r_lo;
+      lo1 = s_lo;
+      span1 = max(0, s_hi - s_lo);
+      per = a.C / BK;
+      ntot = max(0, r_hi - r_lo) * span1 * per;
+    }
+  } else {
+    ntot = (a.M + BK - 1) / BK;
+    if (a.posmajor && a.C % BN == 0 && a.N % BK == 0) {
+      const int tap = n0 / a.C;
+      const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
+      const int oh_lo = max(0, (a.pad - r + a.stride - 1) / a.stride);
+      const int oh_hi = min(a.P, (a.H - 1 + a.pad - r) / a.stride + 1);
+      const int ow_lo = max(0, (a.pad - s + a.stride - 1) / a.stride);
+      const int ow_hi = min(a.Q, (a.W - 1 + a.pad - s) / a.stride + 1);
+      skip = true;
+      lo0 = oh_lo;
+      lo1 = ow_lo;
+      span1 = max(0, ow_hi - ow_lo);
+      per = a.N / BK;
+      ntot = max(0, oh_hi - oh_lo) * span1 * per;
+    }
+  }
+  const int tchunk = (ntot + a.splits - 1) / a.splits;
+  const int vbeg = split * tchunk;
+  const int ntiles = max(0, min(ntot, vbeg + tchunk) - vbeg);
+  auto tile_off = [&](int v) -> int {
+    if (!skip) return v * BK;
+    const int cell = v / per, sub = v - (v / per) * per;
+    const int i0 = lo0 + cell / span1, i1 = lo1 + cell % span1;
+    if constexpr (!WG)
+      return (i0 * a.S + i1) * a.C + sub * BK;
+    else
+      return (i0 * a.Q + i1) * a.N + sub * BK;
+  };
+  const int KMAX = WG ? a.M : a.Ktot;
+
+  // ---------------- per-thread staging slot ----------------
+  // FPROP: A row = tid>>1 (im2col row m), k chunk = (tid&1)*8; B row = tid>>1 (weight row n).
+  // WGRAD: A m-row = tid/(BM/8), kout chunk = tid%(BM/8); B m-row = tid/(BN/8), rsc chunk.
+  int a_img = -1, a_ih0 = 0, a_iw0 = 0, a_kc = 0;     // FPROP A
+  int b_row = 0;                                        // FPROP B
+  int wa_mrow = 0, wa_col = 0;                          // WGRAD A
+  int wb_mrow = 0, wb_rr = 0, wb_ss = 0, wb_c = 0;      // WGRAD B
+  bool wb_valid = false;
+  if constexpr (!WG) {
+    a_kc = (tid & 1) * 8;
+    const int m = m0 + (tid >> 1);
+    if (m < a.M) {
+      unsigned img, oh, ow;
+      decode_row(a, (unsigned)m, img, oh, ow);
+      a_img = (int)img;
+      a_ih0 = (int)oh * a.stride - a.pad;
+      a_iw0 = (int)ow * a.stride - a.pad;
+    }
+    b_row = n0 + (tid >> 1);
+  } else {
+    wa_mrow = tid / (BM / 8);
+    wa_col = m0 + (tid % (BM / 8)) * 8;
+    wb_mrow = tid / (BN / 8);
+    const int rsc = n0 + (tid % (BN / 8)) * 8;
+    wb_valid = rsc < a.Ktot;
+    const unsigned tap = fdiv((unsigned)rsc, a.fd_C);
+    wb_c = rsc - (int)tap * a.C;
+    const unsigned rr = fdiv(tap, a.fd_S);
+    wb_rr = (int)rr - a.pad;
+    wb_ss = (int)(tap - rr * a.S) - a.pad;
+  }
+
+  uint4 ra[NP], rb[NP];
+  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+
+  auto load_tile = [&](int v) {
+    const int kb = tile_off(vbeg + v);
+    if constexpr (!WG) {
+      const int k = kb + a_kc;
+      const unsigned tap = fdiv((unsigned)k, a.fd_C);
+      const int c = k - (int)tap * a.C;
+      const unsigned r = fdiv(tap, a.fd_S);
+      const int s = (int)(tap - r * a.S);
+      const int ih = a_ih0 + (int)r, iw = a_iw0 + s;
+      const bool va = k < KMAX && a_img >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const long aoff = (((long)a_img * a.H + ih) * a.W + iw) * a.C + c;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) ra[p] = va ? ld16(a.x + p * a.xps + aoff) : zero4;
+      const bool vb = k < KMAX && b_row < a.Nout;
+      const long boff = (long)b_row * a.Ktot + k;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rb[p] = vb ? ld16(a.w + p * a.wps + boff) : zero4;
+    } else {
+      {
+        const int m = kb + wa_mrow;
+        const bool v = m < KMAX && wa_col < a.Nout;
+        unsigned img = 0, oh = 0, ow = 0;
+        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        const long off = (((long)img * a.P + oh) * a.Q + ow) * a.Nout + wa_col;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) ra[p] = v ? ld16(a.w + p * a.wps + off) : zero4;
+      }
+      {
+        const int m = kb + wb_mrow;
+        bool v = m < KMAX && wb_valid;
+        unsigned img = 0, oh = 0, ow = 0;
+        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        const int ih = (int)oh * a.stride + wb_rr, iw = (int)ow * a.stride + wb_ss;
+        v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const long off = (((long)img * a.H + ih) * a.W + iw) * a.C + wb_c;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) rb[p] = v ? ld16(a.x + p * a.xps + off) : zero4;
+      }
+    }
+  };
+
+  auto store_tile = [&](int stage) {
+    u16* As = lds + stage * STAGE;
+    u16* Bs = As + NP * A_PLANE;
+    if constexpr (!WG) {
+      const int row = tid >> 1;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        *reinterpret_cast<uint4*>(As + p * A_PLANE + row * APITCH + a_kc) = ra[p];
+        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + row * BPITCH + a_kc) = rb[p];
+      }
+    } else {
+      const int ca = (tid % (BM / 8)) * 8, cb = (tid % (BN / 8)) * 8;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        *reinterpret_cast<uint4*>(As + p * A_PLANE + wa_mrow * APITCH + ca) = ra[p];
+        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + wb_mrow * BPITCH + cb) = rb[p];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // Fragment fetch.  k-contiguous image: lane reads 16 B at [row][8*lh].  Row-contiguous image
+  // ([m][col]): two ds_read_b64_tr_b16; lane 4q+p of each 16-lane group addresses row q of its
+  // 4-row block, columns 4p..4p+3, and receives its own column (kout/rsc = l&31) of the block.
+  auto frag = [&](const u16* base, int pitch, int row0) -> bf16x8 {
+    if constexpr (!WG) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + (row0 + li) * pitch + 8 * lh);
+      return __builtin_bit_cast(bf16x8, v);
+    } else {
+      const int g = lane >> 4, idx = lane & 15;
+      const int q = idx >> 2, p4 = idx & 3;
+      const int col = row0 + 16 * (g & 1) + 4 * p4;
+      const int mrow = 8 * (g >> 1) + q;
+      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + mrow * pitch + col));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (mrow + 4) * pitch + col));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  };
+
+  auto compute_tile = [&](int stage) {
+    const u16* As = lds + stage * STAGE;
+    const u16* Bs = As + NP * A_PLANE;
+    bf16x8 fa[TM][NP], fb[TN][NP];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) fa[i][p] = frag(As + p * A_PLANE, APITCH, wr * WTM + i * 32);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) fb[j][p] = frag(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32);
+    // smallest products first
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (NP == 3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+      }
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < ntiles) load_tile(kt + 1);
+      compute_tile(cur);
+      if (kt + 1 < ntiles) store_tile(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---------------- epilogue (fp32; FPROP rows stored at their NHWC memory row) ----------------
+  float* out = a.out + (long)split * a.slab;
+  const int ldc = WG ? a.Ktot : a.Nout;
+  const int nrows = WG ? a.Nout : a.M;
+  const int ncols = WG ? a.Ktot : a.Nout;
+  const bool remap = !WG && a.posmajor;
+  const int PQ = a.P * a.Q;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc * WTN + j * 32 + li;
+      if (col < ncols) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < nrows) {
+            long mrow = row;
+            if (remap) {
+              const unsigned pos = fdiv((unsigned)row, a.fd_N);
+              mrow = (long)(row - (int)pos * a.N) * PQ + pos;
+            }
+            out[mrow * ldc + col] = acc[i][j][r];
+          }
+        }
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void splitk_sum_x3(const float* __restrict__ slabs, float* __restrict__ out, long n4,
+                                                     int splits) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(slabs)[i];
+    for (int k = 1; k < splits; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(slabs)[(long)k * n4 + i];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+}
+
+// ---------------- fp32 -> bf16 planes ----------------
+__device__ __forceinline__ u16 bf16_rne(float f) {
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+__device__ __forceinline__ float bf16_f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
+
+template <int NP>
+__device__ __forceinline__ void split_val(float v, u16* o) {
+  const u16 h0 = bf16_rne(v);
+  o[0] = h0;
+  if (NP == 3) {
+    const float r1 = v - bf16_f(h0);
+    const u16 h1 = bf16_rne(r1);
+    o[1] = h1;
+    o[2] = bf16_rne(r1 - bf16_f(h1));
+  }
+}
+
+// x [n] fp32 -> planes [NP][n] (n % 4 == 0)
+template <int NP>
+__global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, u16* __restrict__ out, long n4,
+                                                    long ps) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    u16 o[4][3];
+    split_val<NP>(v.x, o[0]);
+    split_val<NP>(v.y, o[1]);
+    split_val<NP>(v.z, o[2]);
+    split_val<NP>(v.w, o[3]);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      ushort4 w = make_ushort4(o[0][p], o[1][p], o[2][p], o[3][p]);
+      reinterpret_cast<ushort4*>(out + p * ps)[i] = w;
+    }
+  }
+}
+
+// weights KRSC fp32 -> planes of W [K][R][S][C] and of the dgrad weights Wd[c][r][s][k] =
+// W[k][R-1-r][S-1-s][c] (both [NP][...]); one thread per Wd element (k fastest: coalesced writes)
+template <int NP>
+__global__ __launch_bounds__(256) void split_weights_kernel(const float* __restrict__ w, u16* __restrict__ w3,
+                                                            u16* __restrict__ wd3, int K, int R, int S, int C) {
+  const long total = (long)K * R * S * C;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    {  // W planes (same index)
+      u16 o[3];
+      split_val<NP>(w[i], o);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) w3[p * total + i] = o[p];
+    }
+    if (wd3) {
+      const int k = (int)(i % K);
+      long t = i / K;
+      const int s = (int)(t % S);
+      t /= S;
+      const int r = (int)(t % R);
+      const int c = (int)(t / R);
+      u16 o[3];
+      split_val<NP>(w[(((long)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c], o);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) wd3[p * total + i] = o[p];
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, int NP>
+int launch_x3(const Args& a, hipStream_t st) {
+  dim3 grid(a.gm * a.gn, a.splits);
+  conv_x3_kernel<BM, BN, WM, WN, MODE, NP><<<grid, WM * WN * 64, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+int grid_1d(long n) {
+  long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void fill(Args& a, int N, int H, int W, int C, int R, int S, int stride, int pad) {
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.R = R;
+  a.S = S;
+  a.stride = stride;
+  a.pad = pad;
+  a.P = (H + 2 * pad - R) / stride + 1;
+  a.Q = (W + 2 * pad - S) / stride + 1;
+  a.M = N * a.P * a.Q;
+  a.Ktot = R * S * C;
+  a.fd_C = make_fastdiv(C);
+  a.fd_S = make_fastdiv(S);
+  a.fd_Q = make_fastdiv(a.Q);
+  a.fd_PQ = make_fastdiv(a.P * a.Q);
+  a.fd_N = make_fastdiv(N);
+}
+
+int xsplits(int Kred, int splits) {
+  const int nt = cdiv(Kred, BK);
+  if (splits < 1) splits = 1;
+  if (splits > nt) splits = nt;
+  return splits < 1 ? 1 : splits;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpa_x3_splits(int Kred, int splits) { return xsplits(Kred, splits); }
+
+// x planes [NP][N,H,W,C] (plane stride xps), w planes [NP][Kout][R][S][C] (stride wps; for a data
+// gradient pass the flipped/transposed Wd planes), out fp32 [N,P,Q,Kout] (or slabs, see
+// conv_gemm.hip).  np: 1 (bf16) or 3 (fp32 via bf16x6).  tile: 0 = 128x128, 1 = 64x64.
+int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out, float* slab, int N, int H, int W,
+                      int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
+                      int posmajor, int np, hipStream_t st) {
+  Args a{};
+  a.x = x;
+  a.xps = xps;
+  a.w = w;
+  a.wps = wps;
+  fill(a, N, H, W, C, R, S, stride, pad);
+  a.Nout = Kout;
+  if (C % 8 || Kout % 8) return -2;
+  const int T = tile == 0 ? 128 : 64;
+  a.gm = cdiv(a.M, T);
+  a.gn = cdiv(Kout, T);
+  a.splits = xsplits(a.Ktot, splits);
+  a.posmajor = posmajor ? 1 : 0;
+  a.out = a.splits > 1 ? slab : out;
+  a.slab = a.splits > 1 ? (long)a.M * Kout : 0;
+  int rc;
+  if (np == 3)
+    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_FPROP, 3>(a, st) : launch_x3<64, 64, 1, 2, XM_FPROP, 3>(a, st);
+  else
+    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_FPROP, 1>(a, st) : launch_x3<64, 64, 1, 2, XM_FPROP, 1>(a, st);
+  if (rc) return rc;
+  if (a.splits > 1 && reduce) {
+    const long n4 = (long)a.M * Kout / 4;
+    splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, a.splits);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
+}
+
+// dW[Kout][R*S*C] = sum_m dZ[m][kout] Xcol[m][rsc]; x planes [NP][N,H,W,C], dz planes [NP][N,P,Q,Kout]
+int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* dw, float* slab, int N, int H, int W,
+                      int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int posmajor, int np,
+                      hipStream_t st) {
+  Args a{};
+  a.x = x;
+  a.xps = xps;
+  a.w = dz;
+  a.wps = dzps;
+  fill(a, N, H, W, C, R, S, stride, pad);
+  a.Nout = Kout;
+  if (C % 8 || Kout % 8) return -2;
+  const int T = tile == 0 ? 128 : 64;
+  a.gm = cdiv(Kout, T);
+  a.gn = cdiv(a.Ktot, T);
+  a.splits = xsplits(a.M, splits);
+  a.posmajor = posmajor ? 1 : 0;
+  a.out = a.splits > 1 ? slab : dw;
+  a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
+  int rc;
+  if (np == 3)
+    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_WGRAD, 3>(a, st) : launch_x3<64, 64, 1, 2, XM_WGRAD, 3>(a, st);
+  else
+    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_WGRAD, 1>(a, st) : launch_x3<64, 64, 1, 2, XM_WGRAD, 1>(a, st);
+  if (rc) return rc;
+  if (a.splits > 1) {
+    const long n4 = (long)Kout * a.Ktot / 4;
+    splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, a.splits);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
+}
+
+int dpa_split_planes(const float* x, u16* out, long n, long ps, int np, hipStream_t st) {
+  if (n % 4) return -2;
+  if (np == 3)
+    split_kernel<3><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
+  else
+    split_kernel<1><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
+  return (int)hipGetLastError();
+}
+
+int dpa_split_weights(const float* w, u16* w3, u16* wd3, int K, int R, int S, int C, int np, hipStream_t st) {
+  const long total = (long)K * R * S * C;
+  if (np == 3)
+    split_weights_kernel<3><<<grid_1d(total), 256, 0, st>>>(w, w3, wd3, K, R, S, C);
+  else
+    split_weights_kernel<1><<<grid_1d(total), 256, 0, st>>>(w, w3, wd3, K, R, S, C);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

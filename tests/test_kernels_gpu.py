@@ -127,3 +127,102 @@ def test_conv_dgrad_mode(shape, splits, tile, posmajor):
     torch.cuda.synchronize()
     res = slab.view(eff, N, H, W, Cin).sum(0) if eff > 1 else dx
     assert rel_err(res.permute(0, 3, 1, 2), gx) < 1e-5
+
+
+# ----------------------------------------------------------------- bf16-plane (x3) kernels
+X3_SHAPES = [
+    (8, 16, 16, 64, 128, 3, 1, 1),
+    (4, 8, 8, 128, 256, 3, 1, 1),
+    (128, 4, 4, 64, 64, 3, 1, 1),
+    (128, 2, 2, 32, 64, 3, 1, 1),
+    (3, 7, 5, 24, 40, 3, 1, 1),
+    (2, 9, 9, 16, 32, 3, 2, 1),
+    (2, 8, 8, 16, 32, 1, 1, 0),
+    (64, 5, 5, 64, 64, 3, 2, 1),
+]
+
+
+def _planes(t, np_):
+    C = _C()
+    out = torch.empty((np_,) + tuple(t.shape), device="cuda", dtype=torch.bfloat16)
+    C.split_planes(t.contiguous().cuda(), out)
+    return out
+
+
+def test_split_planes_exact():
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4096, generator=g) * torch.exp(torch.randn(4096, generator=g) * 4)
+    p = _planes(x, 3).float().cpu()
+    rec = p[0].double() + p[1].double() + p[2].double()
+    rel = ((rec - x.double()).abs() / x.double().abs().clamp_min(1e-30)).max().item()
+    assert rel < 2 ** -22
+    p1 = _planes(x, 1).float().cpu()
+    assert torch.equal(p1[0], x.bfloat16().float())
+
+
+@pytest.mark.parametrize("shape", X3_SHAPES)
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("posmajor", [False, True])
+@pytest.mark.parametrize("np_", [3, 1])
+def test_conv_x3_fprop(shape, splits, tile, posmajor, np_):
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(K, Cin, R, R, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), stride=st, padding=pd)
+    P, Q = ref.shape[2], ref.shape[3]
+    x3 = _planes(x.permute(0, 2, 3, 1), np_)
+    w3 = _planes(w.permute(0, 2, 3, 1), np_)
+    out = torch.empty(N, P, Q, K, device="cuda")
+    slab = torch.empty(splits * N * P * Q * K, device="cuda") if splits > 1 else None
+    C.conv_x3_fprop(x3, w3, out, slab, st, pd, splits, tile, True, posmajor)
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < (1e-5 if np_ == 3 else 2e-2)
+
+
+@pytest.mark.parametrize("shape", [s for s in X3_SHAPES if s[6] == 1 and 2 * s[7] == s[5] - 1])
+@pytest.mark.parametrize("posmajor", [False, True])
+def test_conv_x3_dgrad_via_split_weights(shape, posmajor):
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(True)
+    w = torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, dy)
+    wk = w.float().permute(0, 2, 3, 1).contiguous().cuda()
+    w3 = torch.empty((3,) + tuple(wk.shape), device="cuda", dtype=torch.bfloat16)
+    wd3 = torch.empty(3, Cin, R, R, K, device="cuda", dtype=torch.bfloat16)
+    C.split_weights(wk, w3, wd3)
+    dz3 = _planes(dy.float().permute(0, 2, 3, 1), 3)
+    dx = torch.empty(N, H, W, Cin, device="cuda")
+    slab = torch.empty(4 * N * H * W * Cin, device="cuda")
+    C.conv_x3_fprop(dz3, wd3, dx, slab, 1, pd, 4, 0, True, posmajor)
+    torch.cuda.synchronize()
+    assert rel_err(dx.permute(0, 3, 1, 2), gx) < 1e-5
+
+
+@pytest.mark.parametrize("shape", X3_SHAPES)
+@pytest.mark.parametrize("splits", [1, 7])
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("posmajor", [False, True])
+@pytest.mark.parametrize("np_", [3, 1])
+def test_conv_x3_wgrad(shape, splits, tile, posmajor, np_):
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
+    w = (torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1).requires_grad_(True)
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gw,) = torch.autograd.grad(y, w, dy)
+    x3 = _planes(x.float().permute(0, 2, 3, 1), np_)
+    dz3 = _planes(dy.float().permute(0, 2, 3, 1), np_)
+    dw = torch.empty(K, R, R, Cin, device="cuda")
+    slab = torch.empty(splits * K * R * R * Cin, device="cuda") if splits > 1 else None
+    C.conv_x3_wgrad(x3, dz3, dw, slab, st, pd, splits, tile, posmajor)
+    torch.cuda.synchronize()
+    assert rel_err(dw.permute(0, 3, 1, 2), gw) < (1e-5 if np_ == 3 else 2e-2)
