@@ -24,11 +24,12 @@ int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M,
                      float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
                        const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st);
-int dpa_bn_apply(const float* z, float* a, const float* scale, const float* shift, int N, int H, int W, int C,
-                 int pool, hipStream_t st);
+int dpa_bn_apply(const float* z, float* a, unsigned short* a3, int np, const float* scale, const float* shift, int N,
+                 int H, int W, int C, int pool, hipStream_t st);
 int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
-               float* dbeta, float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st);
+               float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
+               int pool, hipStream_t st);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st);
@@ -279,12 +280,22 @@ void bn_eval_params(Tensor gamma, Tensor beta, OptT bias, Tensor rmean, Tensor r
       "bn_eval_params");
 }
 
+// a: fp32 [N,Ho,Wo,C] or bf16 planes [NP,N,Ho,Wo,C]
 void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool) {
   need(z, "z");
-  need(a, "a");
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
-  TORCH_CHECK(a.numel() == (int64_t)N * (pool ? (H / 2) * (W / 2) : H * W) * C, "bn_apply: a shape");
-  chk(dpa_bn_apply(fp(z), fp(a), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()), "bn_apply");
+  const int64_t outn = (int64_t)N * (pool ? (H / 2) * (W / 2) : H * W) * C;
+  if (a.scalar_type() == at::kBFloat16) {
+    need_planes(a, "a3");
+    TORCH_CHECK(a.numel() == a.size(0) * outn, "bn_apply: a3 shape");
+    chk(dpa_bn_apply(fp(z), nullptr, up(a), a.size(0), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()),
+        "bn_apply");
+  } else {
+    need(a, "a");
+    TORCH_CHECK(a.numel() == outn, "bn_apply: a shape");
+    chk(dpa_bn_apply(fp(z), fp(a), nullptr, 0, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()),
+        "bn_apply");
+  }
 }
 
 // gsrc: grad wrt the layer output (pooled shape if pool) or nsplit slabs of it (then the sum is
@@ -294,7 +305,18 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   need(gsrc, "gsrc");
   need(g, "g");
   need(z, "z");
-  need(dz, "dz");
+  float* dzf = nullptr;
+  u16* dz3 = nullptr;
+  int np = 0;
+  if (dz.scalar_type() == at::kBFloat16) {
+    need_planes(dz, "dz3");
+    TORCH_CHECK(dz.numel() == dz.size(0) * z.numel(), "bn_bwd: dz3 shape");
+    dz3 = up(dz);
+    np = dz.size(0);
+  } else {
+    need(dz, "dz");
+    dzf = fp(dz);
+  }
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   TORCH_CHECK(g.numel() == (int64_t)Mo * C, "bn_bwd: g shape");
@@ -302,7 +324,7 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd: part too small");
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
   chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
-                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), fp(dz), N, H, W, C, pool ? 1 : 0, cur_stream()),
+                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, cur_stream()),
       "bn_bwd");
 }
 

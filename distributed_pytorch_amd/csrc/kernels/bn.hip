@@ -50,6 +50,39 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
+// ---- output writer: NP == 0 -> fp32 float4 store; NP in {1,3} -> bf16 planes x = x0 (+ x1 + x2)
+// (round-to-nearest-even splits, conv_x3.hip header) so the next conv reads MFMA-ready operands.
+typedef unsigned short u16;
+__device__ __forceinline__ u16 bf16_rne(float f) {
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+__device__ __forceinline__ float bf16_f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
+
+template <int NP>
+__device__ __forceinline__ void store4(float* f, u16* pl, long ps, long i4, float4 v) {
+  if constexpr (NP == 0) {
+    reinterpret_cast<float4*>(f)[i4] = v;
+  } else {
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    u16 o[3][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u16 h0 = bf16_rne(vv[k]);
+      o[0][k] = h0;
+      if (NP == 3) {
+        const float r1 = vv[k] - bf16_f(h0);
+        const u16 h1 = bf16_rne(r1);
+        o[1][k] = h1;
+        o[2][k] = bf16_rne(r1 - bf16_f(h1));
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) reinterpret_cast<ushort4*>(pl + p * ps)[i4] = make_ushort4(o[p][0], o[p][1], o[p][2], o[p][3]);
+  }
+}
+
 // ---- forward statistics: per (row-block, channel) (mean, M2) via sums shifted by the block's
 // first row.  If nsplit > 1, src holds nsplit slabs of [M][C] that are summed here and written
 // to z (the split-K reduction of the producing conv, fused).
@@ -199,8 +232,9 @@ __device__ __forceinline__ float4 affine_relu(float4 v, float4 sc, float4 sh) {
 }
 
 // a = relu(z*scale + shift), optionally 2x2/s2 max-pooled.  z: [N,H,W,C]  a: [N,H/2,W/2,C] or [N,H,W,C]
-template <bool POOL>
+template <bool POOL, int NP>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, float* __restrict__ a,
+                                                       u16* __restrict__ a3, long ps,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int N, int H, int W, int C) {
   const int C4 = C >> 2;
@@ -213,7 +247,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
     const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
     if (!POOL) {
-      reinterpret_cast<float4*>(a)[i] = affine_relu(z4[i], sc, sh);
+      store4<NP>(a, a3, ps, i, affine_relu(z4[i], sc, sh));
     } else {
       long t = i / C4;
       const int ow = (int)(t % Wo);
@@ -225,9 +259,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
       const float4 v01 = affine_relu(z4[base + C4], sc, sh);
       const float4 v10 = affine_relu(z4[base + (long)W * C4], sc, sh);
       const float4 v11 = affine_relu(z4[base + (long)W * C4 + C4], sc, sh);
-      reinterpret_cast<float4*>(a)[i] =
-          make_float4(fmaxf(fmaxf(v00.x, v01.x), fmaxf(v10.x, v11.x)), fmaxf(fmaxf(v00.y, v01.y), fmaxf(v10.y, v11.y)),
-                      fmaxf(fmaxf(v00.z, v01.z), fmaxf(v10.z, v11.z)), fmaxf(fmaxf(v00.w, v01.w), fmaxf(v10.w, v11.w)));
+      store4<NP>(a, a3, ps, i,
+                 make_float4(fmaxf(fmaxf(v00.x, v01.x), fmaxf(v10.x, v11.x)),
+                             fmaxf(fmaxf(v00.y, v01.y), fmaxf(v10.y, v11.y)),
+                             fmaxf(fmaxf(v00.z, v01.z), fmaxf(v10.z, v11.z)),
+                             fmaxf(fmaxf(v00.w, v01.w), fmaxf(v10.w, v11.w))));
     }
   }
 }
@@ -404,19 +440,19 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-template <bool POOL>
+template <bool POOL, int NP>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ z,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ coef, float* __restrict__ dz,
-                                                           int N, int H, int W, int C) {
+                                                           u16* __restrict__ dz3, long ps, int N, int H, int W,
+                                                           int C) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
   const long stride = (long)gridDim.x * blockDim.x;
   const float4* z4 = reinterpret_cast<const float4*>(z);
   const float4* g4 = reinterpret_cast<const float4*>(g);
-  float4* o4 = reinterpret_cast<float4*>(dz);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int c4 = (int)(i % C4);
     const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
@@ -434,7 +470,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         const float dy = fmaf(zz, F4GET(sc, k), F4GET(sh, k)) > 0.f ? F4GET(gv, k) : 0.f;
         r[k] = F4GET(k1, k) * dy + F4GET(k2, k) * zz + F4GET(k3, k);
       }
-      o4[i] = make_float4(r[0], r[1], r[2], r[3]);
+      store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]));
     } else {
       long t = i / C4;
       const int ow = (int)(t % Wo);
@@ -456,7 +492,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         for (int q = 0; q < 4; ++q) out[q][k] = F4GET(k1, k) * d[q] + F4GET(k2, k) * F4GET(zq[q], k) + F4GET(k3, k);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o4[idx[q]] = make_float4(out[q][0], out[q][1], out[q][2], out[q][3]);
+      for (int q = 0; q < 4; ++q) store4<NP>(dz, dz3, ps, idx[q], make_float4(out[q][0], out[q][1], out[q][2], out[q][3]));
     }
   }
 }
@@ -497,14 +533,26 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
   return (int)hipGetLastError();
 }
 
-int dpa_bn_apply(const float* z, float* a, const float* scale, const float* shift, int N, int H, int W, int C,
-                 int pool, hipStream_t st) {
+#define BN_DISPATCH_NP(NPV, POOLV, LAUNCH) \
+  do {                                      \
+    if (NPV == 0) {                         \
+      if (POOLV) LAUNCH(true, 0); else LAUNCH(false, 0); \
+    } else if (NPV == 1) {                  \
+      if (POOLV) LAUNCH(true, 1); else LAUNCH(false, 1); \
+    } else {                                \
+      if (POOLV) LAUNCH(true, 3); else LAUNCH(false, 3); \
+    }                                       \
+  } while (0)
+
+// out: fp32 a (np == 0) or bf16 planes a3 [np][...] (np in {1, 3})
+int dpa_bn_apply(const float* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
+                 int W, int C, int pool, hipStream_t st) {
   if (C % 4) return -2;
   const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
-  if (pool)
-    bn_apply_kernel<true><<<grid_1d(total), 256, 0, st>>>(z, a, scale, shift, N, H, W, C);
-  else
-    bn_apply_kernel<false><<<grid_1d(total), 256, 0, st>>>(z, a, scale, shift, N, H, W, C);
+  const long ps = total * 4;
+#define L_APPLY(P, NPT) bn_apply_kernel<P, NPT><<<grid_1d(total), 256, 0, st>>>(z, a, a3, ps, scale, shift, N, H, W, C)
+  BN_DISPATCH_NP(np, pool, L_APPLY);
+#undef L_APPLY
   return (int)hipGetLastError();
 }
 
@@ -512,7 +560,8 @@ int dpa_bn_apply(const float* z, float* a, const float* scale, const float* shif
 // written to g).  Writes dz [N,H,W,C] and dgamma/dbeta/dbias.
 int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
-               float* dbeta, float* dbias, float* dz, int N, int H, int W, int C, int pool, hipStream_t st) {
+               float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool,
+               hipStream_t st) {
   if (C % 4) return -2;
   if (nsplit < 1) nsplit = 1;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
@@ -529,10 +578,11 @@ int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const fl
                                                       dbeta, dbias, coef);
   const float* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
-  if (pool)
-    bn_bwd_apply_kernel<true><<<grid_1d(total), 256, 0, st>>>(gg, z, scale, shift, coef, dz, N, H, W, C);
-  else
-    bn_bwd_apply_kernel<false><<<grid_1d(total), 256, 0, st>>>(gg, z, scale, shift, coef, dz, N, H, W, C);
+  const long ps = (long)N * H * W * C;
+#define L_BAPPLY(P, NPT) \
+  bn_bwd_apply_kernel<P, NPT><<<grid_1d(total), 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, N, H, W, C)
+  BN_DISPATCH_NP(np, pool, L_BAPPLY);
+#undef L_BAPPLY
   return (int)hipGetLastError();
 }
 

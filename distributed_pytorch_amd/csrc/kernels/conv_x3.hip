@@ -30,8 +30,7 @@ typedef unsigned short u16;
 
 namespace {
 
-constexpr int BK = 16;
-constexpr int KCP = 24;  // k-contiguous LDS row pitch in bf16 (16 data + 8 pad = 48 B: conflict-free b128 reads)
+constexpr int BKMIN = 16;  // smallest stage depth (split-K granularity)
 
 struct FastDiv {
   unsigned d, mul, shift;
@@ -88,18 +87,26 @@ __device__ __forceinline__ uint4 ld16(const u16* p) { return *reinterpret_cast<c
 
 enum { XM_FPROP = 0, XM_WGRAD = 2 };
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP>
+// BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  k-contiguous LDS rows are
+// BK+8 bf16 long (48/80/144 B: the 16 rows of every ds_read_b128 lane group hit 16 distinct 16-B
+// slots); row-contiguous ([m][col]) rows are cols+32 bf16 (4 consecutive rows 64 B apart modulo
+// the 256-B bank row: conflict-free transpose reads).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
   constexpr bool WG = MODE == XM_WGRAD;
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
-  // one 16-B chunk per plane per operand per thread per k step
-  static_assert(WG ? (BK * BM / 8 == THREADS && BK * BN / 8 == THREADS) : (2 * BM == THREADS && 2 * BN == THREADS),
+  constexpr int CPR = BK / 8;  // 16-B chunks per k-contiguous row
+  // staging: every thread owns NCA / NCB 16-byte chunks per plane of A / B per stage
+  constexpr int NCA = WG ? BK * BM / 8 / THREADS : BM * CPR / THREADS;
+  constexpr int NCB = WG ? BK * BN / 8 / THREADS : BN * CPR / THREADS;
+  static_assert(NCA >= 1 && NCB >= 1 && (WG ? (BK * BM / 8) % THREADS == 0 : (BM * CPR) % THREADS == 0),
                 "tile/threads mismatch");
-  constexpr int APITCH = WG ? BM + 32 : KCP;  // bf16 per LDS row
-  constexpr int BPITCH = WG ? BN + 32 : KCP;
+  static_assert(WG ? THREADS % (BM / 8) == 0 && THREADS % (BN / 8) == 0 : THREADS % CPR == 0, "slot mapping");
+  constexpr int APITCH = WG ? BM + 32 : BK + 8;  // bf16 per LDS row
+  constexpr int BPITCH = WG ? BN + 32 : BK + 8;
   constexpr int AROWS = WG ? BK : BM, BROWS = WG ? BK : BN;
   constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
   constexpr int STAGE = NP * (A_PLANE + B_PLANE);
@@ -166,30 +173,35 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   };
   const int KMAX = WG ? a.M : a.Ktot;
 
-  // ---------------- per-thread staging slot ----------------
-  // FPROP: A row = tid>>1 (im2col row m), k chunk = (tid&1)*8; B row = tid>>1 (weight row n).
-  // WGRAD: A m-row = tid/(BM/8), kout chunk = tid%(BM/8); B m-row = tid/(BN/8), rsc chunk.
-  int a_img = -1, a_ih0 = 0, a_iw0 = 0, a_kc = 0;     // FPROP A
-  int b_row = 0;                                        // FPROP B
-  int wa_mrow = 0, wa_col = 0;                          // WGRAD A
-  int wb_mrow = 0, wb_rr = 0, wb_ss = 0, wb_c = 0;      // WGRAD B
+  // ---------------- per-thread staging slots ----------------
+  // FPROP: chunk (row, kc) with kc = tid % CPR fixed, rows tid/CPR + j*(THREADS/CPR).
+  // WGRAD: chunk (m-row, col) with col = tid % (cols/8) fixed, m-rows tid/(cols/8) + j*step.
+  constexpr int AROWSTEP = WG ? THREADS / (BM / 8) : THREADS / CPR;
+  constexpr int BROWSTEP = WG ? THREADS / (BN / 8) : THREADS / CPR;
+  const int a_r0 = WG ? tid / (BM / 8) : tid / CPR;
+  const int b_r0 = WG ? tid / (BN / 8) : tid / CPR;
+  const int a_c8 = WG ? (tid % (BM / 8)) * 8 : (tid % CPR) * 8;  // column (WGRAD) / k offset (FPROP) of the chunk
+  const int b_c8 = WG ? (tid % (BN / 8)) * 8 : (tid % CPR) * 8;
+  int a_img[WG ? 1 : NCA], a_ih0[WG ? 1 : NCA], a_iw0[WG ? 1 : NCA];  // FPROP A rows
+  int wb_rr = 0, wb_ss = 0, wb_c = 0;                                  // WGRAD B column (rsc chunk)
   bool wb_valid = false;
   if constexpr (!WG) {
-    a_kc = (tid & 1) * 8;
-    const int m = m0 + (tid >> 1);
-    if (m < a.M) {
-      unsigned img, oh, ow;
-      decode_row(a, (unsigned)m, img, oh, ow);
-      a_img = (int)img;
-      a_ih0 = (int)oh * a.stride - a.pad;
-      a_iw0 = (int)ow * a.stride - a.pad;
+#pragma unroll
+    for (int j = 0; j < NCA; ++j) {
+      const int m = m0 + a_r0 + j * AROWSTEP;
+      a_img[j] = -1;
+      a_ih0[j] = 0;
+      a_iw0[j] = 0;
+      if (m < a.M) {
+        unsigned img, oh, ow;
+        decode_row(a, (unsigned)m, img, oh, ow);
+        a_img[j] = (int)img;
+        a_ih0[j] = (int)oh * a.stride - a.pad;
+        a_iw0[j] = (int)ow * a.stride - a.pad;
+      }
     }
-    b_row = n0 + (tid >> 1);
   } else {
-    wa_mrow = tid / (BM / 8);
-    wa_col = m0 + (tid % (BM / 8)) * 8;
-    wb_mrow = tid / (BN / 8);
-    const int rsc = n0 + (tid % (BN / 8)) * 8;
+    const int rsc = n0 + b_c8;
     wb_valid = rsc < a.Ktot;
     const unsigned tap = fdiv((unsigned)rsc, a.fd_C);
     wb_c = rsc - (int)tap * a.C;
@@ -198,38 +210,49 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     wb_ss = (int)(tap - rr * a.S) - a.pad;
   }
 
-  uint4 ra[NP], rb[NP];
+  uint4 ra[NCA][NP], rb[NCB][NP];
   const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
 
   auto load_tile = [&](int v) {
     const int kb = tile_off(vbeg + v);
     if constexpr (!WG) {
-      const int k = kb + a_kc;
+      const int k = kb + a_c8;
       const unsigned tap = fdiv((unsigned)k, a.fd_C);
       const int c = k - (int)tap * a.C;
       const unsigned r = fdiv(tap, a.fd_S);
       const int s = (int)(tap - r * a.S);
-      const int ih = a_ih0 + (int)r, iw = a_iw0 + s;
-      const bool va = k < KMAX && a_img >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const long aoff = (((long)a_img * a.H + ih) * a.W + iw) * a.C + c;
+      const bool kv = k < KMAX;
 #pragma unroll
-      for (int p = 0; p < NP; ++p) ra[p] = va ? ld16(a.x + p * a.xps + aoff) : zero4;
-      const bool vb = k < KMAX && b_row < a.Nout;
-      const long boff = (long)b_row * a.Ktot + k;
+      for (int j = 0; j < NCA; ++j) {
+        const int ih = a_ih0[j] + (int)r, iw = a_iw0[j] + s;
+        const bool va = kv && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const long aoff = (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c;
 #pragma unroll
-      for (int p = 0; p < NP; ++p) rb[p] = vb ? ld16(a.w + p * a.wps + boff) : zero4;
+        for (int p = 0; p < NP; ++p) ra[j][p] = va ? ld16(a.x + p * a.xps + aoff) : zero4;
+      }
+#pragma unroll
+      for (int j = 0; j < NCB; ++j) {
+        const int n = n0 + b_r0 + j * BROWSTEP;
+        const bool vb = kv && n < a.Nout;
+        const long boff = (long)n * a.Ktot + k;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) rb[j][p] = vb ? ld16(a.w + p * a.wps + boff) : zero4;
+      }
     } else {
-      {
-        const int m = kb + wa_mrow;
-        const bool v = m < KMAX && wa_col < a.Nout;
+#pragma unroll
+      for (int j = 0; j < NCA; ++j) {
+        const int m = kb + a_r0 + j * AROWSTEP;
+        const int col = m0 + a_c8;
+        const bool v = m < KMAX && col < a.Nout;
         unsigned img = 0, oh = 0, ow = 0;
         if (v) decode_row(a, (unsigned)m, img, oh, ow);
-        const long off = (((long)img * a.P + oh) * a.Q + ow) * a.Nout + wa_col;
+        const long off = (((long)img * a.P + oh) * a.Q + ow) * a.Nout + col;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) ra[p] = v ? ld16(a.w + p * a.wps + off) : zero4;
+        for (int p = 0; p < NP; ++p) ra[j][p] = v ? ld16(a.w + p * a.wps + off) : zero4;
       }
-      {
-        const int m = kb + wb_mrow;
+#pragma unroll
+      for (int j = 0; j < NCB; ++j) {
+        const int m = kb + b_r0 + j * BROWSTEP;
         bool v = m < KMAX && wb_valid;
         unsigned img = 0, oh = 0, ow = 0;
         if (v) decode_row(a, (unsigned)m, img, oh, ow);
@@ -237,7 +260,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const long off = (((long)img * a.H + ih) * a.W + iw) * a.C + wb_c;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) rb[p] = v ? ld16(a.x + p * a.xps + off) : zero4;
+        for (int p = 0; p < NP; ++p) rb[j][p] = v ? ld16(a.x + p * a.xps + off) : zero4;
       }
     }
   };
@@ -245,21 +268,16 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   auto store_tile = [&](int stage) {
     u16* As = lds + stage * STAGE;
     u16* Bs = As + NP * A_PLANE;
-    if constexpr (!WG) {
-      const int row = tid >> 1;
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        *reinterpret_cast<uint4*>(As + p * A_PLANE + row * APITCH + a_kc) = ra[p];
-        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + row * BPITCH + a_kc) = rb[p];
-      }
-    } else {
-      const int ca = (tid % (BM / 8)) * 8, cb = (tid % (BN / 8)) * 8;
+    for (int j = 0; j < NCA; ++j)
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        *reinterpret_cast<uint4*>(As + p * A_PLANE + wa_mrow * APITCH + ca) = ra[p];
-        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + wb_mrow * BPITCH + cb) = rb[p];
-      }
-    }
+      for (int p = 0; p < NP; ++p)
+        *reinterpret_cast<uint4*>(As + p * A_PLANE + (a_r0 + j * AROWSTEP) * APITCH + a_c8) = ra[j][p];
+#pragma unroll
+    for (int j = 0; j < NCB; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + (b_r0 + j * BROWSTEP) * BPITCH + b_c8) = rb[j][p];
   };
 
   f32x16 acc[TM][TN];
@@ -273,15 +291,15 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   // Fragment fetch.  k-contiguous image: lane reads 16 B at [row][8*lh].  Row-contiguous image
   // ([m][col]): two ds_read_b64_tr_b16; lane 4q+p of each 16-lane group addresses row q of its
   // 4-row block, columns 4p..4p+3, and receives its own column (kout/rsc = l&31) of the block.
-  auto frag = [&](const u16* base, int pitch, int row0) -> bf16x8 {
+  auto frag = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
     if constexpr (!WG) {
-      const uint4 v = *reinterpret_cast<const uint4*>(base + (row0 + li) * pitch + 8 * lh);
+      const uint4 v = *reinterpret_cast<const uint4*>(base + (row0 + li) * pitch + 16 * ks + 8 * lh);
       return __builtin_bit_cast(bf16x8, v);
     } else {
       const int g = lane >> 4, idx = lane & 15;
       const int q = idx >> 2, p4 = idx & 3;
       const int col = row0 + 16 * (g & 1) + 4 * p4;
-      const int mrow = 8 * (g >> 1) + q;
+      const int mrow = 16 * ks + 8 * (g >> 1) + q;
       typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
       const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + mrow * pitch + col));
       const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (mrow + 4) * pitch + col));
@@ -294,15 +312,17 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   auto compute_tile = [&](int stage) {
     const u16* As = lds + stage * STAGE;
     const u16* Bs = As + NP * A_PLANE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
     bf16x8 fa[TM][NP], fb[TN][NP];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int p = 0; p < NP; ++p) fa[i][p] = frag(As + p * A_PLANE, APITCH, wr * WTM + i * 32);
+      for (int p = 0; p < NP; ++p) fa[i][p] = frag(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks);
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int p = 0; p < NP; ++p) fb[j][p] = frag(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32);
+      for (int p = 0; p < NP; ++p) fb[j][p] = frag(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
     // smallest products first
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -317,6 +337,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         }
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
       }
+    }
   };
 
   if (ntiles > 0) {
@@ -446,12 +467,24 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float* __restr
   }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int NP>
+template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK>
 int launch_x3(const Args& a, hipStream_t st) {
   dim3 grid(a.gm * a.gn, a.splits);
-  conv_x3_kernel<BM, BN, WM, WN, MODE, NP><<<grid, WM * WN * 64, 0, st>>>(a);
+  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
+
+// tile id -> (block tile, stage depth): 0: 128x128/k32  1: 64x64/k32  2: 128x128/k16  3: 64x64/k64
+template <int MODE, int NP>
+int launch_tile(const Args& a, int tile, hipStream_t st) {
+  switch (tile) {
+    case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32>(a, st);
+    case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32>(a, st);
+    case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16>(a, st);
+    default: return launch_x3<64, 64, 1, 2, MODE, NP, 64>(a, st);
+  }
+}
+int tile_rows(int tile) { return (tile == 0 || tile == 2) ? 128 : 64; }
 
 int grid_1d(long n) {
   long g = (n + 255) / 256;
@@ -480,7 +513,7 @@ void fill(Args& a, int N, int H, int W, int C, int R, int S, int stride, int pad
 }
 
 int xsplits(int Kred, int splits) {
-  const int nt = cdiv(Kred, BK);
+  const int nt = cdiv(Kred, BKMIN);
   if (splits < 1) splits = 1;
   if (splits > nt) splits = nt;
   return splits < 1 ? 1 : splits;
@@ -506,25 +539,21 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out
   fill(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
   if (C % 8 || Kout % 8) return -2;
-  const int T = tile == 0 ? 128 : 64;
+  const int T = tile_rows(tile);
   a.gm = cdiv(a.M, T);
   a.gn = cdiv(Kout, T);
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor ? 1 : 0;
   a.out = a.splits > 1 ? slab : out;
   a.slab = a.splits > 1 ? (long)a.M * Kout : 0;
-  int rc;
-  if (np == 3)
-    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_FPROP, 3>(a, st) : launch_x3<64, 64, 1, 2, XM_FPROP, 3>(a, st);
-  else
-    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_FPROP, 1>(a, st) : launch_x3<64, 64, 1, 2, XM_FPROP, 1>(a, st);
+  const int rc = np == 3 ? launch_tile<XM_FPROP, 3>(a, tile, st) : launch_tile<XM_FPROP, 1>(a, tile, st);
   if (rc) return rc;
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * Kout / 4;
     splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, a.splits);
-    rc = (int)hipGetLastError();
+    return (int)hipGetLastError();
   }
-  return rc;
+  return 0;
 }
 
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] Xcol[m][rsc]; x planes [NP][N,H,W,C], dz planes [NP][N,P,Q,Kout]
@@ -539,25 +568,21 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   fill(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
   if (C % 8 || Kout % 8) return -2;
-  const int T = tile == 0 ? 128 : 64;
+  const int T = tile_rows(tile);
   a.gm = cdiv(Kout, T);
   a.gn = cdiv(a.Ktot, T);
   a.splits = xsplits(a.M, splits);
   a.posmajor = posmajor ? 1 : 0;
   a.out = a.splits > 1 ? slab : dw;
   a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
-  int rc;
-  if (np == 3)
-    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_WGRAD, 3>(a, st) : launch_x3<64, 64, 1, 2, XM_WGRAD, 3>(a, st);
-  else
-    rc = tile == 0 ? launch_x3<128, 128, 2, 2, XM_WGRAD, 1>(a, st) : launch_x3<64, 64, 1, 2, XM_WGRAD, 1>(a, st);
+  const int rc = np == 3 ? launch_tile<XM_WGRAD, 3>(a, tile, st) : launch_tile<XM_WGRAD, 1>(a, tile, st);
   if (rc) return rc;
   if (a.splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;
     splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, a.splits);
-    rc = (int)hipGetLastError();
+    return (int)hipGetLastError();
   }
-  return rc;
+  return 0;
 }
 
 int dpa_split_planes(const float* x, u16* out, long n, long ps, int np, hipStream_t st) {
