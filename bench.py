@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--impl", default="fp32", choices=["fp32", "x3", "bf16"],
+                    help="conv kernels: fp32 MFMA | fp32-grade bf16x6 planes | bf16 (mixed precision)")
     a = ap.parse_args()
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -58,7 +60,7 @@ def main():
     train = synthetic_cifar(50000, 0)
     sampler = ShardSampler(len(train), ctx.world, ctx.rank, shuffle=True, seed=0)
     loader = DeviceLoader(train, a.batch, dev, sampler=sampler, train=True, seed=7919 + ctx.rank, drop_last=True)
-    engine = VGGEngine(a.model, dev, max_batch=a.batch)
+    engine = VGGEngine(a.model, dev, max_batch=a.batch, impl=a.impl)
     engine.init_parameters(seed=1)
     sync = make_sync(a.mode, engine, ctx.comm, bucket_mb=a.bucket_mb, overlap=not a.no_overlap)
 
@@ -116,7 +118,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / base, 2) if base else None,
-            "dtype": "fp32",
+            "dtype": "bf16" if a.impl == "bf16" else "fp32",
+            "conv_impl": a.impl,
             "data": "synthetic (CIFAR-10-shaped uint8 on device, random-crop/flip/normalize each step)",
             "config": {"model": a.model, "global_batch": a.batch * ctx.world, "seq_len": None, "image_size": 32,
                        "parallelism": f"dp{ctx.world}", "sync_mode": a.mode, "comm": ctx.comm.name,

@@ -95,6 +95,13 @@ struct RowContigSlots {  // a row-contiguous operand tile BK x ROWS, loaded as f
 
 __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// Branch-free masked load: always issue the load (from the tensor base when masked off) and select
+// afterwards — a per-slot "valid ? load : 0" makes hipcc branch around each load and drain vmcnt.
+__device__ __forceinline__ float4 ldg4m(const float* base, long off, bool valid) {
+  const float4 v = *reinterpret_cast<const float4*>(base + (valid ? off : 0));
+  return valid ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // logical GEMM row m -> (img, oh, ow)
 __device__ __forceinline__ void decode_row(const ConvArgs& a, unsigned m, unsigned& img, unsigned& oh,
                                            unsigned& ow) {
@@ -261,7 +268,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
       for (int j = 0; j < NA; ++j) {
         const int ih = a_ih0[j] + (int)r, iw = a_iw0[j] + s;
         const bool v = kval && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        ra[j] = v ? ldg4(a.x + (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ra[j] = ldg4m(a.x, (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c, v);
       }
       if constexpr (MODE == MODE_FPROP) {
         const int kb4 = kb + b_k4 * 4;
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         for (int j = 0; j < NB; ++j) {
           const int n = n0 + b_row0 + j * BSl::ROW_STEP;
           const bool v = kbv && n < a.Nout;
-          rb[j] = v ? ldg4(a.w + (long)n * a.Ktot + kb4) : make_float4(0.f, 0.f, 0.f, 0.f);
+          rb[j] = ldg4m(a.w, (long)n * a.Ktot + kb4, v);
         }
       } else {
         // DGRAD: B[n=c][k=(r',s',kk)] = W[kk][R-1-r'][S-1-s'][c], W stored [Kout=a.C][R][S][Nout]
@@ -282,8 +289,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
           const unsigned rr = fdiv(tp, a.fd_S);
           const int ss = (int)(tp - rr * a.S);
           const bool v = k < KMAX && b_colvalid;
-          rb[j] = v ? ldg4(a.w + (((long)kk * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + b_c)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
+          rb[j] = ldg4m(a.w, (((long)kk * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + b_c, v);
         }
       }
     } else {
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         unsigned img = 0, oh = 0, ow = 0;
         if (v) decode_row(a, (unsigned)m, img, oh, ow);
         const long row = ((long)img * a.P + oh) * a.Q + ow;
-        ra[j] = v ? ldg4(a.w + row * a.Nout + a_col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ra[j] = ldg4m(a.w, row * a.Nout + a_col, v);
       }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         if (v) decode_row(a, (unsigned)m, img, oh, ow);
         const int ih = (int)oh * a.stride + b_rr, iw = (int)ow * a.stride + b_ss;
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        rb[j] = v ? ldg4(a.x + (((long)img * a.H + ih) * a.W + iw) * a.C + b_c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        rb[j] = ldg4m(a.x, (((long)img * a.H + ih) * a.W + iw) * a.C + b_c, v);
       }
     }
   };

@@ -83,7 +83,14 @@ __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& 
   ow = pos - oh * (unsigned)a.Q;
 }
 
-__device__ __forceinline__ uint4 ld16(const u16* p) { return *reinterpret_cast<const uint4*>(p); }
+// 16-byte operand-plane load; always issued (from the plane base when masked off), selected after:
+// branch-free (a "valid ? load : 0" becomes a branch + vmcnt drain per load) and 16-B aligned
+// (every chunk starts on a multiple of 8 bf16), so it lowers to one global_load_dwordx4.
+__device__ __forceinline__ uint4 ld16m(const u16* base, long off, bool valid) {
+  const uint4* p = reinterpret_cast<const uint4*>(__builtin_assume_aligned(base + (valid ? off : 0), 16));
+  const uint4 v = *p;
+  return valid ? v : make_uint4(0u, 0u, 0u, 0u);
+}
 
 enum { XM_FPROP = 0, XM_WGRAD = 2 };
 
@@ -91,7 +98,9 @@ enum { XM_FPROP = 0, XM_WGRAD = 2 };
 // BK+8 bf16 long (48/80/144 B: the 16 rows of every ds_read_b128 lane group hit 16 distinct 16-B
 // slots); row-contiguous ([m][col]) rows are cols+32 bf16 (4 consecutive rows 64 B apart modulo
 // the 256-B bank row: conflict-free transpose reads).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK>
+// NSTAGE: 2 = double-buffered LDS (one barrier per k step); 1 = single LDS stage + register
+// prefetch (two barriers per step, half the LDS -> more resident blocks to hide load latency).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK, int NSTAGE>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
   constexpr bool WG = MODE == XM_WGRAD;
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
@@ -110,7 +119,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   constexpr int AROWS = WG ? BK : BM, BROWS = WG ? BK : BN;
   constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
   constexpr int STAGE = NP * (A_PLANE + B_PLANE);
-  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) u16 lds[NSTAGE * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -211,7 +220,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   }
 
   uint4 ra[NCA][NP], rb[NCB][NP];
-  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
 
   auto load_tile = [&](int v) {
     const int kb = tile_off(vbeg + v);
@@ -228,7 +236,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         const bool va = kv && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const long aoff = (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) ra[j][p] = va ? ld16(a.x + p * a.xps + aoff) : zero4;
+        for (int p = 0; p < NP; ++p) ra[j][p] = ld16m(a.x + p * a.xps, aoff, va);
       }
 #pragma unroll
       for (int j = 0; j < NCB; ++j) {
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         const bool vb = kv && n < a.Nout;
         const long boff = (long)n * a.Ktot + k;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) rb[j][p] = vb ? ld16(a.w + p * a.wps + boff) : zero4;
+        for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.w + p * a.wps, boff, vb);
       }
     } else {
 #pragma unroll
@@ -248,7 +256,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         if (v) decode_row(a, (unsigned)m, img, oh, ow);
         const long off = (((long)img * a.P + oh) * a.Q + ow) * a.Nout + col;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) ra[j][p] = v ? ld16(a.w + p * a.wps + off) : zero4;
+        for (int p = 0; p < NP; ++p) ra[j][p] = ld16m(a.w + p * a.wps, off, v);
       }
 #pragma unroll
       for (int j = 0; j < NCB; ++j) {
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const long off = (((long)img * a.H + ih) * a.W + iw) * a.C + wb_c;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) rb[j][p] = v ? ld16(a.x + p * a.xps + off) : zero4;
+        for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.x + p * a.xps, off, v);
       }
     }
   };
@@ -345,11 +353,21 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     store_tile(0);
     __syncthreads();
     for (int kt = 0; kt < ntiles; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < ntiles) load_tile(kt + 1);
-      compute_tile(cur);
-      if (kt + 1 < ntiles) store_tile(cur ^ 1);
-      __syncthreads();
+      if constexpr (NSTAGE == 2) {
+        const int cur = kt & 1;
+        if (kt + 1 < ntiles) load_tile(kt + 1);
+        compute_tile(cur);
+        if (kt + 1 < ntiles) store_tile(cur ^ 1);
+        __syncthreads();
+      } else {
+        if (kt + 1 < ntiles) load_tile(kt + 1);
+        compute_tile(0);
+        if (kt + 1 < ntiles) {
+          __syncthreads();
+          store_tile(0);
+          __syncthreads();
+        }
+      }
     }
   }
 
@@ -467,24 +485,29 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float* __restr
   }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK>
+template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK, int NS>
 int launch_x3(const Args& a, hipStream_t st) {
   dim3 grid(a.gm * a.gn, a.splits);
-  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK><<<grid, WM * WN * 64, 0, st>>>(a);
+  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 
-// tile id -> (block tile, stage depth): 0: 128x128/k32  1: 64x64/k32  2: 128x128/k16  3: 64x64/k64
+// tile id -> (block tile, stage depth, LDS stages):
+//   0: 128x128/k32/2  1: 64x64/k32/2  2: 128x128/k16/2  3: 64x64/k64/2
+//   4: 128x128/k16/1  5: 128x128/k32/1  6: 64x64/k32/1
 template <int MODE, int NP>
 int launch_tile(const Args& a, int tile, hipStream_t st) {
   switch (tile) {
-    case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32>(a, st);
-    case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32>(a, st);
-    case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16>(a, st);
-    default: return launch_x3<64, 64, 1, 2, MODE, NP, 64>(a, st);
+    case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 2>(a, st);
+    case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 2>(a, st);
+    case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 2>(a, st);
+    case 3: return launch_x3<64, 64, 1, 2, MODE, NP, 64, 2>(a, st);
+    case 4: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 1>(a, st);
+    case 5: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 1>(a, st);
+    default: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 1>(a, st);
   }
 }
-int tile_rows(int tile) { return (tile == 0 || tile == 2) ? 128 : 64; }
+int tile_rows(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : 128; }
 
 int grid_1d(long n) {
   long g = (n + 255) / 256;

@@ -25,6 +25,8 @@ torch), which is what the multi-process gloo tests drive.
 """
 from __future__ import annotations
 
+import json
+import os
 from collections import OrderedDict
 from typing import Callable, Dict, List, Optional
 
@@ -69,13 +71,48 @@ def conv_cfg(kind: str, M: int, N: int, K: int):
     return 0, s
 
 
+IMPLS = ("fp32", "x3", "bf16")
+_TUNING = None
+
+
+def tuning_table() -> Dict[str, list]:
+    """Measured (tile, splits, posmajor) per conv call on MI355X (tools/tune_convs.py writes it)."""
+    global _TUNING
+    if _TUNING is None:
+        _TUNING = {}
+        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "mi355x.json")
+        if os.path.exists(p) and os.environ.get("DPA_NO_TUNING", "0") != "1":
+            with open(p) as f:
+                _TUNING = json.load(f)
+    return _TUNING
+
+
+def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
+    return f"{impl}|{kind}|{n}|{hw}|{cin}|{cout}"
+
+
 class VGGEngine:
+    """Static-schedule trainer.  ``impl`` selects the conv kernels of every layer whose input has a
+    multiple of 8 channels (the 3-channel first layer always runs the fp32-MFMA kernel):
+
+    * ``"fp32"`` — fp32 MFMA implicit GEMM (v_mfma_f32_32x32x2_f32), exact fp32 products;
+    * ``"x3"``   — fp32-grade results on bf16 MFMA: operands kept as three bf16 planes, six plane
+                   products per multiply (conv_x3.hip); error at fp32 rounding level;
+    * ``"bf16"`` — one bf16 plane (mixed precision: bf16 operands, fp32 accumulation/BN/SGD).
+    """
+
     def __init__(self, name: str = "VGG11", device="cuda", max_batch: int = 256, num_classes: int = 10,
                  lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4, bn_momentum: float = 0.1,
-                 bn_eps: float = 1e-5, in_hw: int = 32, backend=None):
+                 bn_eps: float = 1e-5, in_hw: int = 32, backend=None, impl: str = "fp32"):
         self.device = torch.device(device)
         self.spec = VGGSpec.from_name(name, num_classes, in_hw)
         self.K = backend if backend is not None else (_ext.require() if self.device.type == "cuda" else cpu_ref)
+        if impl not in IMPLS:
+            raise ValueError(f"impl must be one of {IMPLS}")
+        if self.K is cpu_ref:
+            impl = "fp32"  # the CPU oracle backend implements the fp32 kernel API only
+        self.impl = impl
+        self.np = {"fp32": 0, "x3": 3, "bf16": 1}[impl]
         self.max_batch = max_batch
         self._cfg_cache: Dict[tuple, tuple] = {}
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
@@ -103,29 +140,39 @@ class VGGEngine:
         f32 = dict(device=dev, dtype=torch.float32)
         self.x0 = torch.zeros(N, in_hw, in_hw, 4, **f32)
         self.target = torch.zeros(N, dtype=torch.int64, device=dev)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        # planes(i): layer i runs the bf16-plane kernels (needs cin % 8 == 0)
+        self.planes = [self.np > 0 and l.cin_pad % 8 == 0 for l in L]
         self.z, self.a, self.g, self.dz = [], [], [], []
+        self.a3: List[Optional[torch.Tensor]] = []   # planes of a[i] when layer i+1 consumes planes
+        self.dz3: List[Optional[torch.Tensor]] = []
+        self.w3: List[Optional[torch.Tensor]] = []
+        self.wd3: List[Optional[torch.Tensor]] = []
         self.stats = []  # per layer dict(mean, invstd, scale, shift)
         self.eval_ss = []
-        slab_need, part_need = 1, 1
-        for l in L:
+        part_need = 1
+        for i, l in enumerate(L):
             hw, ho = l.hw, (l.hw // 2 if l.pool else l.hw)
+            nxt_planes = i + 1 < len(L) and self.planes[i + 1]
             self.z.append(torch.empty(N, hw, hw, l.cout, **f32))
-            self.a.append(torch.empty(N, ho, ho, l.cout, **f32))
+            self.a.append(None if nxt_planes else torch.empty(N, ho, ho, l.cout, **f32))
+            self.a3.append(torch.empty(self.np, N, ho, ho, l.cout, **bf) if nxt_planes else None)
             self.g.append(torch.empty(N, ho, ho, l.cout, **f32))
-            self.dz.append(torch.empty(N, hw, hw, l.cout, **f32))
+            self.dz.append(None if self.planes[i] else torch.empty(N, hw, hw, l.cout, **f32))
+            self.dz3.append(torch.empty(self.np, N, hw, hw, l.cout, **bf) if self.planes[i] else None)
+            self.w3.append(torch.empty(self.np, l.cout, 3, 3, l.cin_pad, **bf) if self.planes[i] else None)
+            self.wd3.append(torch.empty(self.np, l.cin_pad, 3, 3, l.cout, **bf) if self.planes[i] else None)
             self.stats.append({k: torch.zeros(l.cout, **f32) for k in ("mean", "invstd", "scale", "shift")})
             self.eval_ss.append({k: torch.zeros(l.cout, **f32) for k in ("scale", "shift")})
-            M = N * hw * hw
-            for kind, (m, n, k) in (("fprop", (M, l.cout, 9 * l.cin_pad)), ("dgrad", (M, l.cin_pad, 9 * l.cout)),
-                                    ("wgrad", (M, l.cout, 9 * l.cin_pad))):
-                _, s = self._cfg("wgrad" if kind == "wgrad" else "fprop", m, n, k)
-                out = m * n if kind != "wgrad" else n * k
-                if s > 1:
-                    slab_need = max(slab_need, s * out)
-            Mo = N * ho * ho
-            part_need = max(part_need, 3 * ((M + 63) // 64) * l.cout, self.K.bn_part_floats(M, l.cout, False),
+            M, Mo = N * hw * hw, N * ho * ho
+            part_need = max(part_need, self.K.bn_part_floats(M, l.cout, False),
                             self.K.bn_part_floats(Mo, l.cout, True))
-        self.slab = torch.empty(slab_need, **f32)
+        self.slab = torch.empty(1, **f32)
+        for i in range(len(L)):  # size the split-K workspace for the full-batch plan
+            for kind in ("fprop", "dgrad", "wgrad"):
+                if kind == "dgrad" and i == 0:
+                    continue
+                self._ensure_slab(self._slab_need(i, kind, N))
         self.part = torch.empty(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
         self.loss_row = torch.zeros(N, **f32)
@@ -174,6 +221,14 @@ class VGGEngine:
             if extra:
                 raise KeyError(f"unexpected keys in state_dict: {sorted(extra)[:5]}")
         self._eval_dirty = True
+        self.refresh_weight_planes()
+
+    def refresh_weight_planes(self):
+        """Re-split the conv weights into the bf16 operand planes (W for forward, the flipped/
+        transposed Wd for the data gradient) — after every parameter update."""
+        for i, l in enumerate(self.spec.convs):
+            if self.planes[i]:
+                self.K.split_weights(self.params[f"{l.conv_key}.weight"], self.w3[i], self.wd3[i])
 
     @torch.no_grad()
     def state_dict(self, prefix: str = "") -> "OrderedDict[str, torch.Tensor]":
@@ -239,34 +294,153 @@ class VGGEngine:
             self.buffers.numels.values())
 
     # ------------------------------------------------------------------ kernel configs
-    def _cfg(self, kind, M, N, K):
-        """(tile, effective split count) for a conv GEMM."""
-        key = (kind, M, N, K)
+    def _layer_impl(self, i: int) -> str:
+        return self.impl if self.planes[i] else "fp32"
+
+    def conv_config(self, i: int, kind: str, n: int):
+        """(tile, effective splits, posmajor) for conv call `kind` of layer i at batch n: the measured
+        table (tuning/mi355x.json) when it has the call, else the heuristic."""
+        impl = self._layer_impl(i)
+        l = self.spec.convs[i]
+        key = (impl, kind, n, i)
         c = self._cfg_cache.get(key)
-        if c is None:
-            tile, s = conv_cfg(kind, M, N, K)
-            s = self.K.conv_splits(M if kind == "wgrad" else K, s)
-            c = (tile, s)
-            self._cfg_cache[key] = c
+        if c is not None:
+            return c
+        M = n * l.hw * l.hw
+        if kind == "fprop":
+            gm, gn, gk = M, l.cout, 9 * l.cin_pad
+        elif kind == "dgrad":
+            gm, gn, gk = M, l.cin_pad, 9 * l.cout
+        else:
+            gm, gn, gk = M, l.cout, 9 * l.cin_pad
+        t = tuning_table().get(conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout))
+        if t is not None:
+            tile, s, pm = int(t[0]), int(t[1]), bool(t[2])
+        elif impl == "fp32":
+            tile, s = conv_cfg("wgrad" if kind == "wgrad" else "fprop", gm, gn, gk)
+            pm = l.hw <= 8
+        else:  # bf16-plane kernels: 128x128/k32 tiles, ~512 blocks
+            cd = lambda a_, b_: (a_ + b_ - 1) // b_
+            tiles = cd(gn, 128) * cd(gk, 128) if kind == "wgrad" else cd(gm, 128) * cd(gn, 128)
+            red = gm if kind == "wgrad" else gk
+            tile, s = 0, max(1, min(128, _pow2_round(512 / max(tiles, 1))))
+            while s > 1 and red // s < 64:
+                s //= 2
+            pm = l.hw <= 4
+        if kind != "wgrad" or impl == "fp32":
+            s = self.K.conv_splits(gm if kind == "wgrad" else gk, s) if impl == "fp32" else self.K.x3_splits(gk, s)
+        else:
+            s = self.K.x3_splits(gm, s)
+        c = (tile, s, pm)
+        self._cfg_cache[key] = c
         return c
 
-    @staticmethod
-    def _posmajor(hw: int) -> bool:
-        """Position-major GEMM rows + padding-tap skipping pays on small feature maps
-        (conv_gemm.hip header: 2x2 maps do 4/9 of the taps)."""
-        return hw <= 8
+    def _slab_need(self, i: int, kind: str, n: int) -> int:
+        l = self.spec.convs[i]
+        _, s, _ = self.conv_config(i, kind, n)
+        if s <= 1:
+            return 0
+        M = n * l.hw * l.hw
+        out = {"fprop": M * l.cout, "dgrad": M * l.cin_pad, "wgrad": l.cout * 9 * l.cin_pad}[kind]
+        return s * out
 
-    def _conv(self, x, w, out, l_cin, l_cout, hw, n, reduce=True):
-        """Forward conv; returns the split count left UNREDUCED in self.slab (1 = result in out)."""
-        M = n * hw * hw
-        tile, s = self._cfg("fprop", M, l_cout, 9 * l_cin)
-        self.K.conv_fprop(x, w, out, self.slab if s > 1 else None, 1, 1, s, tile, False, reduce, self._posmajor(hw))
+    def conv_candidates(self, i: int, kind: str):
+        impl = self._layer_impl(i)
+        tiles = (0, 1) if impl == "fp32" else (0, 1, 2, 3, 4, 5, 6)
+        splits = (1, 2, 4, 8, 16, 32, 64, 128) if kind == "wgrad" else (1, 2, 4, 8, 16)
+        return [(t, s, pm) for t in tiles for s in splits for pm in (False, True)]
+
+    def autotune(self, n: Optional[int] = None, iters: int = 3, verbose: bool = False) -> Dict[str, list]:
+        """Time every candidate (tile, splits, posmajor) of every conv call of the step at batch n on
+        this GPU and adopt the fastest.  Returns {conv_key: [tile, splits, posmajor, ms]} (the
+        format of tuning/mi355x.json).  Buffers must hold one step's data (run a step first)."""
+        n = n or self.max_batch
+        res: Dict[str, list] = {}
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        L = self.spec.convs
+        for i, l in enumerate(L):
+            for kind in ("fprop", "dgrad", "wgrad"):
+                if kind == "dgrad" and i == 0:
+                    continue
+                impl = self._layer_impl(i)
+                key = (impl, kind, n, i)
+                best = None
+                for cand in self.conv_candidates(i, kind):
+                    tile, s, pm = cand
+                    M = n * l.hw * l.hw
+                    red = M if kind == "wgrad" else (9 * (l.cin_pad if kind == "fprop" else l.cout))
+                    s = (self.K.conv_splits(red, s) if impl == "fp32" else self.K.x3_splits(red, s))
+                    self._cfg_cache[key] = (tile, s, pm)
+                    fn = {"fprop": lambda: self._conv_fwd(i, self.x0[:n], n, reduce=False),
+                          "dgrad": lambda: self._conv_dgrad(i, n),
+                          "wgrad": lambda: self._conv_wgrad(i, self.x0[:n], n)}[kind]
+                    fn()
+                    ev0.record()
+                    for _ in range(iters):
+                        fn()
+                    ev1.record()
+                    torch.cuda.synchronize(self.device)
+                    ms = ev0.elapsed_time(ev1) / iters
+                    if best is None or ms < best[3]:
+                        best = [tile, s, pm, ms]
+                self._cfg_cache[key] = tuple(best[:3])
+                ck = conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout)
+                res[ck] = best
+                if verbose:
+                    print(ck, best, flush=True)
+        return res
+
+    def _ensure_slab(self, numel: int):
+        if numel > self.slab.numel():
+            self.slab = torch.empty(numel, device=self.device, dtype=torch.float32)
+
+    def _in_planes(self, i: int, n: int) -> torch.Tensor:
+        return self.a3[i - 1][:, :n]
+
+    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool) -> int:
+        """Forward conv of layer i into z[i] (or split-K slabs); returns the split count left
+        UNREDUCED in self.slab (1 = result is in z[i])."""
+        l = self.spec.convs[i]
+        tile, s, pm = self.conv_config(i, "fprop", n)
+        self._ensure_slab(self._slab_need(i, "fprop", n))
+        z = self.z[i][:n]
+        slab = self.slab if s > 1 else None
+        if self.planes[i]:
+            self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm)
+        else:
+            xin = x if i == 0 else self.a[i - 1][:n]
+            self.K.conv_fprop(xin, self.params[f"{l.conv_key}.weight"], z, slab, 1, 1, s, tile, False, reduce, pm)
         return 1 if (reduce or s == 1) else s
 
-    def _wgrad(self, x, dz, dw, cin, cout, hw, n):
-        M = n * hw * hw
-        tile, s = self._cfg("wgrad", M, cout, 9 * cin)
-        self.K.conv_wgrad(x, dz, dw, self.slab if s > 1 else None, 1, 1, s, tile, self._posmajor(hw))
+    def _conv_dgrad(self, i: int, n: int) -> int:
+        """Data gradient of layer i into g[i-1] (or slabs); returns the unreduced split count."""
+        l = self.spec.convs[i]
+        tile, s, pm = self.conv_config(i, "dgrad", n)
+        self._ensure_slab(self._slab_need(i, "dgrad", n))
+        slab = self.slab if s > 1 else None
+        out = self.g[i - 1][:n]
+        if self.planes[i]:
+            self.K.conv_x3_fprop(self.dz3[i][:, :n], self.wd3[i], out, slab, 1, 1, s, tile, False, pm)
+        else:
+            self.K.conv_fprop(self.dz[i][:n], self.params[f"{l.conv_key}.weight"], out, slab, 1, 1, s, tile, True,
+                              False, pm)
+        return s
+
+    def _conv_wgrad(self, i: int, x: torch.Tensor, n: int):
+        l = self.spec.convs[i]
+        tile, s, pm = self.conv_config(i, "wgrad", n)
+        self._ensure_slab(self._slab_need(i, "wgrad", n))
+        slab = self.slab if s > 1 else None
+        dw = self.grads[f"{l.conv_key}.weight"]
+        if self.planes[i]:
+            self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
+        else:
+            xin = x if i == 0 else self.a[i - 1][:n]
+            self.K.conv_wgrad(xin, self.dz[i][:n], dw, slab, 1, 1, s, tile, pm)
+
+    def _act_out(self, i: int, n: int) -> torch.Tensor:
+        """Where bn_apply of layer i writes: bf16 planes if layer i+1 consumes planes, else fp32."""
+        return self.a3[i][:, :n] if self.a3[i] is not None else self.a[i][:n]
 
     # ------------------------------------------------------------------ training step
     def forward_backward(self, x: torch.Tensor, target: torch.Tensor,
@@ -280,18 +454,16 @@ class VGGEngine:
         L = self.spec.convs
         if pre_forward is not None:
             pre_forward()
-        inp = x
         for i, l in enumerate(L):
-            z, a, st = self.z[i][:n], self.a[i][:n], self.stats[i]
-            ns = self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n, reduce=False)
+            z, st = self.z[i][:n], self.stats[i]
+            ns = self._conv_fwd(i, x, n, reduce=False)
             K.bn_fwd_stats(self.slab if ns > 1 else z, ns, z, self.part, P[f"{l.bn_key}.weight"],
                            P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                            self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"], self.bn_momentum,
                            self.bn_eps)
-            K.bn_apply(z, a, st["scale"], st["shift"], l.pool)
-            inp = a
-        feat = inp.view(n, -1)
+            K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
+        feat = self.a[-1][:n].view(n, -1)
         K.fc_ce_train(feat, P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n], self.dlogits[:n],
                       self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
         if grad_ready is not None:
@@ -300,23 +472,18 @@ class VGGEngine:
         for i in range(len(L) - 1, -1, -1):
             l = L[i]
             st = self.stats[i]
-            z, dz = self.z[i][:n], self.dz[i][:n]
+            z = self.z[i][:n]
             g = self.g[i][:n]
+            dzbuf = self.dz3[i][:, :n] if self.planes[i] else self.dz[i][:n]
             K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                      st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                     G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dz, l.pool)
-            xin = x if i == 0 else self.a[i - 1][:n]
-            # wgrad first: it must consume the slab workspace-free dz before the dgrad's split-K
-            # slabs (which bn_bwd of layer i-1 reads) are written
-            self._wgrad(xin, dz, G[f"{l.conv_key}.weight"], l.cin_pad, l.cout, l.hw, n)
+                     G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool)
+            # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early
+            self._conv_wgrad(i, x, n)
             if grad_ready is not None:
                 grad_ready([f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"])
             if i > 0:
-                M = n * l.hw * l.hw
-                tile, s = self._cfg("fprop", M, l.cin_pad, 9 * l.cout)
-                K.conv_fprop(dz, P[f"{l.conv_key}.weight"], self.g[i - 1][:n], self.slab if s > 1 else None, 1, 1, s,
-                             tile, True, False, self._posmajor(l.hw))
-                gsplit = s
+                gsplit = self._conv_dgrad(i, n)
         self._eval_dirty = True
         return self.loss
 
@@ -328,6 +495,7 @@ class VGGEngine:
     def finish_step(self):
         self.steps_taken += 1
         self._eval_dirty = True
+        self.refresh_weight_planes()
 
     # ------------------------------------------------------------------ evaluation
     def begin_eval(self):
@@ -346,12 +514,11 @@ class VGGEngine:
             raise RuntimeError("call begin_eval() after the last parameter update")
         n = x.shape[0]
         P = self.params
-        inp = x
         for i, l in enumerate(self.spec.convs):
-            z, a = self.z[i][:n], self.a[i][:n]
-            self._conv(inp, P[f"{l.conv_key}.weight"], z, l.cin_pad, l.cout, l.hw, n, reduce=True)
-            self.K.bn_apply(z, a, self.eval_ss[i]["scale"], self.eval_ss[i]["shift"], l.pool)
-            inp = a
+            self._conv_fwd(i, x, n, reduce=True)
+            self.K.bn_apply(self.z[i][:n], self._act_out(i, n), self.eval_ss[i]["scale"], self.eval_ss[i]["shift"],
+                            l.pool)
+        inp = self.a[-1][:n]
         self.K.fc_ce_eval(inp.view(n, -1), P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n],
                           self.correct[:n], logits, self.eval_acc)
         return self.eval_acc

@@ -112,6 +112,7 @@ class GradSync:
             if e.steps_taken > 0:
                 self.comm.broadcast(e.mom.flat, 0)
         self.comm.wait()
+        e.refresh_weight_planes()
 
     def pre_forward(self):
         pass

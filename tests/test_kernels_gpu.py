@@ -162,7 +162,7 @@ def test_split_planes_exact():
 
 @pytest.mark.parametrize("shape", X3_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("posmajor", [False, True])
 @pytest.mark.parametrize("np_", [3, 1])
 def test_conv_x3_fprop(shape, splits, tile, posmajor, np_):
@@ -207,7 +207,7 @@ def test_conv_x3_dgrad_via_split_weights(shape, posmajor):
 
 @pytest.mark.parametrize("shape", X3_SHAPES)
 @pytest.mark.parametrize("splits", [1, 7])
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("posmajor", [False, True])
 @pytest.mark.parametrize("np_", [3, 1])
 def test_conv_x3_wgrad(shape, splits, tile, posmajor, np_):

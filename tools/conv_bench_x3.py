@@ -52,7 +52,7 @@ def main():
         best = {}
         for kind in ("fprop", "dgrad", "wgrad"):
             res = []
-            for tile, pm in [(t, p) for t in (0, 1, 2, 3) for p in (False, True)]:
+            for tile, pm in [(t, p) for t in (0, 1, 2, 3, 4, 5, 6) for p in (False, True)]:
                 for splits in (1, 2, 4, 8, 16, 32, 64, 128):
                     if kind != "wgrad" and splits > 16:
                         continue
