@@ -46,8 +46,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--device", default="auto")
-    ap.add_argument("--impl", default="fp32", choices=["fp32", "x3", "bf16"],
-                    help="conv kernels: fp32 MFMA | fp32-grade bf16x6 planes | bf16 (mixed precision)")
+    ap.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
+                    help="conv kernels: x3 = fp32-grade results from bf16 matrix cores (3 bf16 planes per "
+                         "operand, 6 plane products; default) | fp32 = fp32 MFMA | bf16 = mixed precision")
     a = ap.parse_args()
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))

@@ -126,6 +126,8 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--test-size", type=int, default=10000)
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     g.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    g.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
+                   help="GPU conv kernels: x3 (fp32-grade via bf16 planes, default) | fp32 MFMA | bf16")
     g.add_argument("--bucket-mb", type=float, default=None)
     g.add_argument("--no-overlap", action="store_true", help="sync after backward (reference placement)")
     g.add_argument("--checkpoint-dir", default=None)
@@ -150,7 +152,7 @@ def run(ctx: DistContext, mode: str, args):
                                 seed=args.seed * 7919 + ctx.rank)
     test_loader = DeviceLoader(test_set, args.batch_size, ctx.device, sampler=None, train=False)
     engine = VGGEngine(args.model, ctx.device, max_batch=args.batch_size, lr=args.lr, momentum=args.momentum,
-                       weight_decay=args.weight_decay)
+                       weight_decay=args.weight_decay, impl=args.impl)
     engine.init_parameters(seed=args.seed)
     start_epoch, start_batch = 0, 0
     if args.resume and args.checkpoint_dir:
