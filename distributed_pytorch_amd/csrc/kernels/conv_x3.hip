@@ -494,10 +494,11 @@ int launch_x3(const Args& a, hipStream_t st) {
 
 // tile id -> (block tile, stage depth, LDS stages):
 //   0: 128x128/k32/2  1: 64x64/k32/2  2: 128x128/k16/2  3: 64x64/k64/2
-//   4: 128x128/k16/1  5: 128x128/k32/1  6: 64x64/k32/1
+//   4: 128x128/k16/1  5: 128x128/k32/1  6: 64x64/k32/1  7: 256x128/k32/1 (8 waves)
 template <int MODE, int NP>
 int launch_tile(const Args& a, int tile, hipStream_t st) {
   switch (tile) {
+    case 7: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 1>(a, st);
     case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 2>(a, st);
     case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 2>(a, st);
     case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 2>(a, st);
@@ -507,7 +508,8 @@ int launch_tile(const Args& a, int tile, hipStream_t st) {
     default: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 1>(a, st);
   }
 }
-int tile_rows(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : 128; }
+int tile_rows(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : (tile == 7 ? 256 : 128); }
+int tile_cols(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : 128; }
 
 int grid_1d(long n) {
   long g = (n + 255) / 256;
@@ -562,9 +564,8 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out
   fill(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
   if (C % 8 || Kout % 8) return -2;
-  const int T = tile_rows(tile);
-  a.gm = cdiv(a.M, T);
-  a.gn = cdiv(Kout, T);
+  a.gm = cdiv(a.M, tile_rows(tile));
+  a.gn = cdiv(Kout, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor ? 1 : 0;
   a.out = a.splits > 1 ? slab : out;
@@ -591,9 +592,8 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   fill(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
   if (C % 8 || Kout % 8) return -2;
-  const int T = tile_rows(tile);
-  a.gm = cdiv(Kout, T);
-  a.gn = cdiv(a.Ktot, T);
+  a.gm = cdiv(Kout, tile_rows(tile));
+  a.gn = cdiv(a.Ktot, tile_cols(tile));
   a.splits = xsplits(a.M, splits);
   a.posmajor = posmajor ? 1 : 0;
   a.out = a.splits > 1 ? slab : dw;

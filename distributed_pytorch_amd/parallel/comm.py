@@ -156,6 +156,18 @@ class TorchComm(Comm):
         dist.barrier(group=self.group)
 
 
+def exchange_unique_id(store, rank: int, make_uid, tag: str = "dpa_rccl_uid", timeout_s: Optional[int] = None) -> bytes:
+    """Rank 0 creates the RCCL unique id and publishes it in the rendezvous store; every other rank
+    blocks (bounded) until it appears.  (Replaces the store half of NCCL's bootstrap.)"""
+    timeout_s = timeout_s or int(os.environ.get("DPA_RCCL_INIT_TIMEOUT", "600"))
+    if rank == 0:
+        uid = bytes(make_uid())
+        store.set(tag, uid)
+        return uid
+    store.wait([tag], datetime.timedelta(seconds=timeout_s))
+    return bytes(store.get(tag))
+
+
 class RcclComm(Comm):
     """Native RCCL communicator (one per process/GPU)."""
 
@@ -171,12 +183,7 @@ class RcclComm(Comm):
         if uid is None:
             if store is None:
                 raise ValueError("RcclComm needs a store (or an explicit unique id) for bootstrap")
-            if rank == 0:
-                uid = C.rccl_unique_id()
-                store.set(tag, uid)
-            else:
-                store.wait([tag], datetime.timedelta(seconds=int(os.environ.get("DPA_RCCL_INIT_TIMEOUT", "600"))))
-                uid = store.get(tag)
+            uid = exchange_unique_id(store, rank, C.rccl_unique_id, tag)
         with torch.cuda.device(self.device):
             self._c = C.RcclComm(rank, world, bytes(uid), self.device.index or 0)
         self.stream = torch.cuda.ExternalStream(self._c.stream_ptr(), device=self.device)

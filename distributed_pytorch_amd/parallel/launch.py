@@ -59,6 +59,12 @@ def pick_device(local_rank: int, want: str = "auto") -> torch.device:
 
 def _make_comm(kind: str, rank: int, world: int, device: torch.device) -> Comm:
     if world == 1:
+        # DPA_FORCE_COMM=1 runs the real RCCL communicator even on one GPU (a 1-rank communicator:
+        # every collective is an identity), exercising the stream/event/bucket path on a 1-GPU box
+        if os.environ.get("DPA_FORCE_COMM", "0") == "1" and device.type == "cuda":
+            from .. import _ext
+
+            return RcclComm(0, 1, device, uid=_ext.require().rccl_unique_id())
         return NullComm()
     if device.type != "cuda":
         return TorchComm(device=device)

@@ -92,6 +92,7 @@ class GradSync:
         self.engine = engine
         self.comm = comm
         self.world = comm.world
+        self.active = comm.name != "null"  # a real communicator (also a forced 1-rank one)
         self.overlap = overlap
         order = [["fc1.weight", "fc1.bias"]] + [
             [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
@@ -99,7 +100,7 @@ class GradSync:
         self.buckets = plan_buckets(engine.grads, order, bucket_mb)
         self._by_name: Dict[str, Bucket] = {n: b for b in self.buckets for n in b.names}
         self.issued_bytes = 0
-        if broadcast_init and self.world > 1:
+        if broadcast_init and self.active:
             self.broadcast_state()
 
     # -- state broadcast (DDP ctor semantics; torch distributed.py:862-871) --
@@ -123,7 +124,7 @@ class GradSync:
             b.issued = False
 
     def grad_ready(self, names: List[str]):
-        if self.world == 1:
+        if not self.active:
             return
         for n in names:
             b = self._by_name.get(n)
@@ -145,7 +146,7 @@ class GradSync:
     def finish(self) -> float:
         """Issue whatever is left, make the compute stream wait for the comm stream, and return
         the scale the optimizer must apply to the synced grads."""
-        if self.world == 1:
+        if not self.active:
             return 1.0
         for b in self.buckets:
             if not b.issued:
@@ -165,7 +166,7 @@ class GatherScatterSync(GradSync):
     def __init__(self, engine, comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
         super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
         self._recv = None
-        if comm.rank == 0 and comm.world > 1:
+        if comm.rank == 0 and self.active:
             mx = max(b.numel for b in self.buckets)
             self._recv = torch.empty(comm.world * mx, device=engine.device, dtype=torch.float32)
 
@@ -203,7 +204,7 @@ class DDPSync(GradSync):
     def pre_forward(self):
         # DDP._sync_buffers: rank 0's BN running stats/counters overwrite every replica's before
         # each training forward (torch nn/parallel/distributed.py:2178).
-        if self.world == 1 or not self.broadcast_buffers:
+        if not self.active or not self.broadcast_buffers:
             return
         e = self.engine
         with self.comm.region():

@@ -104,3 +104,16 @@ def run_cli_main(rank, world, port, script, args, outfile):
         runpy.run_path(os.path.join(root, script), run_name="__main__")
     with open(outfile, "w") as f:
         f.write(buf.getvalue())
+
+
+def run_uid_exchange(rank, world, port, outdir):
+    """The RCCL bootstrap's store exchange, with a fake id generator (runs on CPU/gloo)."""
+    from distributed_pytorch_amd.parallel.comm import exchange_unique_id
+
+    _init(rank, world, port)
+    store = dist.distributed_c10d._get_default_store()
+    uid = exchange_unique_id(store, rank, lambda: bytes(range(128)), tag="test_uid")
+    with open(os.path.join(outdir, f"uid_{rank}.bin"), "wb") as f:
+        f.write(uid)
+    dist.barrier()
+    dist.destroy_process_group()

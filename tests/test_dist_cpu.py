@@ -108,3 +108,10 @@ def test_cli_entrypoints_log_format(tmp_path, script):
         assert [LOSS_RE.match(l).groups() for l in loss_lines] == [("1", "20"), ("21", "40")]
         assert [TIME_RE.match(l).groups() for l in time_lines] == [("2", "40")]
         assert len(test_lines) == 1 and TEST_RE.match(test_lines[0]).group(1) == "40"
+
+
+def test_rccl_bootstrap_store_exchange(tmp_path):
+    _spawn(H.run_uid_exchange, str(tmp_path))
+    a = open(tmp_path / "uid_0.bin", "rb").read()
+    b = open(tmp_path / "uid_1.bin", "rb").read()
+    assert a == b == bytes(range(128))

@@ -273,3 +273,36 @@ def test_engine_training_converges_and_evaluates(impl):
         e.eval_batch(x, t)
     acc = e.eval_acc.cpu()
     assert 0 <= acc[1] <= 256 and acc[0] == acc[0]
+
+
+@pytest.mark.parametrize("mode", ["ddp", "allreduce", "gather"])
+def test_sync_modes_through_native_rccl_single_rank(mode):
+    """A 1-rank native RCCL communicator (every collective is an identity) driving the real
+    bucket / comm-stream / event path: results must equal the no-communication run bit for bit."""
+    from distributed_pytorch_amd import _ext
+    from distributed_pytorch_amd.engine import VGGEngine
+    from distributed_pytorch_amd.parallel import NullComm, RcclComm, make_sync
+
+    C = _ext.require()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(9)
+    xs = [torch.randn(32, 32, 32, 4, generator=g) for _ in range(3)]
+    ts = [torch.randint(0, 10, (32,), generator=g) for _ in range(3)]
+    outs = []
+    for comm in (NullComm(), RcclComm(0, 1, dev, uid=C.rccl_unique_id())):
+        e = VGGEngine("VGG11", dev, max_batch=32, impl="x3", lr=0.01)
+        e.init_parameters(seed=3)
+        sync = make_sync(mode, e, comm, bucket_mb=1.0 if mode == "ddp" else None)
+        for x, t in zip(xs, ts):
+            x = x.cuda()
+            x[..., 3] = 0
+            sync.begin_step()
+            e.forward_backward(x, t.cuda(), grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+            gs = sync.finish()
+            e.sgd_step(gs)
+            e.finish_step()
+        torch.cuda.synchronize()
+        comm.check()
+        outs.append(e.params.flat.clone())
+        comm.close()
+    assert torch.equal(outs[0], outs[1])
