@@ -410,8 +410,8 @@ ncclRedOp_t nccl_op(const std::string& op) {
 
 class PyRcclComm {
  public:
-  PyRcclComm(int rank, int world, py::bytes uid, int device)
-      : stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)),
+  PyRcclComm(int rank, int world, py::bytes uid, int device, bool high_priority)
+      : stream_(c10::hip::getStreamFromPool(high_priority, (c10::DeviceIndex)device)),
         comm_(rank, world, std::string(uid), device, stream_.stream()) {}
 
   void track(const Tensor& t) { c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_); }
@@ -504,7 +504,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rccl_unique_id", []() { return py::bytes(dpa::RcclComm::unique_id()); });
   m.def("rccl_version", &dpa::RcclComm::version);
   py::class_<PyRcclComm>(m, "RcclComm")
-      .def(py::init<int, int, py::bytes, int>(), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+      .def(py::init<int, int, py::bytes, int, bool>(), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"),
+           py::arg("high_priority") = false)
       .def("all_reduce", &PyRcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
       .def("broadcast", &PyRcclComm::broadcast)
       .def("gather", &PyRcclComm::gather)

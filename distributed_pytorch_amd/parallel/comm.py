@@ -185,7 +185,8 @@ class RcclComm(Comm):
                 raise ValueError("RcclComm needs a store (or an explicit unique id) for bootstrap")
             uid = exchange_unique_id(store, rank, C.rccl_unique_id, tag)
         with torch.cuda.device(self.device):
-            self._c = C.RcclComm(rank, world, bytes(uid), self.device.index or 0)
+            self._c = C.RcclComm(rank, world, bytes(uid), self.device.index or 0,
+                                 os.environ.get("DPA_COMM_HIPRIO", "0") == "1")
         self.stream = torch.cuda.ExternalStream(self._c.stream_ptr(), device=self.device)
         self._store = store
 
