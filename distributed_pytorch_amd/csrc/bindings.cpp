@@ -8,7 +8,7 @@
 
 extern "C" {
 int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd, float gscale,
-                 int first, hipStream_t s);
+                 int first, unsigned short* planes, long ps, int np, hipStream_t s);
 int dpa_scale(float* x, long n, float sc, hipStream_t s);
 int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
@@ -43,8 +43,9 @@ int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* d
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
                       int posmajor, int np, hipStream_t st);
 int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
-int dpa_split_weights(const float* w, unsigned short* w3, unsigned short* wd3, int K, int R, int S, int C, int np,
-                      hipStream_t st);
+int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, float* dx, float* slab,
+                      int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
+                      int tile, int reduce, int posmajor, int np, hipStream_t st);
 int dpa_augment(const unsigned char* img, const long long* idx, const long long* labels, float* out,
                 long long* target, int B, int Hs, int Ws, int pad, int train, unsigned long long seed,
                 unsigned long long salt, const float* mean, const float* std, hipStream_t st);
@@ -71,16 +72,29 @@ float* fp(const Tensor& t) { return t.data_ptr<float>(); }
 float* ofp(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
 
 // ---------------- optimizer / elementwise ----------------
+// planes (optional): bf16 [NP, p.numel()] operand planes of the whole arena, refreshed in the same pass
 void sgd_flat(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double wd, double gscale, bool first,
-              int64_t offset, int64_t count) {
+              int64_t offset, int64_t count, OptT planes) {
   need(p, "p");
   need(g, "g");
   need(buf, "buf");
   if (count < 0) count = p.numel() - offset;
   TORCH_CHECK(offset % 4 == 0 && count % 4 == 0, "sgd_flat: offset/count must be multiples of 4");
   TORCH_CHECK(offset + count <= p.numel() && p.numel() == g.numel() && p.numel() == buf.numel(), "sgd_flat sizes");
+  unsigned short* pl = nullptr;
+  long ps = 0;
+  int np = 0;
+  if (planes.has_value() && planes->defined()) {
+    const Tensor& t = *planes;
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 &&
+                    (t.size(0) == 1 || t.size(0) == 3) && t.size(1) == p.numel(),
+                "sgd_flat: planes must be contiguous bfloat16 [NP, p.numel()]");
+    np = t.size(0);
+    ps = t.stride(0);
+    pl = reinterpret_cast<unsigned short*>(t.data_ptr<at::BFloat16>()) + offset;
+  }
   chk(dpa_sgd_flat(fp(p) + offset, fp(g) + offset, fp(buf) + offset, count, (float)lr, (float)momentum, (float)wd,
-                   (float)gscale, first ? 1 : 0, cur_stream()),
+                   (float)gscale, first ? 1 : 0, pl, ps, np, cur_stream()),
       "sgd_flat");
 }
 
@@ -167,10 +181,15 @@ void wflip(Tensor w, Tensor wd) {
 using u16 = unsigned short;
 u16* up(const Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr<at::BFloat16>()); }
 
+// Each plane must be contiguous and 16-byte aligned; planes may be strided views of a larger
+// buffer (e.g. the engine's weight-plane arena) as long as the plane stride keeps that alignment.
 void need_planes(const Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16 planes");
   TORCH_CHECK(t.size(0) == 1 || t.size(0) == 3, name, " must have 1 or 3 planes in dim 0");
+  TORCH_CHECK(t.select(0, 0).is_contiguous(), name, ": each plane must be contiguous");
+  TORCH_CHECK(t.size(0) == 1 || t.stride(0) % 8 == 0, name, ": plane stride must be a multiple of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, ": planes must be 16-byte aligned");
 }
 
 int64_t x3_splits(int64_t Kred, int64_t splits) { return dpa_x3_splits((int)Kred, (int)splits); }
@@ -227,6 +246,35 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
       "conv_x3_wgrad");
 }
 
+// dz3 [NP,N,Hd,Wd,K], w3 [NP,K,R,S,C] (forward weight planes), dx [N,H,W,C] fp32: data gradient of
+// conv(x, w, stride, pad); stride a power of two.
+void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, int64_t pad, int64_t splits,
+                   int64_t tile, bool reduce, bool posmajor) {
+  need_planes(dz3, "dz3");
+  need_planes(w3, "w3");
+  need(dx, "dx");
+  const int np = dz3.size(0);
+  TORCH_CHECK(w3.size(0) == np, "plane count mismatch");
+  const int N = dz3.size(1), Hd = dz3.size(2), Wd = dz3.size(3), K = dz3.size(4);
+  const int R = w3.size(2), S = w3.size(3), C = w3.size(4);
+  TORCH_CHECK(w3.size(1) == K, "conv_x3_dgrad: weight K mismatch");
+  const int H = dx.size(1), W = dx.size(2);
+  TORCH_CHECK(dx.size(0) == N && dx.size(3) == C, "conv_x3_dgrad: dx shape");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == Hd && (W + 2 * pad - S) / stride + 1 == Wd,
+              "conv_x3_dgrad: dz spatial does not match conv(dx)");
+  float* sl = nullptr;
+  const int eff = dpa_x3_splits(R * S * K, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_dgrad: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * C, "conv_x3_dgrad: slab too small");
+    sl = fp(*slab);
+  }
+  chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), fp(dx), sl, N, Hd, Wd, K, C, R, S, (int)stride,
+                        (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, cur_stream()),
+      "conv_x3_dgrad");
+}
+
 // x fp32 (any shape) -> out [NP, *x.shape] bf16 planes
 void split_planes(Tensor x, Tensor out) {
   need(x, "x");
@@ -235,18 +283,6 @@ void split_planes(Tensor x, Tensor out) {
   chk(dpa_split_planes(fp(x), up(out), x.numel(), out.stride(0), out.size(0), cur_stream()), "split_planes");
 }
 
-// w [K,R,S,C] fp32 -> w3 [NP,K,R,S,C] and (optional) wd3 [NP,C,R,S,K] (flipped, for the data gradient)
-void split_weights(Tensor w, Tensor w3, OptT wd3) {
-  need(w, "w");
-  need_planes(w3, "w3");
-  u16* wdp = nullptr;
-  if (wd3.has_value() && wd3->defined()) {
-    need_planes(*wd3, "wd3");
-    wdp = up(*wd3);
-  }
-  chk(dpa_split_weights(fp(w), up(w3), wdp, w.size(0), w.size(1), w.size(2), w.size(3), w3.size(0), cur_stream()),
-      "split_weights");
-}
 
 // ---------------- batch norm ----------------
 int64_t bn_part_floats(int64_t M, int64_t C, bool bwd) { return dpa_bn_part_floats((int)M, (int)C, bwd ? 1 : 0); }
@@ -475,7 +511,8 @@ class PyRcclComm {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_pytorch_amd native extension (gfx950 HIP kernels + RCCL communicator)";
   m.def("sgd_flat", &sgd_flat, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
-        py::arg("wd"), py::arg("gscale"), py::arg("first"), py::arg("offset") = 0, py::arg("count") = -1);
+        py::arg("wd"), py::arg("gscale"), py::arg("first"), py::arg("offset") = 0, py::arg("count") = -1,
+        py::arg("planes") = py::none());
   m.def("scale_", &scale_);
   m.def("mean_of_w", &mean_of_w);
   m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
@@ -491,8 +528,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("posmajor") = false);
   m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
+  m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
+        py::arg("posmajor") = false);
   m.def("split_planes", &split_planes);
-  m.def("split_weights", &split_weights);
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);

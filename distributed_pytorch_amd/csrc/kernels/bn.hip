@@ -52,13 +52,6 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
 
 // ---- output writer: NP == 0 -> fp32 float4 store; NP in {1,3} -> bf16 planes x = x0 (+ x1 + x2)
 // (round-to-nearest-even splits, conv_x3.hip header) so the next conv reads MFMA-ready operands.
-typedef unsigned short u16;
-__device__ __forceinline__ u16 bf16_rne(float f) {
-  unsigned u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (u16)(u >> 16);
-}
-__device__ __forceinline__ float bf16_f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
 
 template <int NP>
 __device__ __forceinline__ void store4(float* f, u16* pl, long ps, long i4, float4 v) {

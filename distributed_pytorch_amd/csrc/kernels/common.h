@@ -37,3 +37,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
+
+// ---- fp32 -> bf16 operand planes (round-to-nearest-even): x = x0 (+ x1 + x2) ----
+// NP = 3 carries the full 24-bit fp32 mantissa (conv_x3.hip header); NP = 1 is plain bf16.
+typedef unsigned short u16;
+__device__ __forceinline__ u16 bf16_rne(float f) {
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+__device__ __forceinline__ float bf16_f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
+
+template <int NP>
+__device__ __forceinline__ void split_val(float v, u16* o) {
+  const u16 h0 = bf16_rne(v);
+  o[0] = h0;
+  if (NP == 3) {
+    const float r1 = v - bf16_f(h0);
+    const u16 h1 = bf16_rne(r1);
+    o[1] = h1;
+    o[2] = bf16_rne(r1 - bf16_f(h1));
+  }
+}

@@ -15,18 +15,20 @@
 // (register-staged, double-buffered, one barrier per 16-deep k step) and feeds MFMAs.
 //
 // Modes (same GEMM formulations and position-major tap skipping as conv_gemm.hip):
-//   FPROP  out[m][n] = sum_k Xcol[m][k] W[n][k]      (dgrad = FPROP of dZ with the flipped,
-//                                                     transposed weight planes Wd[c][r][s][k])
-//   WGRAD  dW[n][k]  = sum_m dZ[m][n] Xcol[m][k]     (operands are m-major in memory: the LDS
-//          images keep the loaded [m][col] order and the MFMA fragments are fetched with the
-//          gfx950 transpose read ds_read_b64_tr_b16)
+//   FPROP  out[m][n] = sum_k Xcol[m][k] W[n][k]
+//   DGRAD  dX[m][c]  = sum_{(r,s,k)} dZcol[m][(r,s,k)] W[k][R-1-r][S-1-s][c]: the FPROP gather of
+//          dZ (padding R-1-pad; a forward stride st becomes an input dilation: tap (r,s) of
+//          output row (h,w) reads dZ[(h-pad'+r)/st] only when divisible) against the weight
+//          planes read in place, row-contiguous ([(r,s,k)][c]) -- no flipped weight copy
+//   WGRAD  dW[n][k]  = sum_m dZ[m][n] Xcol[m][k]
+// Row-contiguous operands (WGRAD A and B, DGRAD B) keep the loaded [k][col] order in LDS and the
+// MFMA fragments are fetched with the gfx950 transpose read ds_read_b64_tr_b16.
 // Tiles: T128 = 128x128 block, 2x2 waves of 64x64 (2x2 32x32 sub-tiles); T64 = 64x64 block, 1x2
 // waves of 64x32.  Each thread stages one 16-byte chunk per plane per operand per k step.
 #include "common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef unsigned short u16;
 
 namespace {
 
@@ -67,6 +69,7 @@ struct Args {
   int N, H, W, C, P, Q, R, S, stride, pad;
   int M, Nout, Ktot;
   int gm, gn, splits, posmajor;
+  int imask, ishift;  // input dilation (DGRAD of a strided conv): 2^ishift, imask = 2^ishift - 1
   FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
 };
 
@@ -92,7 +95,7 @@ __device__ __forceinline__ uint4 ld16m(const u16* base, long off, bool valid) {
   return valid ? v : make_uint4(0u, 0u, 0u, 0u);
 }
 
-enum { XM_FPROP = 0, XM_WGRAD = 2 };
+enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
 
 // BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  k-contiguous LDS rows are
 // BK+8 bf16 long (48/80/144 B: the 16 rows of every ds_read_b128 lane group hit 16 distinct 16-B
@@ -103,20 +106,24 @@ enum { XM_FPROP = 0, XM_WGRAD = 2 };
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK, int NSTAGE>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
   constexpr bool WG = MODE == XM_WGRAD;
+  constexpr bool DG = MODE == XM_DGRAD;
+  constexpr bool ARC = WG, BRC = WG || DG;  // operand images row-contiguous ([k][col]) in LDS
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
   constexpr int CPR = BK / 8;  // 16-B chunks per k-contiguous row
   // staging: every thread owns NCA / NCB 16-byte chunks per plane of A / B per stage
-  constexpr int NCA = WG ? BK * BM / 8 / THREADS : BM * CPR / THREADS;
-  constexpr int NCB = WG ? BK * BN / 8 / THREADS : BN * CPR / THREADS;
-  static_assert(NCA >= 1 && NCB >= 1 && (WG ? (BK * BM / 8) % THREADS == 0 : (BM * CPR) % THREADS == 0),
-                "tile/threads mismatch");
-  static_assert(WG ? THREADS % (BM / 8) == 0 && THREADS % (BN / 8) == 0 : THREADS % CPR == 0, "slot mapping");
-  constexpr int APITCH = WG ? BM + 32 : BK + 8;  // bf16 per LDS row
-  constexpr int BPITCH = WG ? BN + 32 : BK + 8;
-  constexpr int AROWS = WG ? BK : BM, BROWS = WG ? BK : BN;
+  constexpr int NCA = ARC ? BK * BM / 8 / THREADS : BM * CPR / THREADS;
+  constexpr int NCB = BRC ? BK * BN / 8 / THREADS : BN * CPR / THREADS;
+  static_assert(NCA >= 1 && NCB >= 1, "tile/threads mismatch");
+  static_assert(ARC ? (BK * BM / 8) % THREADS == 0 && THREADS % (BM / 8) == 0
+                    : (BM * CPR) % THREADS == 0 && THREADS % CPR == 0, "A slot mapping");
+  static_assert(BRC ? (BK * BN / 8) % THREADS == 0 && THREADS % (BN / 8) == 0
+                    : (BN * CPR) % THREADS == 0 && THREADS % CPR == 0, "B slot mapping");
+  constexpr int APITCH = ARC ? BM + 32 : BK + 8;  // bf16 per LDS row
+  constexpr int BPITCH = BRC ? BN + 32 : BK + 8;
+  constexpr int AROWS = ARC ? BK : BM, BROWS = BRC ? BK : BN;
   constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
   constexpr int STAGE = NP * (A_PLANE + B_PLANE);
   __shared__ __attribute__((aligned(16))) u16 lds[NSTAGE * STAGE];
@@ -138,7 +145,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   int lo0 = 0, lo1 = 0, span1 = 1, per = 1, ntot;
   if constexpr (!WG) {
     ntot = (a.Ktot + BK - 1) / BK;
-    if (a.posmajor && a.C % BK == 0 && a.N % BM == 0) {
+    if (a.posmajor && a.imask == 0 && a.C % BK == 0 && a.N % BM == 0) {
       const int pos = m0 / a.N;
       const int oh = pos / a.Q, ow = pos - (pos / a.Q) * a.Q;
       const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
@@ -185,12 +192,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   // ---------------- per-thread staging slots ----------------
   // FPROP: chunk (row, kc) with kc = tid % CPR fixed, rows tid/CPR + j*(THREADS/CPR).
   // WGRAD: chunk (m-row, col) with col = tid % (cols/8) fixed, m-rows tid/(cols/8) + j*step.
-  constexpr int AROWSTEP = WG ? THREADS / (BM / 8) : THREADS / CPR;
-  constexpr int BROWSTEP = WG ? THREADS / (BN / 8) : THREADS / CPR;
-  const int a_r0 = WG ? tid / (BM / 8) : tid / CPR;
-  const int b_r0 = WG ? tid / (BN / 8) : tid / CPR;
-  const int a_c8 = WG ? (tid % (BM / 8)) * 8 : (tid % CPR) * 8;  // column (WGRAD) / k offset (FPROP) of the chunk
-  const int b_c8 = WG ? (tid % (BN / 8)) * 8 : (tid % CPR) * 8;
+  constexpr int AROWSTEP = ARC ? THREADS / (BM / 8) : THREADS / CPR;
+  constexpr int BROWSTEP = BRC ? THREADS / (BN / 8) : THREADS / CPR;
+  const int a_r0 = ARC ? tid / (BM / 8) : tid / CPR;
+  const int b_r0 = BRC ? tid / (BN / 8) : tid / CPR;
+  const int a_c8 = ARC ? (tid % (BM / 8)) * 8 : (tid % CPR) * 8;  // column (row-contig) / k offset (k-contig)
+  const int b_c8 = BRC ? (tid % (BN / 8)) * 8 : (tid % CPR) * 8;
   int a_img[WG ? 1 : NCA], a_ih0[WG ? 1 : NCA], a_iw0[WG ? 1 : NCA];  // FPROP A rows
   int wb_rr = 0, wb_ss = 0, wb_c = 0;                                  // WGRAD B column (rsc chunk)
   bool wb_valid = false;
@@ -232,19 +239,41 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
       const bool kv = k < KMAX;
 #pragma unroll
       for (int j = 0; j < NCA; ++j) {
-        const int ih = a_ih0[j] + (int)r, iw = a_iw0[j] + s;
-        const bool va = kv && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        int ih = a_ih0[j] + (int)r, iw = a_iw0[j] + s;
+        bool va = kv && a_img[j] >= 0;
+        if constexpr (DG) {  // dilated input: only taps landing on a stride multiple exist
+          va = va && ((ih | iw) & a.imask) == 0;
+          ih >>= a.ishift;
+          iw >>= a.ishift;
+        }
+        va = va && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const long aoff = (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c;
 #pragma unroll
         for (int p = 0; p < NP; ++p) ra[j][p] = ld16m(a.x + p * a.xps, aoff, va);
       }
+      if constexpr (DG) {  // weight rows (r,s,k) of the flipped filter, c-contiguous
 #pragma unroll
-      for (int j = 0; j < NCB; ++j) {
-        const int n = n0 + b_r0 + j * BROWSTEP;
-        const bool vb = kv && n < a.Nout;
-        const long boff = (long)n * a.Ktot + k;
+        for (int j = 0; j < NCB; ++j) {
+          const int kr = kb + b_r0 + j * BROWSTEP;
+          const int col = n0 + b_c8;
+          const bool vb = kr < KMAX && col < a.Nout;
+          const unsigned tp = fdiv((unsigned)kr, a.fd_C);
+          const int ko = kr - (int)tp * a.C;
+          const unsigned rr = fdiv(tp, a.fd_S);
+          const int ss = (int)(tp - rr * a.S);
+          const long boff = (((long)ko * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + col;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.w + p * a.wps, boff, vb);
+          for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.w + p * a.wps, boff, vb);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NCB; ++j) {
+          const int n = n0 + b_r0 + j * BROWSTEP;
+          const bool vb = kv && n < a.Nout;
+          const long boff = (long)n * a.Ktot + k;
+#pragma unroll
+          for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.w + p * a.wps, boff, vb);
+        }
       }
     } else {
 #pragma unroll
@@ -299,11 +328,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   // Fragment fetch.  k-contiguous image: lane reads 16 B at [row][8*lh].  Row-contiguous image
   // ([m][col]): two ds_read_b64_tr_b16; lane 4q+p of each 16-lane group addresses row q of its
   // 4-row block, columns 4p..4p+3, and receives its own column (kout/rsc = l&31) of the block.
-  auto frag = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
-    if constexpr (!WG) {
-      const uint4 v = *reinterpret_cast<const uint4*>(base + (row0 + li) * pitch + 16 * ks + 8 * lh);
-      return __builtin_bit_cast(bf16x8, v);
-    } else {
+  auto frag_k = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + (row0 + li) * pitch + 16 * ks + 8 * lh);
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto frag_r = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
+    {
       const int g = lane >> 4, idx = lane & 15;
       const int q = idx >> 2, p4 = idx & 3;
       const int col = row0 + 16 * (g & 1) + 4 * p4;
@@ -326,11 +356,21 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int p = 0; p < NP; ++p) fa[i][p] = frag(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks);
+      for (int p = 0; p < NP; ++p) {
+        if constexpr (ARC)
+          fa[i][p] = frag_r(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks);
+        else
+          fa[i][p] = frag_k(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks);
+      }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int p = 0; p < NP; ++p) fb[j][p] = frag(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
+      for (int p = 0; p < NP; ++p) {
+        if constexpr (BRC)
+          fb[j][p] = frag_r(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
+        else
+          fb[j][p] = frag_k(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
+      }
     // smallest products first
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -417,25 +457,6 @@ __global__ __launch_bounds__(256) void splitk_sum_x3(const float* __restrict__ s
 }
 
 // ---------------- fp32 -> bf16 planes ----------------
-__device__ __forceinline__ u16 bf16_rne(float f) {
-  unsigned u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (u16)(u >> 16);
-}
-__device__ __forceinline__ float bf16_f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
-
-template <int NP>
-__device__ __forceinline__ void split_val(float v, u16* o) {
-  const u16 h0 = bf16_rne(v);
-  o[0] = h0;
-  if (NP == 3) {
-    const float r1 = v - bf16_f(h0);
-    const u16 h1 = bf16_rne(r1);
-    o[1] = h1;
-    o[2] = bf16_rne(r1 - bf16_f(h1));
-  }
-}
-
 // x [n] fp32 -> planes [NP][n] (n % 4 == 0)
 template <int NP>
 __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, u16* __restrict__ out, long n4,
@@ -452,35 +473,6 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x,
     for (int p = 0; p < NP; ++p) {
       ushort4 w = make_ushort4(o[0][p], o[1][p], o[2][p], o[3][p]);
       reinterpret_cast<ushort4*>(out + p * ps)[i] = w;
-    }
-  }
-}
-
-// weights KRSC fp32 -> planes of W [K][R][S][C] and of the dgrad weights Wd[c][r][s][k] =
-// W[k][R-1-r][S-1-s][c] (both [NP][...]); one thread per Wd element (k fastest: coalesced writes)
-template <int NP>
-__global__ __launch_bounds__(256) void split_weights_kernel(const float* __restrict__ w, u16* __restrict__ w3,
-                                                            u16* __restrict__ wd3, int K, int R, int S, int C) {
-  const long total = (long)K * R * S * C;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    {  // W planes (same index)
-      u16 o[3];
-      split_val<NP>(w[i], o);
-#pragma unroll
-      for (int p = 0; p < NP; ++p) w3[p * total + i] = o[p];
-    }
-    if (wd3) {
-      const int k = (int)(i % K);
-      long t = i / K;
-      const int s = (int)(t % S);
-      t /= S;
-      const int r = (int)(t % R);
-      const int c = (int)(t / R);
-      u16 o[3];
-      split_val<NP>(w[(((long)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c], o);
-#pragma unroll
-      for (int p = 0; p < NP; ++p) wd3[p * total + i] = o[p];
     }
   }
 }
@@ -580,6 +572,44 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out
   return 0;
 }
 
+// Data gradient of conv(x [N,H,W,C], w [K,R,S,C], stride, pad) -> dZ [N,Hd,Wd,K]:
+// dx [N,H,W,C] fp32 (or slabs) from dz planes [NP][N,Hd,Wd,K] and the forward weight planes.
+// stride must be a power of two.
+int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, float* dx, float* slab, int N, int Hd, int Wd,
+                      int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
+                      int posmajor, int np, hipStream_t st) {
+  Args a{};
+  a.x = dz;
+  a.xps = dzps;
+  a.w = w;
+  a.wps = wps;
+  if (stride < 1 || (stride & (stride - 1)) || R - 1 - pad < 0) return -3;
+  fill(a, N, Hd, Wd, K, R, S, 1, R - 1 - pad);
+  a.P = H;
+  a.Q = W;
+  a.M = N * H * W;
+  a.fd_Q = make_fastdiv(W);
+  a.fd_PQ = make_fastdiv(H * W);
+  a.imask = stride - 1;
+  while ((1 << a.ishift) < stride) ++a.ishift;
+  a.Nout = C;
+  if (C % 8 || K % 8) return -2;
+  a.gm = cdiv(a.M, tile_rows(tile));
+  a.gn = cdiv(C, tile_cols(tile));
+  a.splits = xsplits(a.Ktot, splits);
+  a.posmajor = posmajor ? 1 : 0;
+  a.out = a.splits > 1 ? slab : dx;
+  a.slab = a.splits > 1 ? (long)a.M * C : 0;
+  const int rc = np == 3 ? launch_tile<XM_DGRAD, 3>(a, tile, st) : launch_tile<XM_DGRAD, 1>(a, tile, st);
+  if (rc) return rc;
+  if (a.splits > 1 && reduce) {
+    const long n4 = (long)a.M * C / 4;
+    splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, dx, n4, a.splits);
+    return (int)hipGetLastError();
+  }
+  return 0;
+}
+
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] Xcol[m][rsc]; x planes [NP][N,H,W,C], dz planes [NP][N,P,Q,Kout]
 int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* dw, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int posmajor, int np,
@@ -614,15 +644,6 @@ int dpa_split_planes(const float* x, u16* out, long n, long ps, int np, hipStrea
     split_kernel<3><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
   else
     split_kernel<1><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
-  return (int)hipGetLastError();
-}
-
-int dpa_split_weights(const float* w, u16* w3, u16* wd3, int K, int R, int S, int C, int np, hipStream_t st) {
-  const long total = (long)K * R * S * C;
-  if (np == 3)
-    split_weights_kernel<3><<<grid_1d(total), 256, 0, st>>>(w, w3, wd3, K, R, S, C);
-  else
-    split_weights_kernel<1><<<grid_1d(total), 256, 0, st>>>(w, w3, wd3, K, R, S, C);
   return (int)hipGetLastError();
 }
 

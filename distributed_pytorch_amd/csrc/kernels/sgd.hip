@@ -7,9 +7,14 @@
 //   d = g*scale + wd*p ; buf = first ? d : momentum*buf + d ; p -= lr*buf
 #include "common.h"
 
+// NP > 0: the updated parameters are also written as NP bf16 operand planes (plane stride ps, same
+// element index as the arena): the conv kernels' weight operands are refreshed in the same pass
+// instead of a separate split kernel per layer.
+template <int NP>
 __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                        float* __restrict__ buf, long n4, float lr, float momentum,
-                                                       float wd, float gscale, int first) {
+                                                       float wd, float gscale, int first, u16* __restrict__ planes,
+                                                       long ps) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pv = reinterpret_cast<float4*>(p)[i];
@@ -34,6 +39,16 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, co
     pv.w -= lr * bv.w;
     reinterpret_cast<float4*>(buf)[i] = bv;
     reinterpret_cast<float4*>(p)[i] = pv;
+    if constexpr (NP > 0) {
+      u16 o[4][3];
+      split_val<NP>(pv.x, o[0]);
+      split_val<NP>(pv.y, o[1]);
+      split_val<NP>(pv.z, o[2]);
+      split_val<NP>(pv.w, o[3]);
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        reinterpret_cast<ushort4*>(planes + q * ps)[i] = make_ushort4(o[0][q], o[1][q], o[2][q], o[3][q]);
+    }
   }
 }
 
@@ -63,11 +78,18 @@ static int grid_for(long n, int block) {
   return (int)g;
 }
 
+// planes: NP bf16 planes of the same arena slice (plane stride ps), or nullptr / np = 0
 extern "C" int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd,
-                            float gscale, int first, hipStream_t s) {
+                            float gscale, int first, u16* planes, long ps, int np, hipStream_t s) {
   if (n % 4) return -1;
   const long n4 = n / 4;
-  sgd_flat_kernel<<<grid_for(n4, 256), 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first);
+  const int grid = grid_for(n4, 256);
+  if (planes && np == 3)
+    sgd_flat_kernel<3><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, planes, ps);
+  else if (planes && np == 1)
+    sgd_flat_kernel<1><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, planes, ps);
+  else
+    sgd_flat_kernel<0><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, nullptr, 0);
   return (int)hipGetLastError();
 }
 

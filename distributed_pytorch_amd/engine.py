@@ -146,8 +146,11 @@ class VGGEngine:
         self.z, self.a, self.g, self.dz = [], [], [], []
         self.a3: List[Optional[torch.Tensor]] = []   # planes of a[i] when layer i+1 consumes planes
         self.dz3: List[Optional[torch.Tensor]] = []
+        # bf16 operand planes of the WHOLE parameter arena (same element index as params.flat): the
+        # fused SGD kernel rewrites them with every update; conv layer i reads its slice as w3[i]
+        # (forward and, read transposed in place, data gradient)
+        self.wplanes = torch.zeros(self.np, self.params.flat.numel(), **bf) if any(self.planes) else None
         self.w3: List[Optional[torch.Tensor]] = []
-        self.wd3: List[Optional[torch.Tensor]] = []
         self.stats = []  # per layer dict(mean, invstd, scale, shift)
         self.eval_ss = []
         part_need = 1
@@ -160,8 +163,11 @@ class VGGEngine:
             self.g.append(torch.empty(N, ho, ho, l.cout, **f32))
             self.dz.append(None if self.planes[i] else torch.empty(N, hw, hw, l.cout, **f32))
             self.dz3.append(torch.empty(self.np, N, hw, hw, l.cout, **bf) if self.planes[i] else None)
-            self.w3.append(torch.empty(self.np, l.cout, 3, 3, l.cin_pad, **bf) if self.planes[i] else None)
-            self.wd3.append(torch.empty(self.np, l.cin_pad, 3, 3, l.cout, **bf) if self.planes[i] else None)
+            if self.planes[i]:
+                off, cnt = self.params.offsets[f"{l.conv_key}.weight"], self.params.numels[f"{l.conv_key}.weight"]
+                self.w3.append(self.wplanes[:, off:off + cnt].view(self.np, l.cout, 3, 3, l.cin_pad))
+            else:
+                self.w3.append(None)
             self.stats.append({k: torch.zeros(l.cout, **f32) for k in ("mean", "invstd", "scale", "shift")})
             self.eval_ss.append({k: torch.zeros(l.cout, **f32) for k in ("scale", "shift")})
             M, Mo = N * hw * hw, N * ho * ho
@@ -224,11 +230,11 @@ class VGGEngine:
         self.refresh_weight_planes()
 
     def refresh_weight_planes(self):
-        """Re-split the conv weights into the bf16 operand planes (W for forward, the flipped/
-        transposed Wd for the data gradient) — after every parameter update."""
-        for i, l in enumerate(self.spec.convs):
-            if self.planes[i]:
-                self.K.split_weights(self.params[f"{l.conv_key}.weight"], self.w3[i], self.wd3[i])
+        """Re-split the parameter arena into the bf16 operand planes (one launch).  Needed after
+        parameters change outside ``sgd_step`` (load, broadcast); the SGD kernel refreshes them
+        itself."""
+        if self.wplanes is not None:
+            self.K.split_planes(self.params.flat, self.wplanes)
 
     @torch.no_grad()
     def state_dict(self, prefix: str = "") -> "OrderedDict[str, torch.Tensor]":
@@ -420,7 +426,7 @@ class VGGEngine:
         slab = self.slab if s > 1 else None
         out = self.g[i - 1][:n]
         if self.planes[i]:
-            self.K.conv_x3_fprop(self.dz3[i][:, :n], self.wd3[i], out, slab, 1, 1, s, tile, False, pm)
+            self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm)
         else:
             self.K.conv_fprop(self.dz[i][:n], self.params[f"{l.conv_key}.weight"], out, slab, 1, 1, s, tile, True,
                               False, pm)
@@ -490,12 +496,11 @@ class VGGEngine:
     def sgd_step(self, grad_scale: float = 1.0, offset: int = 0, count: int = -1):
         """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
         self.K.sgd_flat(self.params.flat, self.grads.flat, self.mom.flat, self.lr, self.momentum, self.weight_decay,
-                        grad_scale, self.steps_taken == 0, offset, count)
+                        grad_scale, self.steps_taken == 0, offset, count, self.wplanes)
 
     def finish_step(self):
         self.steps_taken += 1
         self._eval_dirty = True
-        self.refresh_weight_planes()
 
     # ------------------------------------------------------------------ evaluation
     def begin_eval(self):

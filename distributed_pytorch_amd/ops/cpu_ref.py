@@ -25,7 +25,7 @@ def _nhwc(t):
 
 
 # ---------------------------------------------------------------- optimizer / elementwise
-def sgd_flat(p, g, buf, lr, momentum, wd, gscale, first, offset=0, count=-1):
+def sgd_flat(p, g, buf, lr, momentum, wd, gscale, first, offset=0, count=-1, planes=None):
     if count < 0:
         count = p.numel() - offset
     sl = slice(offset, offset + count)
@@ -36,6 +36,18 @@ def sgd_flat(p, g, buf, lr, momentum, wd, gscale, first, offset=0, count=-1):
     else:
         bb.mul_(momentum).add_(d)
     pp.sub_(lr * bb)
+    if planes is not None:
+        planes[:, sl].copy_(split_bf16(pp, planes.shape[0]))
+
+
+def split_bf16(x, np_):
+    """fp32 -> [np_, *x.shape] bf16 planes (round-to-nearest-even), the HIP split's semantics."""
+    out, r = [], x.float()
+    for _ in range(np_):
+        h = r.to(torch.bfloat16)
+        out.append(h)
+        r = r - h.float()
+    return torch.stack(out)
 
 
 def scale_(x, s):

@@ -182,9 +182,21 @@ def test_conv_x3_fprop(shape, splits, tile, posmajor, np_):
     assert rel_err(out.permute(0, 3, 1, 2), ref) < (1e-5 if np_ == 3 else 2e-2)
 
 
-@pytest.mark.parametrize("shape", [s for s in X3_SHAPES if s[6] == 1 and 2 * s[7] == s[5] - 1])
+X3_DGRAD_SHAPES = X3_SHAPES + [
+    (2, 16, 16, 8, 64, 1, 2, 0),     # ResNet downsample 1x1/s2
+    (2, 20, 20, 8, 64, 7, 2, 3),     # ResNet stem 7x7/s2
+    (4, 14, 14, 64, 64, 3, 2, 1),    # ResNet 3x3/s2
+]
+
+
+@pytest.mark.parametrize("shape", X3_DGRAD_SHAPES)
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("tile", [0, 1, 5, 6, 7])
 @pytest.mark.parametrize("posmajor", [False, True])
-def test_conv_x3_dgrad_via_split_weights(shape, posmajor):
+@pytest.mark.parametrize("np_", [3, 1])
+def test_conv_x3_dgrad(shape, splits, tile, posmajor, np_):
+    """Data gradient straight from the forward weight planes (transposed in-LDS reads), including
+    strided convs (input dilation)."""
     C = _C()
     N, H, W, Cin, K, R, st, pd = shape
     g = torch.Generator().manual_seed(13)
@@ -193,16 +205,29 @@ def test_conv_x3_dgrad_via_split_weights(shape, posmajor):
     y = F.conv2d(x, w, stride=st, padding=pd)
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     (gx,) = torch.autograd.grad(y, x, dy)
-    wk = w.float().permute(0, 2, 3, 1).contiguous().cuda()
-    w3 = torch.empty((3,) + tuple(wk.shape), device="cuda", dtype=torch.bfloat16)
-    wd3 = torch.empty(3, Cin, R, R, K, device="cuda", dtype=torch.bfloat16)
-    C.split_weights(wk, w3, wd3)
-    dz3 = _planes(dy.float().permute(0, 2, 3, 1), 3)
+    w3 = _planes(w.float().permute(0, 2, 3, 1), np_)
+    dz3 = _planes(dy.float().permute(0, 2, 3, 1), np_)
     dx = torch.empty(N, H, W, Cin, device="cuda")
-    slab = torch.empty(4 * N * H * W * Cin, device="cuda")
-    C.conv_x3_fprop(dz3, wd3, dx, slab, 1, pd, 4, 0, True, posmajor)
+    slab = torch.empty(splits * N * H * W * Cin, device="cuda") if splits > 1 else None
+    C.conv_x3_dgrad(dz3, w3, dx, slab, st, pd, splits, tile, True, posmajor)
     torch.cuda.synchronize()
-    assert rel_err(dx.permute(0, 3, 1, 2), gx) < 1e-5
+    assert rel_err(dx.permute(0, 3, 1, 2), gx) < (1e-5 if np_ == 3 else 2e-2)
+
+
+def test_conv_x3_planes_as_arena_views():
+    """Weight planes may be strided views of one plane arena (the engine's layout)."""
+    C = _C()
+    g = torch.Generator().manual_seed(15)
+    x = torch.randn(4, 32, 8, 8, generator=g)
+    w = torch.randn(64, 32, 3, 3, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    arena = torch.zeros(3, 1000 + w.numel() + 64, device="cuda", dtype=torch.bfloat16)
+    wv = arena[:, 1024:1024 + w.numel()].view(3, 64, 3, 3, 32)
+    wv.copy_(_planes(w.permute(0, 2, 3, 1), 3))
+    out = torch.empty(4, 8, 8, 64, device="cuda")
+    C.conv_x3_fprop(_planes(x.permute(0, 2, 3, 1), 3), wv, out, None, 1, 1, 1, 0, True, False)
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-5
 
 
 @pytest.mark.parametrize("shape", X3_SHAPES)

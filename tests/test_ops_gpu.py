@@ -170,6 +170,29 @@ def test_fc_ce(B, Cin, J):
     close(ev[0:1], loss.detach().reshape(1), 1e-5)
 
 
+@pytest.mark.parametrize("np_", [1, 3])
+def test_sgd_flat_writes_planes(np_):
+    """The fused update also refreshes the bf16 operand planes of the updated slice (only)."""
+    C_ = _C()
+    n = 8192
+    g = torch.Generator().manual_seed(5)
+    p, gr, m = torch.randn(n, generator=g), torch.randn(n, generator=g), torch.randn(n, generator=g)
+    pr, mr = p.clone(), m.clone()
+    cpu_ref.sgd_flat(pr, gr, mr, 0.1, 0.9, 1e-4, 1.0, False, 1024, 4096)
+    pd, md = p.cuda(), m.cuda()
+    planes = torch.zeros(np_, n, device="cuda", dtype=torch.bfloat16)
+    C_.sgd_flat(pd, gr.cuda(), md, 0.1, 0.9, 1e-4, 1.0, False, 1024, 4096, planes)
+    torch.cuda.synchronize()
+    close(pd, pr, 1e-6)
+    # planes are the exact RNE split of the kernel's own updated parameters
+    assert torch.equal(planes.cpu()[:, 1024:5120], cpu_ref.split_bf16(pd.cpu()[1024:5120], np_))
+    assert planes[:, :1024].abs().sum().item() == 0 and planes[:, 5120:].abs().sum().item() == 0
+    # the planes reconstruct the updated fp32 parameters
+    rec = planes.double().sum(0).cpu()[1024:5120]
+    tol = 2 ** -22 if np_ == 3 else 2 ** -8
+    assert ((rec - pd.double().cpu()[1024:5120]).abs() / pd.double().cpu()[1024:5120].abs()).max() < tol
+
+
 @pytest.mark.parametrize("first", [True, False])
 def test_sgd_flat(first):
     C_ = _C()

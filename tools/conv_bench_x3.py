@@ -41,7 +41,6 @@ def main():
     for (H, Cin, K) in VGG11:
         x3 = torch.randn(NP, N, H, H, Cin, device="cuda").bfloat16()
         w3 = (torch.randn(NP, K, 3, 3, Cin, device="cuda") * 0.05).bfloat16()
-        wd3 = (torch.randn(NP, Cin, 3, 3, K, device="cuda") * 0.05).bfloat16()
         dz3 = torch.randn(NP, N, H, H, K, device="cuda").bfloat16()
         z = torch.empty(N, H, H, K, device="cuda")
         dx = torch.empty(N, H, H, Cin, device="cuda")
@@ -52,14 +51,14 @@ def main():
         best = {}
         for kind in ("fprop", "dgrad", "wgrad"):
             res = []
-            for tile, pm in [(t, p) for t in (0, 1, 2, 3, 4, 5, 6) for p in (False, True)]:
+            for tile, pm in [(t, p) for t in (0, 1, 2, 3, 4, 5, 6, 7) for p in (False, True)]:
                 for splits in (1, 2, 4, 8, 16, 32, 64, 128):
                     if kind != "wgrad" and splits > 16:
                         continue
                     if kind == "fprop":
                         fn = lambda: C.conv_x3_fprop(x3, w3, z, slab, 1, 1, splits, tile, False, pm)
                     elif kind == "dgrad":
-                        fn = lambda: C.conv_x3_fprop(dz3, wd3, dx, slab, 1, 1, splits, tile, False, pm)
+                        fn = lambda: C.conv_x3_dgrad(dz3, w3, dx, slab, 1, 1, splits, tile, False, pm)
                     else:
                         fn = lambda: C.conv_x3_wgrad(x3, dz3, dw, slab, 1, 1, splits, tile, pm)
                     res.append((timeit(fn, a.iters), tile, splits, pm))
