@@ -43,6 +43,7 @@ int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* d
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
                       int posmajor, int np, hipStream_t st);
 int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
+int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, float* dx, float* slab,
                       int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
                       int tile, int reduce, int posmajor, int np, hipStream_t st);
@@ -273,6 +274,16 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
   chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), fp(dx), sl, N, Hd, Wd, K, C, R, S, (int)stride,
                         (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, cur_stream()),
       "conv_x3_dgrad");
+}
+
+// x fp32 [..., cin] (cin <= 8) -> out [NP, ..., 8] bf16 planes, channels >= cin zero
+void pad_split8(Tensor x, Tensor out) {
+  need(x, "x");
+  need_planes(out, "out");
+  TORCH_CHECK(out.size(-1) == 8 && x.size(-1) <= 8, "pad_split8: out [NP, ..., 8]");
+  const long npix = x.numel() / x.size(-1);
+  TORCH_CHECK(out.numel() == out.size(0) * npix * 8, "pad_split8: pixel count mismatch");
+  chk(dpa_pad_split8(fp(x), up(out), npix, x.size(-1), out.stride(0), out.size(0), cur_stream()), "pad_split8");
 }
 
 // x fp32 (any shape) -> out [NP, *x.shape] bf16 planes
@@ -532,6 +543,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
         py::arg("posmajor") = false);
   m.def("split_planes", &split_planes);
+  m.def("pad_split8", &pad_split8);
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);

@@ -59,3 +59,55 @@ __device__ __forceinline__ void split_val(float v, u16* o) {
     o[2] = bf16_rne(r1 - bf16_f(h1));
   }
 }
+
+// ---- deterministic split-K reduction: out[i] = sum_k slabs[k * n4 + i] over float4 elements ----
+// Block = 64 float4 columns x G split lanes: lane g sums splits g, g+G, ... and the G partials are
+// combined in LDS in a fixed order.  G > 1 gives small outputs with many splits (e.g. first-layer
+// weight gradients: 1152 float4 x 512 splits) enough parallel loads to stream at HBM rate.
+template <int G>
+__global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __restrict__ slabs,
+                                                               float4* __restrict__ out, long n4, int splits) {
+  __shared__ float4 part[G > 1 ? G : 1][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+#pragma unroll 4
+    for (int k = g; k < splits; k += G) {
+      const float4 v = slabs[(long)k * n4 + i];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  }
+  if constexpr (G == 1) {
+    if (i < n4) out[i] = s;
+  } else {
+    part[g][c] = s;
+    __syncthreads();
+    if (g == 0 && i < n4) {
+#pragma unroll
+      for (int j = 1; j < G; ++j) {
+        s.x += part[j][c].x;
+        s.y += part[j][c].y;
+        s.z += part[j][c].z;
+        s.w += part[j][c].w;
+      }
+      out[i] = s;
+    }
+  }
+}
+
+inline int launch_splitk_reduce(const float* slabs, float* out, long n4, int splits, hipStream_t st) {
+  const long blocks = (n4 + 63) / 64;
+  const float4* in4 = reinterpret_cast<const float4*>(slabs);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  if (splits >= 16 && blocks < 4096)
+    splitk_reduce_kernel<16><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits);
+  else if (splits >= 4 && blocks < 16384)
+    splitk_reduce_kernel<4><<<blocks, 256, 0, st>>>(in4, o4, n4, splits);
+  else
+    splitk_reduce_kernel<1><<<blocks, 64, 0, st>>>(in4, o4, n4, splits);
+  return (int)hipGetLastError();
+}

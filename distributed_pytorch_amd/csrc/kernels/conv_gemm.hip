@@ -434,21 +434,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
 }
 
 // Sum split-K slabs: out[i] = sum_s slab[s*n + i]  (float4 vectorised; n % 4 == 0)
-__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ slabs, float* __restrict__ out,
-                                                         long n4, int splits) {
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 s = reinterpret_cast<const float4*>(slabs)[i];
-    for (int k = 1; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(slabs)[(long)k * n4 + i];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
-    reinterpret_cast<float4*>(out)[i] = s;
-  }
-}
 
 // Dgrad weight transform for stride-1 "same" convs: Wd[c][r][s][k] = W[k][R-1-r][S-1-s][c].
 __global__ __launch_bounds__(256) void wflip_kernel(const float* __restrict__ w, float* __restrict__ wd, int K,
@@ -544,8 +529,7 @@ int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int 
   if (rc) return rc;
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * Kout / 4;
-    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, a.splits);
-    rc = (int)hipGetLastError();
+    rc = launch_splitk_reduce(slab, out, n4, a.splits, st);
   }
   return rc;
 }
@@ -570,8 +554,7 @@ int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int 
   if (rc) return rc;
   if (a.splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;
-    splitk_sum_kernel<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, a.splits);
-    rc = (int)hipGetLastError();
+    rc = launch_splitk_reduce(slab, dw, n4, a.splits, st);
   }
   return rc;
 }

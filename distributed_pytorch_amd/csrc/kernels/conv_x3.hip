@@ -440,21 +440,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     }
 }
 
-__global__ __launch_bounds__(256) void splitk_sum_x3(const float* __restrict__ slabs, float* __restrict__ out, long n4,
-                                                     int splits) {
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 s = reinterpret_cast<const float4*>(slabs)[i];
-    for (int k = 1; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(slabs)[(long)k * n4 + i];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
-    reinterpret_cast<float4*>(out)[i] = s;
-  }
-}
 
 // ---------------- fp32 -> bf16 planes ----------------
 // x [n] fp32 -> planes [NP][n] (n % 4 == 0)
@@ -473,6 +458,28 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x,
     for (int p = 0; p < NP; ++p) {
       ushort4 w = make_ushort4(o[0][p], o[1][p], o[2][p], o[3][p]);
       reinterpret_cast<ushort4*>(out + p * ps)[i] = w;
+    }
+  }
+}
+
+// x fp32 [npix][cin] -> planes [NP][npix][cout] (channels >= cin zero): the network input, padded
+// to the 8-channel operand granularity, one 16-byte chunk per pixel per plane.
+template <int NP>
+__global__ __launch_bounds__(256) void pad_split_kernel(const float* __restrict__ x, u16* __restrict__ out, long npix,
+                                                        int cin, long ps) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < npix; i += stride) {
+    u16 o[8][3];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) split_val<NP>(c < cin ? x[i * cin + c] : 0.f, o[c]);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      uint4 v;
+      v.x = o[0][p] | ((unsigned)o[1][p] << 16);
+      v.y = o[2][p] | ((unsigned)o[3][p] << 16);
+      v.z = o[4][p] | ((unsigned)o[5][p] << 16);
+      v.w = o[6][p] | ((unsigned)o[7][p] << 16);
+      reinterpret_cast<uint4*>(out + p * ps)[i] = v;
     }
   }
 }
@@ -566,8 +573,7 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out
   if (rc) return rc;
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * Kout / 4;
-    splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, out, n4, a.splits);
-    return (int)hipGetLastError();
+    return launch_splitk_reduce(slab, out, n4, a.splits, st);
   }
   return 0;
 }
@@ -604,8 +610,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, float* d
   if (rc) return rc;
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * C / 4;
-    splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, dx, n4, a.splits);
-    return (int)hipGetLastError();
+    return launch_splitk_reduce(slab, dx, n4, a.splits, st);
   }
   return 0;
 }
@@ -632,8 +637,7 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   if (rc) return rc;
   if (a.splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;
-    splitk_sum_x3<<<grid_1d(n4), 256, 0, st>>>(slab, dw, n4, a.splits);
-    return (int)hipGetLastError();
+    return launch_splitk_reduce(slab, dw, n4, a.splits, st);
   }
   return 0;
 }
@@ -644,6 +648,15 @@ int dpa_split_planes(const float* x, u16* out, long n, long ps, int np, hipStrea
     split_kernel<3><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
   else
     split_kernel<1><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
+  return (int)hipGetLastError();
+}
+
+int dpa_pad_split8(const float* x, u16* out, long npix, int cin, long ps, int np, hipStream_t st) {
+  if (cin > 8) return -2;
+  if (np == 3)
+    pad_split_kernel<3><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps);
+  else
+    pad_split_kernel<1><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps);
   return (int)hipGetLastError();
 }
 

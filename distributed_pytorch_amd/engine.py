@@ -105,7 +105,6 @@ class VGGEngine:
                  lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4, bn_momentum: float = 0.1,
                  bn_eps: float = 1e-5, in_hw: int = 32, backend=None, impl: str = "fp32"):
         self.device = torch.device(device)
-        self.spec = VGGSpec.from_name(name, num_classes, in_hw)
         self.K = backend if backend is not None else (_ext.require() if self.device.type == "cuda" else cpu_ref)
         if impl not in IMPLS:
             raise ValueError(f"impl must be one of {IMPLS}")
@@ -113,6 +112,8 @@ class VGGEngine:
             impl = "fp32"  # the CPU oracle backend implements the fp32 kernel API only
         self.impl = impl
         self.np = {"fp32": 0, "x3": 3, "bf16": 1}[impl]
+        # plane kernels take the 3-channel input padded to 8 (one 16-B chunk per pixel)
+        self.spec = VGGSpec.from_name(name, num_classes, in_hw, in_pad=8 if self.np else 4)
         self.max_batch = max_batch
         self._cfg_cache: Dict[tuple, tuple] = {}
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
@@ -139,6 +140,9 @@ class VGGEngine:
         N = max_batch
         f32 = dict(device=dev, dtype=torch.float32)
         self.x0 = torch.zeros(N, in_hw, in_hw, 4, **f32)
+        # bf16 planes of the (padded) network input when layer 0 runs the plane kernels
+        self.x0p = (torch.zeros(self.np, N, in_hw, in_hw, L[0].cin_pad, dtype=torch.bfloat16, device=dev)
+                    if self.np and L[0].cin_pad % 8 == 0 else None)
         self.target = torch.zeros(N, dtype=torch.int64, device=dev)
         bf = dict(device=dev, dtype=torch.bfloat16)
         # planes(i): layer i runs the bf16-plane kernels (needs cin % 8 == 0)
@@ -353,7 +357,7 @@ class VGGEngine:
     def conv_candidates(self, i: int, kind: str):
         impl = self._layer_impl(i)
         tiles = (0, 1) if impl == "fp32" else (0, 1, 2, 3, 4, 5, 6, 7)
-        splits = (1, 2, 4, 8, 16, 32, 64, 128) if kind == "wgrad" else (1, 2, 4, 8, 16)
+        splits = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if kind == "wgrad" else (1, 2, 4, 8, 16)
         return [(t, s, pm) for t in tiles for s in splits for pm in (False, True)]
 
     def autotune(self, n: Optional[int] = None, iters: int = 3, verbose: bool = False) -> Dict[str, list]:
@@ -377,6 +381,8 @@ class VGGEngine:
                     red = M if kind == "wgrad" else (9 * (l.cin_pad if kind == "fprop" else l.cout))
                     s = (self.K.conv_splits(red, s) if impl == "fp32" else self.K.x3_splits(red, s))
                     self._cfg_cache[key] = (tile, s, pm)
+                    if self._slab_need(i, kind, n) * 4 > (256 << 20):
+                        continue  # split-K workspace beyond 256 MiB: not a sensible plan
                     fn = {"fprop": lambda: self._conv_fwd(i, self.x0[:n], n, reduce=False),
                           "dgrad": lambda: self._conv_dgrad(i, n),
                           "wgrad": lambda: self._conv_wgrad(i, self.x0[:n], n)}[kind]
@@ -401,7 +407,7 @@ class VGGEngine:
             self.slab = torch.empty(numel, device=self.device, dtype=torch.float32)
 
     def _in_planes(self, i: int, n: int) -> torch.Tensor:
-        return self.a3[i - 1][:, :n]
+        return self.x0p[:, :n] if i == 0 else self.a3[i - 1][:, :n]
 
     def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool) -> int:
         """Forward conv of layer i into z[i] (or split-K slabs); returns the split count left
@@ -460,6 +466,8 @@ class VGGEngine:
         L = self.spec.convs
         if pre_forward is not None:
             pre_forward()
+        if self.x0p is not None:
+            K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(L):
             z, st = self.z[i][:n], self.stats[i]
             ns = self._conv_fwd(i, x, n, reduce=False)
@@ -519,6 +527,8 @@ class VGGEngine:
             raise RuntimeError("call begin_eval() after the last parameter update")
         n = x.shape[0]
         P = self.params
+        if self.x0p is not None:
+            self.K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(self.spec.convs):
             self._conv_fwd(i, x, n, reduce=True)
             self.K.bn_apply(self.z[i][:n], self._act_out(i, n), self.eval_ss[i]["scale"], self.eval_ss[i]["shift"],

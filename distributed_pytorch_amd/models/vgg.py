@@ -74,7 +74,7 @@ def VGG19(num_classes: int = 10) -> VGG:
 class ConvLayer:
     idx: int          # position in the reference Sequential (conv module index)
     cin: int          # true input channels (3 for the first layer)
-    cin_pad: int      # channels as stored by the engine (first layer padded to 4)
+    cin_pad: int      # channels as stored by the engine (first layer padded to 4 or 8)
     cout: int
     hw: int           # input (= conv output) spatial size
     pool: bool        # followed by MaxPool2d(2,2)
@@ -91,7 +91,9 @@ class VGGSpec:
     in_hw: int = 32
 
     @classmethod
-    def from_name(cls, name: str = "VGG11", num_classes: int = 10, in_hw: int = 32) -> "VGGSpec":
+    def from_name(cls, name: str = "VGG11", num_classes: int = 10, in_hw: int = 32, in_pad: int = 4) -> "VGGSpec":
+        """in_pad: channels the 3-channel input is zero-padded to (4 for the fp32 kernels, 8 for
+        the bf16-plane kernels, whose 16-byte operand chunks are 8 channels)."""
         cfg = CFG[name]
         spec = cls(name=name, num_classes=num_classes, in_hw=in_hw)
         c, hw, mi = 3, in_hw, 0
@@ -101,7 +103,7 @@ class VGGSpec:
                 hw //= 2
                 mi += 1
                 continue
-            layer = ConvLayer(idx=mi, cin=c, cin_pad=4 if c == 3 else c, cout=v, hw=hw, pool=False,
+            layer = ConvLayer(idx=mi, cin=c, cin_pad=in_pad if c == 3 else c, cout=v, hw=hw, pool=False,
                               conv_key=f"layers.{mi}", bn_key=f"layers.{mi + 1}")
             spec.convs.append(layer)
             mi += 3

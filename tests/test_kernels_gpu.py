@@ -276,3 +276,17 @@ def test_x3_accuracy_matches_fp32_mfma():
     e1 = (o1.double().cpu() - r).abs().max().item()
     assert e3 <= 2.0 * e32 + 1e-12, (e3, e32)
     assert e1 > 20 * e3  # and the plain bf16 path really is lower precision
+
+
+@pytest.mark.parametrize("np_", [1, 3])
+def test_pad_split8(np_):
+    C = _C()
+    g = torch.Generator().manual_seed(16)
+    x = torch.randn(3, 5, 7, 4, generator=g)
+    x[..., 3] = 0
+    out = torch.full((np_, 3, 5, 7, 8), 7.0, device="cuda", dtype=torch.bfloat16)
+    C.pad_split8(x.cuda(), out)
+    torch.cuda.synchronize()
+    ref = torch.zeros(3, 5, 7, 8)
+    ref[..., :4] = x
+    assert torch.equal(out.cpu(), _planes(ref, np_).cpu())
