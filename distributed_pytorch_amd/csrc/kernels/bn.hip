@@ -16,12 +16,19 @@
 //           reduce pass (sum dy, sum dy*xhat, sum xhat; optionally summing split-K dgrad slabs
 //           of g and writing g) -> finalize -> apply pass writing dz.
 //
-// Reductions: a 256-thread block covers RPB rows x all channels (threads per row = C/4 float4
-// lanes, 256/(C/4) rows in flight), keeps per-thread partials in registers, combines them through
-// LDS, and writes ONE partial per (block, channel) — deterministic, no atomics.
+// Reductions: a RT-thread (1024) block covers RPB rows x all channels (threads per row = C/4
+// float4 lanes, RT/(C/4) rows in flight, 4 rows' loads issued together), keeps per-thread partials
+// in registers, combines them with an LDS tree, and writes ONE partial per (block, channel) —
+// deterministic, no atomics.  ~256 blocks: one wave of full CUs, few partials to merge.
 #include "common.h"
 
 namespace {
+
+constexpr int RT = 1024;  // reduction block size
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 
 struct RedGeom {
   int C4, TPR, RPI, CG;  // float4 lanes per row, threads per row, rows per iteration, channel groups/thread
@@ -30,25 +37,37 @@ struct RedGeom {
 __host__ __device__ inline RedGeom red_geom(int C) {
   RedGeom g;
   g.C4 = C >> 2;
-  g.TPR = g.C4 < 256 ? g.C4 : 256;
-  g.RPI = 256 / g.TPR;
+  g.TPR = g.C4 < RT ? g.C4 : RT;
+  g.RPI = RT / g.TPR;
   g.CG = (g.C4 + g.TPR - 1) / g.TPR;
   return g;
 }
 
-// rows per block so that the grid has ~1024 blocks (at least one full iteration per block)
+// rows per block so that the grid has ~256 blocks (at least one full iteration per block)
 __host__ inline int red_rows_per_block(int M, int C) {
   const RedGeom g = red_geom(C);
-  int rpb = (M + 1023) / 1024;
+  int rpb = (M + 255) / 256;
   rpb = ((rpb + g.RPI - 1) / g.RPI) * g.RPI;
   return rpb < g.RPI ? g.RPI : rpb;
 }
 
+// In-block tree over the RPI row lanes of each channel lane (fixed order): on return sh[t] for
+// lane_r == 0 holds the block sum.  Caller has stored sh[t] and synchronised.
+template <int NARR>
+__device__ __forceinline__ void tree_rows(float4 (*sh)[RT], int t, int lane_r, int TPR, int RPI) {
+  int p2 = 1;
+  while (p2 < RPI) p2 <<= 1;
+  for (int o = p2 >> 1; o >= 1; o >>= 1) {
+    if (lane_r < o && lane_r + o < RPI) {
+#pragma unroll
+      for (int q = 0; q < NARR; ++q) sh[q][t] = f4add(sh[q][t], sh[q][t + o * TPR]);
+    }
+    __syncthreads();
+  }
+}
+
 #define F4GET(v, k) ((k) == 0 ? (v).x : (k) == 1 ? (v).y : (k) == 2 ? (v).z : (v).w)
 
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
 
 // ---- output writer: NP == 0 -> fp32 float4 store; NP in {1,3} -> bf16 planes x = x0 (+ x1 + x2)
 // (round-to-nearest-even splits, conv_x3.hip header) so the next conv reads MFMA-ready operands.
@@ -79,9 +98,8 @@ __device__ __forceinline__ void store4(float* f, u16* pl, long ps, long i4, floa
 // ---- forward statistics: per (row-block, channel) (mean, M2) via sums shifted by the block's
 // first row.  If nsplit > 1, src holds nsplit slabs of [M][C] that are summed here and written
 // to z (the split-K reduction of the producing conv, fused).
-__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ src, float* __restrict__ z,
-                                                       int nsplit, float2* __restrict__ part, int M, int C,
-                                                       int rpb) {
+__global__ __launch_bounds__(RT) void bn_stats_kernel(const float* __restrict__ src, float* __restrict__ z,
+                                                      int nsplit, float2* __restrict__ part, int M, int C, int rpb) {
   const RedGeom g = red_geom(C);
   const int t = threadIdx.x;
   const int lane_c = t % g.TPR, lane_r = t / g.TPR;
@@ -90,7 +108,18 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
   const int r1 = min(M, r0 + rpb);
   const long slab4 = (long)M * g.C4;
   const float4* s4 = reinterpret_cast<const float4*>(src);
-  __shared__ float4 sh1[256], sh2[256];
+  __shared__ float4 sh[2][RT];
+  auto acc = [](float4 v, float4 K, float4& a1, float4& a2) {
+    const float d0 = v.x - K.x, d1 = v.y - K.y, d2 = v.z - K.z, d3 = v.w - K.w;
+    a1.x += d0;
+    a1.y += d1;
+    a1.z += d2;
+    a1.w += d3;
+    a2.x = fmaf(d0, d0, a2.x);
+    a2.y = fmaf(d1, d1, a2.y);
+    a2.z = fmaf(d2, d2, a2.z);
+    a2.w = fmaf(d3, d3, a2.w);
+  };
   for (int cg = 0; cg < g.CG; ++cg) {
     const int c4 = lane_c + cg * g.TPR;
     const bool cval = active && c4 < g.C4;
@@ -99,30 +128,31 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
       // shift = the block's first row (summed over splits)
       K = s4[(long)r0 * g.C4 + c4];
       for (int s = 1; s < nsplit; ++s) K = f4add(K, s4[s * slab4 + (long)r0 * g.C4 + c4]);
-      for (int r = r0 + lane_r; r < r1; r += g.RPI) {
+      int r = r0 + lane_r;
+      if (nsplit == 1) {  // 4 rows' loads in flight
+        for (; r + 3 * g.RPI < r1; r += 4 * g.RPI) {
+          float4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = s4[(long)(r + u * g.RPI) * g.C4 + c4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc(v[u], K, a1, a2);
+        }
+      }
+      for (; r < r1; r += g.RPI) {
         const long i = (long)r * g.C4 + c4;
         float4 v = s4[i];
         for (int s = 1; s < nsplit; ++s) v = f4add(v, s4[s * slab4 + i]);
         if (nsplit > 1) reinterpret_cast<float4*>(z)[i] = v;
-        const float d0 = v.x - K.x, d1 = v.y - K.y, d2 = v.z - K.z, d3 = v.w - K.w;
-        a1.x += d0;
-        a1.y += d1;
-        a1.z += d2;
-        a1.w += d3;
-        a2.x = fmaf(d0, d0, a2.x);
-        a2.y = fmaf(d1, d1, a2.y);
-        a2.z = fmaf(d2, d2, a2.z);
-        a2.w = fmaf(d3, d3, a2.w);
+        acc(v, K, a1, a2);
       }
     }
-    sh1[t] = a1;
-    sh2[t] = a2;
+    sh[0][t] = a1;
+    sh[1][t] = a2;
     __syncthreads();
+    tree_rows<2>(sh, t, lane_r, g.TPR, g.RPI);
     if (cval && lane_r == 0) {
-      for (int k = 1; k < g.RPI; ++k) {
-        a1 = f4add(a1, sh1[t + k * g.TPR]);
-        a2 = f4add(a2, sh2[t + k * g.TPR]);
-      }
+      a1 = sh[0][t];
+      a2 = sh[1][t];
       const float n = (float)(r1 - r0), inv = 1.f / n;
       float2* o = part + (long)blockIdx.x * C + c4 * 4;
       o[0] = make_float2(K.x + a1.x * inv, fmaxf(a2.x - a1.x * a1.x * inv, 0.f));
@@ -281,7 +311,7 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
 // the summed g is written to gout (consumed by the apply pass).  part layout: [block][3][C]
 template <bool POOL>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ gsrc, float* __restrict__ gout,
+__global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restrict__ gsrc, float* __restrict__ gout,
                                                             int nsplit, const float* __restrict__ z,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
@@ -300,7 +330,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   const long slab4 = (long)Mo * gg.C4;
   const float4* z4 = reinterpret_cast<const float4*>(z);
   const float4* g4 = reinterpret_cast<const float4*>(gsrc);
-  __shared__ float4 shA[256], shB[256], shX[256];
+  __shared__ float4 sh[3][RT];
   for (int cg = 0; cg < gg.CG; ++cg) {
     const int c4 = lane_c + cg * gg.TPR;
     const bool cval = active && c4 < gg.C4;
@@ -349,17 +379,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
         }
       }
     }
-    shA[t] = make_float4(sdy[0], sdy[1], sdy[2], sdy[3]);
-    shB[t] = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
-    shX[t] = make_float4(sx[0], sx[1], sx[2], sx[3]);
+    sh[0][t] = make_float4(sdy[0], sdy[1], sdy[2], sdy[3]);
+    sh[1][t] = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
+    sh[2][t] = make_float4(sx[0], sx[1], sx[2], sx[3]);
     __syncthreads();
+    tree_rows<3>(sh, t, lane_r, gg.TPR, gg.RPI);
     if (cval && lane_r == 0) {
-      float4 a = shA[t], b = shB[t], x = shX[t];
-      for (int k = 1; k < gg.RPI; ++k) {
-        a = f4add(a, shA[t + k * gg.TPR]);
-        b = f4add(b, shB[t + k * gg.TPR]);
-        x = f4add(x, shX[t + k * gg.TPR]);
-      }
+      const float4 a = sh[0][t], b = sh[1][t], x = sh[2][t];
       float* o = part + (long)blockIdx.x * 3 * C + c4 * 4;
       *reinterpret_cast<float4*>(o) = a;
       *reinterpret_cast<float4*>(o + C) = b;
@@ -514,7 +540,7 @@ int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M,
   if (C % 4) return -2;
   const int rpb = red_rows_per_block(M, C);
   const int nblk = (M + rpb - 1) / rpb;
-  bn_stats_kernel<<<nblk, 256, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C, rpb);
+  bn_stats_kernel<<<nblk, RT, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C, rpb);
   bn_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
                                                   bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
   return (int)hipGetLastError();
@@ -562,10 +588,10 @@ int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const fl
   const int rpb = red_rows_per_block(Mo, C);
   const int nblk = (Mo + rpb - 1) / rpb;
   if (pool)
-    bn_bwd_reduce_kernel<true><<<nblk, 256, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W, C,
+    bn_bwd_reduce_kernel<true><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W, C,
                                                      rpb);
   else
-    bn_bwd_reduce_kernel<false><<<nblk, 256, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W,
+    bn_bwd_reduce_kernel<false><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W,
                                                       C, rpb);
   bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
                                                       dbeta, dbias, coef);

@@ -11,6 +11,11 @@
 namespace {
 constexpr int MAXJ = 16;
 
+constexpr int MAXCL = 16;  // Cin / 64 values per lane kept in registers (Cin <= 1024)
+
+// W [J][Cin] is staged once per block into LDS (one round of independent 16-B loads), the row
+// (Cin/64 values per lane) is held in registers, and the J wave reductions are interleaved: the
+// kernel pays ~two global-memory latencies instead of a chain of dependent L2 round trips.
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias,
@@ -18,21 +23,39 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
                                                          float* __restrict__ loss_row, float* __restrict__ dlogits,
                                                          float* __restrict__ dx, int* __restrict__ correct_row,
                                                          float* __restrict__ logits_out, int B, int Cin, int J) {
+  extern __shared__ float w_s[];  // [J][Cin]
+  for (int i = threadIdx.x * 4; i < J * Cin; i += blockDim.x * 4)
+    *reinterpret_cast<float4*>(w_s + i) = *reinterpret_cast<const float4*>(w + i);
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
   const float* xr = x + (long)row * Cin;
+  float xv[MAXCL];
+#pragma unroll
+  for (int k = 0; k < MAXCL; ++k) {
+    const int c = lane + 64 * k;
+    xv[k] = c < Cin ? xr[c] : 0.f;
+  }
   float logit[MAXJ];
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
+    float s = 0.f;
     if (j < J) {
-      float s = 0.f;
-      for (int c = lane; c < Cin; c += 64) s += xr[c] * w[(long)j * Cin + c];
-      logit[j] = wave_sum(s) + bias[j];
-    } else {
-      logit[j] = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < MAXCL; ++k) {
+        const int c = lane + 64 * k;
+        if (c < Cin) s = fmaf(xv[k], w_s[j * Cin + c], s);
+      }
     }
+    logit[j] = s;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) logit[j] += __shfl_xor(logit[j], o, 64);
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) logit[j] = j < J ? logit[j] + bias[j] : -INFINITY;
   float mx = logit[0];
   int arg = 0;
 #pragma unroll
@@ -70,51 +93,67 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
       for (int j = 0; j < MAXJ; ++j)
         if (j == lane) dlogits[(long)row * J + j] = dl[j];
     }
-    for (int c = lane; c < Cin; c += 64) {
-      float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < MAXJ; ++j)
-        if (j < J) s += dl[j] * w[(long)j * Cin + c];
-      dx[(long)row * Cin + c] = s;
+    for (int k = 0; k < MAXCL; ++k) {
+      const int c = lane + 64 * k;
+      if (c < Cin) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j)
+          if (j < J) s = fmaf(dl[j], w_s[j * Cin + c], s);
+        dx[(long)row * Cin + c] = s;
+      }
     }
   }
 }
 
-// grid: cdiv(Cin,16) + 1 blocks of 256 threads = 16 columns x 16 row-groups.  Each thread sums
-// its rows (independent loads in flight), the row-groups are combined through LDS in a fixed order
-// (deterministic).  The last block reduces db and the batch-mean loss.
+// grid: cdiv(Cin,8) + 1 blocks of 256 threads = 8 columns x 32 row-groups.  dlogits [B][J] is
+// staged in LDS; each thread issues its rows' x loads together, the row-groups are combined
+// through LDS in a fixed order (deterministic).  The last block reduces db and the batch-mean loss.
 __global__ __launch_bounds__(256) void fc_ce_wgrad_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ dlogits,
                                                           const float* __restrict__ loss_row, float* __restrict__ dw,
                                                           float* __restrict__ db, float* __restrict__ loss_out,
                                                           float* __restrict__ loss_accum, int B, int Cin, int J) {
-  const int ncb = (Cin + 15) / 16;
+  const int ncb = (Cin + 7) / 8;
   const int t = threadIdx.x;
   if ((int)blockIdx.x < ncb) {
-    __shared__ float red[16][16][MAXJ + 1];
-    const int cl = t & 15, rg = t >> 4;
-    const int c = blockIdx.x * 16 + cl;
+    extern __shared__ float dl_s[];  // [B][J]
+    __shared__ float red[32][8][MAXJ + 1];
+    for (int i = t; i < B * J; i += 256) dl_s[i] = dlogits[i];
+    __syncthreads();
+    const int cl = t & 7, rg = t >> 3;
+    const int c = blockIdx.x * 8 + cl;
     float acc[MAXJ];
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) acc[j] = 0.f;
     if (c < Cin) {
-#pragma unroll 4
-      for (int b = rg; b < B; b += 16) {
+      int b = rg;
+      for (; b + 96 < B; b += 128) {
+        float xv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xv[u] = x[(long)(b + 32 * u) * Cin + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < MAXJ; ++j)
+            if (j < J) acc[j] = fmaf(dl_s[(b + 32 * u) * J + j], xv[u], acc[j]);
+      }
+      for (; b < B; b += 32) {
         const float xv = x[(long)b * Cin + c];
-        const float* dl = dlogits + (long)b * J;
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j)
-          if (j < J) acc[j] = fmaf(dl[j], xv, acc[j]);
+          if (j < J) acc[j] = fmaf(dl_s[b * J + j], xv, acc[j]);
       }
     }
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) red[rg][cl][j] = acc[j];
     __syncthreads();
-    if (t < 16 * J) {
-      const int j = t / 16, cc = t % 16;
+    if (t < 8 * J) {
+      const int j = t / 8, cc = t % 8;
       float s = 0.f;
-      for (int k = 0; k < 16; ++k) s += red[k][cc][j];
-      const int col = blockIdx.x * 16 + cc;
+      for (int k = 0; k < 32; ++k) s += red[k][cc][j];
+      const int col = blockIdx.x * 8 + cc;
       if (col < Cin) dw[(long)j * Cin + col] = s;
     }
   } else {
@@ -182,17 +221,18 @@ extern "C" {
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st) {
-  if (J > MAXJ) return -2;
-  fc_ce_rows_kernel<true><<<cdiv(B, 4), 256, 0, st>>>(x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin,
-                                                      J);
-  fc_ce_wgrad_kernel<<<cdiv(Cin, 16) + 1, 256, 0, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B, Cin, J);
+  if (J > MAXJ || Cin > 64 * MAXCL || Cin % 4 || (long)B * J * 4 > 48 * 1024) return -2;
+  fc_ce_rows_kernel<true><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits, dx, nullptr,
+                                                                nullptr, B, Cin, J);
+  fc_ce_wgrad_kernel<<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B,
+                                                               Cin, J);
   return (int)hipGetLastError();
 }
 
 int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                    int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st) {
-  if (J > MAXJ) return -2;
-  fc_ce_rows_kernel<false><<<cdiv(B, 4), 256, 0, st>>>(x, w, b, target, loss_row, nullptr, nullptr, correct_row, logits,
+  if (J > MAXJ || Cin > 64 * MAXCL || Cin % 4) return -2;
+  fc_ce_rows_kernel<false><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, nullptr, nullptr, correct_row, logits,
                                                        B, Cin, J);
   if (acc) eval_accum_kernel<<<1, 256, 0, st>>>(loss_row, correct_row, acc, B);
   return (int)hipGetLastError();

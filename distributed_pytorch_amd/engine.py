@@ -183,7 +183,8 @@ class VGGEngine:
                 if kind == "dgrad" and i == 0:
                     continue
                 self._ensure_slab(self._slab_need(i, kind, N))
-        self.part = torch.empty(part_need, **f32)
+        # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
+        self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
         self.loss_row = torch.zeros(N, **f32)
         self.dlogits = torch.zeros(N, num_classes, **f32)

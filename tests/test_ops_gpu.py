@@ -47,7 +47,7 @@ def test_bn_forward(shape):
     sl = torch.randn(3, *z.shape, generator=g)
     sl[2] = z - sl[0] - sl[1]
     zd = torch.empty(z.shape, device="cuda")
-    part = torch.empty(C_.bn_part_floats(N * H * W, C, False), device="cuda")
+    part = torch.zeros(C_.bn_part_floats(N * H * W, C, False), device="cuda")
     outs = [torch.zeros(C, device="cuda") for _ in range(4)]
     rm_d, rv_d, nbt_d = d(rm), d(rv), torch.zeros(1, dtype=torch.int64, device="cuda")
     C_.bn_fwd_stats(d(sl.reshape(-1)), 3, zd, part, d(gamma), d(beta), d(bias), rm_d, rv_d, nbt_d, *outs, 0.1, 1e-5)
@@ -79,7 +79,7 @@ def test_bn_backward(shape):
     cpu_ref.bn_bwd(gout, 1, gout, z, scale, shift, mean, invstd, gamma, None, None, ref[0], ref[1], ref[2], dz_ref,
                    pool)
     d = lambda t: t.cuda()
-    part = torch.empty(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
+    part = torch.zeros(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
     coef = torch.empty(3 * C, device="cuda")
     for nsplit in (1, 2):
         out = [torch.zeros(C, device="cuda") for _ in range(3)]
@@ -128,7 +128,7 @@ def test_bn_backward_matches_torch_autograd():
     d = lambda t: t.contiguous().cuda()
     out = [torch.zeros(C, device="cuda") for _ in range(3)]
     dz = torch.empty(z.shape, device="cuda")
-    part = torch.empty(C_.bn_part_floats(N * H * W // 4, C, True), device="cuda")
+    part = torch.zeros(C_.bn_part_floats(N * H * W // 4, C, True), device="cuda")
     coef = torch.empty(3 * C, device="cuda")
     gg = d(gy.float().permute(0, 2, 3, 1))
     C_.bn_bwd(gg, 1, gg, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef,
@@ -329,3 +329,27 @@ def test_sync_modes_through_native_rccl_single_rank(mode):
         outs.append(e.params.flat.clone())
         comm.close()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_bn_reductions_bitwise_reproducible():
+    """BN statistics / backward sums use fixed-order merges: repeated launches on a shared
+    workspace (interleaving shapes) give bitwise-identical results."""
+    C_ = _C()
+    shapes = [(256, 32, 32, 64), (256, 2, 2, 512), (64, 8, 8, 256), (3, 5, 7, 12)]
+    need = max(C_.bn_part_floats(n * h * w, c, bwd) for n, h, w, c in shapes for bwd in (False, True))
+    part = torch.zeros(need, device="cuda")
+    results = {}
+    for rep in range(3):
+        for n, h, w, c in shapes:
+            z = (torch.randn(n, h, w, c, generator=torch.Generator().manual_seed(n * c)) * 2 + 1).cuda()
+            gamma, beta = torch.ones(c, device="cuda"), torch.zeros(c, device="cuda")
+            outs = [torch.zeros(c, device="cuda") for _ in range(4)]
+            C_.bn_fwd_stats(z, 1, z, part, gamma, beta, None, None, None, None, *outs, 0.1, 1e-5)
+            zz = z.reshape(-1, c).double()
+            close(outs[0], zz.mean(0).float(), 1e-5)
+            close(outs[1], torch.rsqrt(zz.var(0, unbiased=False) + 1e-5).float(), 1e-4)
+            cur = torch.cat(outs).cpu()
+            key = (n, h, w, c)
+            if key in results:
+                assert torch.equal(cur, results[key])
+            results[key] = cur
