@@ -465,13 +465,15 @@ class VGGEngine:
         K, P, G = self.K, self.params, self.grads
         n = x.shape[0]
         L = self.spec.convs
-        if pre_forward is not None:
-            pre_forward()
+        buffers_wait = pre_forward() if pre_forward is not None else None
         if self.x0p is not None:
             K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(L):
             z, st = self.z[i][:n], self.stats[i]
             ns = self._conv_fwd(i, x, n, reduce=False)
+            if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
+                buffers_wait()
+                buffers_wait = None
             K.bn_fwd_stats(self.slab if ns > 1 else z, ns, z, self.part, P[f"{l.bn_key}.weight"],
                            P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],

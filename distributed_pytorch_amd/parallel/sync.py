@@ -116,7 +116,10 @@ class GradSync:
         e.refresh_weight_planes()
 
     def pre_forward(self):
-        pass
+        """Called before the training forward.  May return a callable that the engine invokes
+        right before the first read of the BN buffers (so a buffer broadcast overlaps the first
+        conv instead of stalling the step)."""
+        return None
 
     def begin_step(self):
         for b in self.buckets:
@@ -210,7 +213,7 @@ class DDPSync(GradSync):
         with self.comm.region():
             self.comm.broadcast(e.buffers.flat, 0)
             self.comm.broadcast(e.nbt, 0)
-        self.comm.wait()
+        return self.comm.wait
 
     def reduce_bucket(self, b: Bucket):
         self.comm.all_reduce(self.engine.grads.flat[b.lo:b.hi], "sum")

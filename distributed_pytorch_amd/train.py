@@ -95,7 +95,9 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
 
 def test_model(engine: VGGEngine, loader: DeviceLoader, sync=None):
     if sync is not None and sync.mode == "ddp":
-        sync.pre_forward()  # first eval forward under DDP still broadcasts rank 0's buffers
+        wait = sync.pre_forward()  # first eval forward under DDP still broadcasts rank 0's buffers
+        if wait is not None:
+            wait()
     engine.begin_eval()
     nb = 0
     for x, target in loader:

@@ -56,7 +56,9 @@ def run_engine_mode(rank, world, port, mode, steps, outdir, bucket_mb=None, over
         e.finish_step()
         losses.append(float(e.loss.item()))
     if mode == "ddp":
-        sync.pre_forward()  # what the first eval forward does
+        wait = sync.pre_forward()  # what the first eval forward does
+        if wait is not None:
+            wait()
     torch.save({"params": e.params.flat.clone(), "buffers": e.buffers.flat.clone(), "losses": losses,
                 "sd": e.state_dict()}, os.path.join(outdir, f"{mode}_{rank}.pt"))
     dist.barrier()
