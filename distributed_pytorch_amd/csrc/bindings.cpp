@@ -457,9 +457,11 @@ ncclRedOp_t nccl_op(const std::string& op) {
 
 class PyRcclComm {
  public:
-  PyRcclComm(int rank, int world, py::bytes uid, int device, bool high_priority)
+  PyRcclComm(int rank, int world, py::bytes uid, int device, bool high_priority, double timeout_s, double poll_s,
+             bool watchdog, bool exit_on_error, bool debug_sync)
       : stream_(c10::hip::getStreamFromPool(high_priority, (c10::DeviceIndex)device)),
-        comm_(rank, world, std::string(uid), device, stream_.stream()) {}
+        comm_(rank, world, std::string(uid), device, stream_.stream(),
+              dpa::WatchdogConfig{timeout_s, poll_s, watchdog, exit_on_error, debug_sync}) {}
 
   void track(const Tensor& t) { c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_); }
 
@@ -509,6 +511,8 @@ class PyRcclComm {
   std::string async_error() { return comm_.async_error(); }
   void abort() { comm_.abort(); }
   int64_t stream_ptr() { return reinterpret_cast<int64_t>(stream_.stream()); }
+  int64_t outstanding() { return (int64_t)comm_.outstanding(); }
+  int64_t ops_issued() { return (int64_t)comm_.ops_issued(); }
   int rank() const { return comm_.rank(); }
   int world() const { return comm_.world(); }
 
@@ -555,8 +559,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("rccl_unique_id", []() { return py::bytes(dpa::RcclComm::unique_id()); });
   m.def("rccl_version", &dpa::RcclComm::version);
   py::class_<PyRcclComm>(m, "RcclComm")
-      .def(py::init<int, int, py::bytes, int, bool>(), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"),
-           py::arg("high_priority") = false)
+      .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool>(), py::arg("rank"),
+           py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("high_priority") = false,
+           py::arg("timeout_s") = 600.0, py::arg("poll_s") = 0.2, py::arg("watchdog") = true,
+           py::arg("exit_on_error") = true, py::arg("debug_sync") = false)
+      .def("outstanding", &PyRcclComm::outstanding)
+      .def("ops_issued", &PyRcclComm::ops_issued)
       .def("all_reduce", &PyRcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
       .def("broadcast", &PyRcclComm::broadcast)
       .def("gather", &PyRcclComm::gather)

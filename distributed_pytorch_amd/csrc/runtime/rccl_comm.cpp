@@ -1,5 +1,7 @@
 #include "rccl_comm.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -27,8 +29,9 @@ int RcclComm::version() {
   return v;
 }
 
-RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream)
-    : rank_(rank), world_(world), device_(device), stream_(comm_stream) {
+RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,
+                   WatchdogConfig wd)
+    : rank_(rank), world_(world), device_(device), stream_(comm_stream), wd_(wd) {
   if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("bad RCCL unique id size");
   hip_check(hipSetDevice(device), "hipSetDevice");
   ncclUniqueId id;
@@ -36,17 +39,123 @@ RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipS
   check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
   hip_check(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate");
+  if (wd_.enabled) watchdog_ = std::thread([this] { watchdog_loop(); });
 }
 
 RcclComm::~RcclComm() {
+  stop_ = true;
+  cv_.notify_all();
+  if (watchdog_.joinable()) watchdog_.join();
   if (comm_) {
     if (aborted_)
       ncclCommAbort(comm_);
     else
       ncclCommDestroy(comm_);
   }
+  for (auto& op : ops_) hipEventDestroy(op.ev);
+  for (auto ev : free_events_) hipEventDestroy(ev);
   hipEventDestroy(ev_in_);
   hipEventDestroy(ev_out_);
+}
+
+void RcclComm::begin_op() {
+  if (aborted_) {
+    std::lock_guard<std::mutex> g(mu_);
+    throw std::runtime_error("RCCL communicator is aborted: " + (error_.empty() ? std::string("abort()") : error_));
+  }
+}
+
+void RcclComm::end_op(const char* what) {
+  ops_issued_++;
+  if (wd_.debug_sync) {  // host-synchronous op: surfaces ordering bugs and errors at the call site
+    hip_check(hipStreamSynchronize(stream_), what);
+    const std::string e = async_error();
+    if (!e.empty()) throw std::runtime_error(std::string("RCCL error after ") + what + ": " + e);
+    return;
+  }
+  if (!wd_.enabled) return;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!free_events_.empty()) {
+      ev = free_events_.back();
+      free_events_.pop_back();
+    } else {
+      hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+    }
+  }
+  hip_check(hipEventRecord(ev, stream_), "hipEventRecord");
+  std::lock_guard<std::mutex> g(mu_);
+  ops_.push_back(Op{ev, std::chrono::steady_clock::now(), what});
+}
+
+size_t RcclComm::outstanding() {
+  std::lock_guard<std::mutex> g(mu_);
+  return ops_.size();
+}
+
+void RcclComm::fail(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (error_.empty()) error_ = msg;
+  }
+  std::fprintf(stderr, "[dpa rank %d] RCCL watchdog: %s\n", rank_, msg.c_str());
+  std::fflush(stderr);
+  if (!aborted_.exchange(true) && comm_) ncclCommAbort(comm_);
+  comm_ = nullptr;
+  if (wd_.exit_on_error) {
+    std::fprintf(stderr, "[dpa rank %d] terminating the process (exit 70) so the launcher can tear the job down\n",
+                 rank_);
+    std::fflush(stderr);
+    std::_Exit(70);
+  }
+}
+
+void RcclComm::watchdog_loop() {
+  hipSetDevice(device_);
+  const auto poll = std::chrono::duration<double>(wd_.poll_s);
+  std::mutex m;
+  while (!stop_) {
+    {
+      std::unique_lock<std::mutex> lk(m);
+      cv_.wait_for(lk, poll, [this] { return stop_.load(); });
+    }
+    if (stop_ || aborted_) break;
+    // retire completed ops in issue order; time out the oldest pending one
+    std::string timeout_msg;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      while (!ops_.empty()) {
+        const hipError_t q = hipEventQuery(ops_.front().ev);
+        if (q == hipSuccess) {
+          free_events_.push_back(ops_.front().ev);
+          ops_.pop_front();
+          continue;
+        }
+        const double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - ops_.front().t).count();
+        if (q == hipErrorNotReady && age > wd_.timeout_s) {
+          char buf[256];
+          std::snprintf(buf, sizeof(buf), "%s outstanding for %.1f s (timeout %.1f s): peer dead or hung",
+                        ops_.front().what, age, wd_.timeout_s);
+          timeout_msg = buf;
+        } else if (q != hipErrorNotReady) {
+          timeout_msg = std::string("HIP error on the comm stream: ") + hipGetErrorString(q);
+        }
+        break;
+      }
+    }
+    if (!timeout_msg.empty()) {
+      fail(timeout_msg);
+      break;
+    }
+    if (comm_) {
+      ncclResult_t e = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress) {
+        fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(e));
+        break;
+      }
+    }
+  }
 }
 
 void RcclComm::fence_after(hipStream_t after) {
@@ -56,13 +165,17 @@ void RcclComm::fence_after(hipStream_t after) {
 }
 
 void RcclComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t after) {
+  begin_op();
   fence_after(after);
   check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
+  end_op("all_reduce");
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t after) {
+  begin_op();
   fence_after(after);
   check(ncclBroadcast(buf, buf, count, dt, root, comm_, stream_), "ncclBroadcast");
+  end_op("broadcast");
 }
 
 static size_t dt_size(ncclDataType_t dt) {
@@ -83,6 +196,7 @@ static size_t dt_size(ncclDataType_t dt) {
 }
 
 void RcclComm::gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t after) {
+  begin_op();
   fence_after(after);
   const size_t bytes = count * dt_size(dt);
   check(ncclGroupStart(), "ncclGroupStart");
@@ -99,27 +213,36 @@ void RcclComm::gather(const void* send, void* recv, size_t count, ncclDataType_t
     check(ncclSend(send, count, dt, root, comm_, stream_), "ncclSend");
   }
   check(ncclGroupEnd(), "ncclGroupEnd");
+  end_op("gather");
 }
 
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t recvcount, ncclDataType_t dt, ncclRedOp_t op,
                               hipStream_t after) {
+  begin_op();
   fence_after(after);
   check(ncclReduceScatter(send, recv, recvcount, dt, op, comm_, stream_), "ncclReduceScatter");
+  end_op("reduce_scatter");
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t sendcount, ncclDataType_t dt, hipStream_t after) {
+  begin_op();
   fence_after(after);
   check(ncclAllGather(send, recv, sendcount, dt, comm_, stream_), "ncclAllGather");
+  end_op("all_gather");
 }
 
 void RcclComm::send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t after) {
+  begin_op();
   fence_after(after);
   check(ncclSend(buf, count, dt, peer, comm_, stream_), "ncclSend");
+  end_op("send");
 }
 
 void RcclComm::recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t after) {
+  begin_op();
   fence_after(after);
   check(ncclRecv(buf, count, dt, peer, comm_, stream_), "ncclRecv");
+  end_op("recv");
 }
 
 void RcclComm::wait(hipStream_t waiter) {
@@ -131,6 +254,11 @@ void RcclComm::wait(hipStream_t waiter) {
 void RcclComm::synchronize() { hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
 
 std::string RcclComm::async_error() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!error_.empty()) return error_;
+  }
+  if (aborted_) return "communicator aborted";
   if (!comm_) return "no communicator";
   ncclResult_t e = ncclSuccess;
   ncclResult_t r = ncclCommGetAsyncError(comm_, &e);
@@ -140,6 +268,9 @@ std::string RcclComm::async_error() {
 }
 
 void RcclComm::abort() {
+  stop_ = true;
+  cv_.notify_all();
+  if (watchdog_.joinable() && watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();
   if (comm_ && !aborted_.exchange(true)) {
     ncclCommAbort(comm_);
     comm_ = nullptr;

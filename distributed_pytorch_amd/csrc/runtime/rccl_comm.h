@@ -10,15 +10,35 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace dpa {
 
+// Failure handling: every issued op is tracked with a completion event; a
+// watchdog thread polls ncclCommGetAsyncError and the oldest outstanding op.  On an async RCCL
+// error or an op outstanding longer than `timeout_s`, it records the error, aborts the
+// communicator (unblocking RCCL kernels stuck on a dead peer) and, if `exit_on_error`, terminates
+// the process (exit code 70) so the launcher tears the job down instead of hanging.
+// `debug_sync` makes every op host-synchronous and error-checked (race / ordering debugging).
+struct WatchdogConfig {
+  double timeout_s = 600.0;
+  double poll_s = 0.2;
+  bool enabled = true;
+  bool exit_on_error = true;
+  bool debug_sync = false;
+};
+
 class RcclComm {
  public:
   // uid: NCCL_UNIQUE_ID_BYTES bytes created by rank 0 (unique_id()) and shared out of band.
-  RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream);
+  RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,
+           WatchdogConfig wd = WatchdogConfig());
   ~RcclComm();
 
   static std::string unique_id();
@@ -44,19 +64,40 @@ class RcclComm {
   void wait(hipStream_t waiter);
   // Host blocks until all comm work issued so far completes.
   void synchronize();
-  // Non-blocking: returns "" if healthy, else an error string (ncclCommGetAsyncError).
+  // Non-blocking: returns "" if healthy, else an error string (async RCCL error or watchdog).
   std::string async_error();
   void abort();
+  // ops issued and still outstanding (watchdog view)
+  size_t outstanding();
+  uint64_t ops_issued() const { return ops_issued_.load(); }
 
  private:
   void fence_after(hipStream_t after);
   void check(ncclResult_t r, const char* what);
+  void begin_op();                // throws if the communicator is dead
+  void end_op(const char* what);  // track completion (or sync in debug mode)
+  void watchdog_loop();
+  void fail(const std::string& msg);
 
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_;
   hipEvent_t ev_in_, ev_out_;
   std::atomic<bool> aborted_{false};
+  WatchdogConfig wd_;
+  struct Op {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t;
+    const char* what;
+  };
+  std::mutex mu_;  // guards ops_, free_events_, error_
+  std::deque<Op> ops_;
+  std::vector<hipEvent_t> free_events_;
+  std::string error_;
+  std::atomic<uint64_t> ops_issued_{0};
+  std::atomic<bool> stop_{false};
+  std::condition_variable cv_;
+  std::thread watchdog_;
 };
 
 }  // namespace dpa

@@ -169,7 +169,14 @@ def exchange_unique_id(store, rank: int, make_uid, tag: str = "dpa_rccl_uid", ti
 
 
 class RcclComm(Comm):
-    """Native RCCL communicator (one per process/GPU)."""
+    """Native RCCL communicator (one per process/GPU).
+
+    Failure handling (native watchdog thread, csrc/runtime/rccl_comm.cpp): env
+    ``DPA_COMM_TIMEOUT`` (s, default 600) bounds how long any collective may stay outstanding;
+    async RCCL errors and timeouts abort the communicator and, unless ``DPA_WATCHDOG_EXIT=0``,
+    end the process with exit code 70 so the launcher tears the job down.  ``DPA_DEBUG_SYNC=1``
+    makes every collective host-synchronous and error-checked (ordering/race debugging).
+    ``DPA_WATCHDOG=0`` disables the thread."""
 
     name = "rccl"
 
@@ -186,7 +193,11 @@ class RcclComm(Comm):
             uid = exchange_unique_id(store, rank, C.rccl_unique_id, tag)
         with torch.cuda.device(self.device):
             self._c = C.RcclComm(rank, world, bytes(uid), self.device.index or 0,
-                                 os.environ.get("DPA_COMM_HIPRIO", "0") == "1")
+                                 high_priority=os.environ.get("DPA_COMM_HIPRIO", "0") == "1",
+                                 timeout_s=float(os.environ.get("DPA_COMM_TIMEOUT", "600")),
+                                 watchdog=os.environ.get("DPA_WATCHDOG", "1") == "1",
+                                 exit_on_error=os.environ.get("DPA_WATCHDOG_EXIT", "1") == "1",
+                                 debug_sync=os.environ.get("DPA_DEBUG_SYNC", "0") == "1")
         self.stream = torch.cuda.ExternalStream(self._c.stream_ptr(), device=self.device)
         self._store = store
 
@@ -237,3 +248,10 @@ class RcclComm(Comm):
 
     def abort(self):
         self._c.abort()
+
+    def outstanding(self) -> int:
+        """Collectives issued whose completion the watchdog has not yet observed."""
+        return self._c.outstanding()
+
+    def ops_issued(self) -> int:
+        return self._c.ops_issued()

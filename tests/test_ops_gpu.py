@@ -298,14 +298,17 @@ def test_engine_training_converges_and_evaluates(impl):
     assert 0 <= acc[1] <= 256 and acc[0] == acc[0]
 
 
+@pytest.mark.parametrize("debug_sync", [False, True])
 @pytest.mark.parametrize("mode", ["ddp", "allreduce", "gather"])
-def test_sync_modes_through_native_rccl_single_rank(mode):
+def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatch):
     """A 1-rank native RCCL communicator (every collective is an identity) driving the real
     bucket / comm-stream / event path: results must equal the no-communication run bit for bit."""
     from distributed_pytorch_amd import _ext
     from distributed_pytorch_amd.engine import VGGEngine
     from distributed_pytorch_amd.parallel import NullComm, RcclComm, make_sync
 
+    if debug_sync:  # every collective host-synchronous + error-checked
+        monkeypatch.setenv("DPA_DEBUG_SYNC", "1")
     C = _ext.require()
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(9)
@@ -353,3 +356,26 @@ def test_bn_reductions_bitwise_reproducible():
             if key in results:
                 assert torch.equal(cur, results[key])
             results[key] = cur
+
+
+def test_rccl_watchdog_tracks_and_retires_ops():
+    import time
+
+    from distributed_pytorch_amd import _ext
+
+    C = _ext.require()
+    c = C.RcclComm(0, 1, C.rccl_unique_id(), 0, timeout_s=60.0, poll_s=0.05, exit_on_error=False)
+    t = torch.ones(1 << 20, device="cuda")
+    for _ in range(5):
+        c.all_reduce(t, "sum")
+    c.broadcast(t, 0)
+    c.synchronize()
+    deadline = time.time() + 10
+    while c.outstanding() and time.time() < deadline:
+        time.sleep(0.05)
+    assert c.outstanding() == 0 and c.ops_issued() == 6
+    assert c.async_error() == ""
+    assert torch.all(t == 1)
+    c.abort()
+    with pytest.raises(RuntimeError, match="aborted"):
+        c.all_reduce(t, "sum")
