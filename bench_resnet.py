@@ -1,0 +1,97 @@
+"""Stress benchmark: ResNet-50, ImageNet-shaped, bf16 MFMA compute, DDP (BASELINE.json config 5).
+
+New scope (the reference has only VGG-11).  Per-GPU batch is fixed (weak scaling); synthetic
+ImageNet-shaped data (224x224x3 NHWC, 1000 classes) resident on the device; random init.
+Every timed step: forward, loss, backward with bucketed RCCL all-reduce issued from gradient
+hooks (parallel/ddp.py), fused SGD(0.1, 0.9, wd 1e-4).
+
+    python bench_resnet.py [--batch 128] [--steps 20] [--warmup 5] [--impl bf16|x3]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench_resnet.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_pytorch_amd.models.resnet import resnet50  # noqa: E402
+from distributed_pytorch_amd.parallel import init_env  # noqa: E402
+from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel, FlatSGD  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--impl", default="bf16", choices=["bf16", "x3"])
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    a = ap.parse_args()
+    ctx = init_env(comm=a.comm)
+    dev = ctx.device
+    torch.manual_seed(1)
+    model = resnet50(1000, a.impl).to(dev)
+    ddp = DistributedDataParallel(model, ctx.comm, bucket_mb=a.bucket_mb)
+    opt = FlatSGD(ddp, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator(device=dev).manual_seed(100 + ctx.rank)
+    x = torch.randn(a.batch, a.image, a.image, 3, device=dev, generator=g)
+    t = torch.randint(0, 1000, (a.batch,), device=dev, generator=g)
+
+    def step():
+        opt.zero_grad()
+        loss = F.cross_entropy(ddp(x), t)
+        loss.backward()
+        opt.step(ddp.finish())
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+
+    def barrier():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if ctx.world > 1:
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    barrier()
+    el = time.perf_counter() - t0
+    if ctx.world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt[0])
+    img_s = a.batch * ctx.world * a.steps / el
+    if ctx.rank == 0:
+        print(json.dumps({
+            "metric": f"images/sec ResNet-50 ImageNet-shaped training (batch {a.batch}/GPU)",
+            "value": round(img_s, 1), "unit": "images/sec", "n_gpus": ctx.world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if a.impl == "bf16" else "fp32",
+            "data": "synthetic (ImageNet-shaped 224x224x3 on device, random labels)",
+            "config": {"model": "resnet50", "global_batch": a.batch * ctx.world, "seq_len": None,
+                       "image_size": a.image, "parallelism": f"dp{ctx.world}", "buckets": ddp.num_buckets(),
+                       "comm": ctx.comm.name, "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
+            "final_loss": round(float(loss.item()), 4),
+        }), flush=True)
+    ctx.shutdown()
+
+
+if __name__ == "__main__":
+    main()

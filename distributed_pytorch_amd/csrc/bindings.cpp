@@ -25,11 +25,11 @@ int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M,
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
                        const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st);
 int dpa_bn_apply(const float* z, float* a, unsigned short* a3, int np, const float* scale, const float* shift, int N,
-                 int H, int W, int C, int pool, hipStream_t st);
+                 int H, int W, int C, int pool, int act, const float* res, hipStream_t st);
 int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
-               int pool, hipStream_t st);
+               int pool, int act, const float* res, float* dres, hipStream_t st);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st);
@@ -327,20 +327,29 @@ void bn_eval_params(Tensor gamma, Tensor beta, OptT bias, Tensor rmean, Tensor r
       "bn_eval_params");
 }
 
-// a: fp32 [N,Ho,Wo,C] or bf16 planes [NP,N,Ho,Wo,C]
-void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool) {
+// a: fp32 [N,Ho,Wo,C] or bf16 planes [NP,N,Ho,Wo,C].  act: 0 relu, 1 none, 2 relu(. + res)
+void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t act, OptT res) {
   need(z, "z");
+  const float* rp = nullptr;
+  if (act == 2) {
+    TORCH_CHECK(res.has_value() && res->defined(), "bn_apply: act=2 needs the residual");
+    need(*res, "res");
+    TORCH_CHECK(res->numel() == z.numel(), "bn_apply: residual shape");
+    rp = fp(*res);
+  }
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
   const int64_t outn = (int64_t)N * (pool ? (H / 2) * (W / 2) : H * W) * C;
   if (a.scalar_type() == at::kBFloat16) {
     need_planes(a, "a3");
     TORCH_CHECK(a.numel() == a.size(0) * outn, "bn_apply: a3 shape");
-    chk(dpa_bn_apply(fp(z), nullptr, up(a), a.size(0), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()),
+    chk(dpa_bn_apply(fp(z), nullptr, up(a), a.size(0), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp,
+                     cur_stream()),
         "bn_apply");
   } else {
     need(a, "a");
     TORCH_CHECK(a.numel() == outn, "bn_apply: a shape");
-    chk(dpa_bn_apply(fp(z), fp(a), nullptr, 0, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, cur_stream()),
+    chk(dpa_bn_apply(fp(z), fp(a), nullptr, 0, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp,
+                     cur_stream()),
         "bn_apply");
   }
 }
@@ -348,8 +357,20 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool) {
 // gsrc: grad wrt the layer output (pooled shape if pool) or nsplit slabs of it (then the sum is
 // written to g).
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
-            Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool) {
+            Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
+            int64_t act, OptT res, OptT dres) {
   need(gsrc, "gsrc");
+  const float* rp = nullptr;
+  float* drp = nullptr;
+  if (act == 2) {
+    TORCH_CHECK(res.has_value() && res->defined() && dres.has_value() && dres->defined(),
+                "bn_bwd: act=2 needs res and dres");
+    need(*res, "res");
+    need(*dres, "dres");
+    TORCH_CHECK(res->numel() == z.numel() && dres->numel() == z.numel(), "bn_bwd: residual shape");
+    rp = fp(*res);
+    drp = fp(*dres);
+  }
   need(g, "g");
   need(z, "z");
   float* dzf = nullptr;
@@ -371,7 +392,8 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd: part too small");
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
   chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
-                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, cur_stream()),
+                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
+                 cur_stream()),
       "bn_bwd");
 }
 
@@ -551,8 +573,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);
-  m.def("bn_apply", &bn_apply);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_apply", &bn_apply, py::arg("z"), py::arg("a"), py::arg("scale"), py::arg("shift"), py::arg("pool"),
+        py::arg("act") = 0, py::arg("res") = py::none());
+  m.def("bn_bwd", &bn_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"), py::arg("scale"),
+        py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
+        py::arg("res") = py::none(), py::arg("dres") = py::none());
   m.def("fc_ce_train", &fc_ce_train);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);

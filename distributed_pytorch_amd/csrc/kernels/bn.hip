@@ -16,6 +16,10 @@
 //           reduce pass (sum dy, sum dy*xhat, sum xhat; optionally summing split-K dgrad slabs
 //           of g and writing g) -> finalize -> apply pass writing dz.
 //
+// Activation modes (ACT): 0 = ReLU (VGG, optional fused 2x2 max-pool), 1 = none (ResNet
+// downsample / pre-add BN), 2 = ReLU(BN(z) + residual) (ResNet block output; backward also emits
+// the residual-branch gradient).  The ReLU mask is recomputed from z (and the residual).
+//
 // Reductions: a RT-thread (1024) block covers RPB rows x all channels (threads per row = C/4
 // float4 lanes, RT/(C/4) rows in flight, 4 rows' loads issued together), keeps per-thread partials
 // in registers, combines them with an LDS tree, and writes ONE partial per (block, channel) —
@@ -254,12 +258,14 @@ __device__ __forceinline__ float4 affine_relu(float4 v, float4 sc, float4 sh) {
                      fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
 }
 
-// a = relu(z*scale + shift), optionally 2x2/s2 max-pooled.  z: [N,H,W,C]  a: [N,H/2,W/2,C] or [N,H,W,C]
-template <bool POOL, int NP>
+// a = act(z*scale + shift [+ res]), optionally 2x2/s2 max-pooled (ACT 0 only).
+// z: [N,H,W,C]  a: [N,H/2,W/2,C] or [N,H,W,C]
+template <bool POOL, int NP, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, float* __restrict__ a,
                                                        u16* __restrict__ a3, long ps,
                                                        const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, int N, int H, int W, int C) {
+                                                       const float* __restrict__ shift, const float* __restrict__ res,
+                                                       int N, int H, int W, int C) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
@@ -270,7 +276,18 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
     const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
     if (!POOL) {
-      store4<NP>(a, a3, ps, i, affine_relu(z4[i], sc, sh));
+      if constexpr (ACT == 0) {
+        store4<NP>(a, a3, ps, i, affine_relu(z4[i], sc, sh));
+      } else {
+        const float4 v = z4[i];
+        float4 u = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
+                               fmaf(v.w, sc.w, sh.w));
+        if constexpr (ACT == 2) {
+          const float4 r = reinterpret_cast<const float4*>(res)[i];
+          u = make_float4(fmaxf(u.x + r.x, 0.f), fmaxf(u.y + r.y, 0.f), fmaxf(u.z + r.z, 0.f), fmaxf(u.w + r.w, 0.f));
+        }
+        store4<NP>(a, a3, ps, i, u);
+      }
     } else {
       long t = i / C4;
       const int ow = (int)(t % Wo);
@@ -289,6 +306,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
                              fmaxf(fmaxf(v00.w, v01.w), fmaxf(v10.w, v11.w))));
     }
   }
+}
+
+// gradient through the activation at one element: u = BN output, r = residual (ACT 2)
+template <int ACT>
+__device__ __forceinline__ float act_grad(float u, float r, float g) {
+  if constexpr (ACT == 0) return u > 0.f ? g : 0.f;
+  else if constexpr (ACT == 1) return g;
+  else return (u + r) > 0.f ? g : 0.f;
 }
 
 // route the pooled grad to the first max of the window (scan order 00,01,10,11), relu mask
@@ -310,9 +335,10 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat.  Rows are OUTPUT rows of
 // the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
 // the summed g is written to gout (consumed by the apply pass).  part layout: [block][3][C]
-template <bool POOL>
+template <bool POOL, int ACT>
 __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restrict__ gsrc, float* __restrict__ gout,
                                                             int nsplit, const float* __restrict__ z,
+                                                            const float* __restrict__ res,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
@@ -347,10 +373,11 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restri
         if (nsplit > 1) reinterpret_cast<float4*>(gout)[gi] = gv;
         if (!POOL) {
           const float4 zv = z4[gi];
+          const float4 rv = ACT == 2 ? reinterpret_cast<const float4*>(res)[gi] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float zz = F4GET(zv, k);
-            const float dy = fmaf(zz, F4GET(sc, k), F4GET(sh, k)) > 0.f ? F4GET(gv, k) : 0.f;
+            const float dy = act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv, k), F4GET(gv, k));
             const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
             sdy[k] += dy;
             sdx[k] = fmaf(dy, xh, sdx[k]);
@@ -459,13 +486,14 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-template <bool POOL, int NP>
+template <bool POOL, int NP, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ z,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ coef, float* __restrict__ dz,
-                                                           u16* __restrict__ dz3, long ps, int N, int H, int W,
-                                                           int C) {
+                                                           u16* __restrict__ dz3, long ps,
+                                                           const float* __restrict__ res, float* __restrict__ dres,
+                                                           int N, int H, int W, int C) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
@@ -482,14 +510,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     const float4 gv = g4[i];
     if (!POOL) {
       const float4 zv = z4[i];
-      float r[4];
+      const float4 rv = ACT == 2 ? reinterpret_cast<const float4*>(res)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float r[4], dyv[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float zz = F4GET(zv, k);
-        const float dy = fmaf(zz, F4GET(sc, k), F4GET(sh, k)) > 0.f ? F4GET(gv, k) : 0.f;
+        const float dy = act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv, k), F4GET(gv, k));
+        dyv[k] = dy;
         r[k] = F4GET(k1, k) * dy + F4GET(k2, k) * zz + F4GET(k3, k);
       }
       store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]));
+      if constexpr (ACT == 2) reinterpret_cast<float4*>(dres)[i] = make_float4(dyv[0], dyv[1], dyv[2], dyv[3]);
     } else {
       long t = i / C4;
       const int ow = (int)(t % Wo);
@@ -563,13 +594,23 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
     }                                       \
   } while (0)
 
-// out: fp32 a (np == 0) or bf16 planes a3 [np][...] (np in {1, 3})
+// out: fp32 a (np == 0) or bf16 planes a3 [np][...] (np in {1, 3}).  act: 0 relu (pool allowed),
+// 1 none, 2 relu(. + res)
 int dpa_bn_apply(const float* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
-                 int W, int C, int pool, hipStream_t st) {
-  if (C % 4) return -2;
+                 int W, int C, int pool, int act, const float* res, hipStream_t st) {
+  if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && !res)) return -2;
   const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   const long ps = total * 4;
-#define L_APPLY(P, NPT) bn_apply_kernel<P, NPT><<<grid_1d(total), 256, 0, st>>>(z, a, a3, ps, scale, shift, N, H, W, C)
+  const int grid = grid_1d(total);
+#define L_APPLY(P, NPT)                                                                                           \
+  do {                                                                                                            \
+    if (act == 0)                                                                                                 \
+      bn_apply_kernel<P, NPT, 0><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);              \
+    else if (!(P) && act == 1)                                                                                    \
+      bn_apply_kernel<false, NPT, 1><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);          \
+    else if (!(P))                                                                                                \
+      bn_apply_kernel<false, NPT, 2><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);          \
+  } while (0)
   BN_DISPATCH_NP(np, pool, L_APPLY);
 #undef L_APPLY
   return (int)hipGetLastError();
@@ -579,27 +620,44 @@ int dpa_bn_apply(const float* z, float* a, u16* a3, int np, const float* scale, 
 // written to g).  Writes dz [N,H,W,C] and dgamma/dbeta/dbias.
 int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
-               float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool,
-               hipStream_t st) {
-  if (C % 4) return -2;
+               float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
+               const float* res, float* dres, hipStream_t st) {
+  if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && (!res || !dres))) return -2;
   if (nsplit < 1) nsplit = 1;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = red_rows_per_block(Mo, C);
   const int nblk = (Mo + rpb - 1) / rpb;
   if (pool)
-    bn_bwd_reduce_kernel<true><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W, C,
-                                                     rpb);
+    bn_bwd_reduce_kernel<true, 0><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N, H,
+                                                        W, C, rpb);
+  else if (act == 0)
+    bn_bwd_reduce_kernel<false, 0><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N,
+                                                         H, W, C, rpb);
+  else if (act == 1)
+    bn_bwd_reduce_kernel<false, 1><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N,
+                                                         H, W, C, rpb);
   else
-    bn_bwd_reduce_kernel<false><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, scale, shift, mean, invstd, part, N, H, W,
-                                                      C, rpb);
+    bn_bwd_reduce_kernel<false, 2><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N,
+                                                         H, W, C, rpb);
   bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
                                                       dbeta, dbias, coef);
   const float* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
   const long ps = (long)N * H * W * C;
-#define L_BAPPLY(P, NPT) \
-  bn_bwd_apply_kernel<P, NPT><<<grid_1d(total), 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, N, H, W, C)
+  const int grid = grid_1d(total);
+#define L_BAPPLY(P, NPT)                                                                                           \
+  do {                                                                                                             \
+    if (act == 0)                                                                                                  \
+      bn_bwd_apply_kernel<P, NPT, 0><<<grid, 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, \
+                                                            W, C);                                                 \
+    else if (!(P) && act == 1)                                                                                     \
+      bn_bwd_apply_kernel<false, NPT, 1><<<grid, 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, \
+                                                                H, W, C);                                          \
+    else if (!(P))                                                                                                 \
+      bn_bwd_apply_kernel<false, NPT, 2><<<grid, 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, \
+                                                                H, W, C);                                          \
+  } while (0)
   BN_DISPATCH_NP(np, pool, L_BAPPLY);
 #undef L_BAPPLY
   return (int)hipGetLastError();

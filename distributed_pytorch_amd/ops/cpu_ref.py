@@ -121,25 +121,36 @@ def bn_eval_params(gamma, beta, bias, rmean, rvar, scale, shift, eps):
     shift.copy_(beta + (b - rmean) * s)
 
 
-def bn_apply(z, a, scale, shift, pool):
-    y = torch.relu(z * scale + shift)
+def _act(u, act, res):
+    if act == 1:
+        return u
+    if act == 2:
+        u = u + res.reshape(u.shape)
+    return torch.relu(u)
+
+
+def bn_apply(z, a, scale, shift, pool, act=0, res=None):
+    y = _act(z * scale + shift, act, res)
     if pool:
         y = _nhwc(F.max_pool2d(_nchw(y), 2, 2))
     a.copy_(y.reshape(a.shape))
 
 
-def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool):
+def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool,
+           act=0, res=None, dres=None):
     N, H, W, C = z.shape
     if nsplit > 1:
         g.copy_(gsrc[:nsplit * g.numel()].view(nsplit, -1).sum(0).view(g.shape))
     else:
         g = gsrc
     with torch.enable_grad():
-        u = (z * scale + shift).detach().requires_grad_(True)  # BN output, pre-ReLU
-        y = torch.relu(u)
+        u = (z * scale + shift).detach().requires_grad_(True)  # BN output, pre-activation
+        y = _act(u, act, res)
         if pool:
             y = _nhwc(F.max_pool2d(_nchw(y), 2, 2))
         (dy,) = torch.autograd.grad(y, u, g.reshape(y.shape))
+    if act == 2:
+        dres.copy_(dy.reshape(dres.shape))
     xh = (z - mean) * invstd
     M = N * H * W
     sdy = dy.reshape(-1, C).sum(0)

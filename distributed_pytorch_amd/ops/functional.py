@@ -1,0 +1,218 @@
+"""Autograd functions over the gfx950 kernels, for generic ``nn.Module`` models (ResNet-50 etc.).
+
+The VGG engine (engine.py) drives the kernels through a static, hand-scheduled step; this module
+exposes the same kernels to PyTorch autograd so arbitrary NHWC conv/BN networks can be built from
+them ("autograd.Functions over the kernels, used for generic nn.Module paths").
+
+Layout and precision contract (all tensors NHWC, contiguous):
+  conv2d_nhwc   x fp32 [N,H,W,C] (C % 8 == 0), w fp32 [K,R,S,C] -> z fp32 [N,P,Q,K]
+                The operands are split into bf16 planes inside the op: impl "bf16" = one plane
+                (mixed precision, fp32 accumulation), "x3" = three planes (fp32-grade, see
+                conv_x3.hip).  No conv bias (every conv here feeds a BatchNorm).
+  bn_act_nhwc   z fp32 -> act(BN(z) [+ residual]) fp32; act 0 = ReLU, 1 = none, 2 = ReLU(. + res).
+                Training mode updates running stats in place (momentum, unbiased var) and
+                num_batches_tracked; backward recomputes the activation mask from z (+res).
+On CPU the same functions run the fp32 CPU oracle (ops/cpu_ref.py) so models are testable here;
+on a GPU the native extension is required (loud failure, no silent fallback).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from . import cpu_ref
+
+ACT = {"relu": 0, "none": 1, "add_relu": 2}
+NPLANES = {"bf16": 1, "x3": 3}
+
+
+def _native(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+class _Workspace:
+    """Per-device scratch reused by consecutive ops (all on the compute stream, so stream order
+    makes reuse safe): split-K slabs and the BN reduction workspace (zero-initialised once)."""
+
+    def __init__(self):
+        self.bufs: Dict[Tuple[str, torch.device], torch.Tensor] = {}
+
+    def get(self, kind: str, numel: int, device, zero: bool = False) -> torch.Tensor:
+        key = (kind, torch.device(device))
+        t = self.bufs.get(key)
+        if t is None or t.numel() < numel:
+            t = (torch.zeros if zero else torch.empty)(max(numel, 64), device=device, dtype=torch.float32)
+            self.bufs[key] = t
+        return t
+
+
+WS = _Workspace()
+
+
+def split_planes(x: torch.Tensor, np_: int) -> torch.Tensor:
+    out = torch.empty((np_,) + tuple(x.shape), device=x.device, dtype=torch.bfloat16)
+    _ext.require().split_planes(x.contiguous(), out)
+    return out
+
+
+# ------------------------------------------------------------------ conv launch configuration
+_cfg_cache: Dict[tuple, Tuple[int, int, bool]] = {}
+
+
+def conv_config(kind: str, M: int, Ngemm: int, Kred: int, hw_small: bool) -> Tuple[int, int, bool]:
+    """(tile, splits, posmajor) heuristic for a GEMM view of a conv call: 128x128 single-stage
+    tiles; split-K until ~2 blocks per CU; position-major rows for small spatial maps."""
+    key = (kind, M, Ngemm, Kred, hw_small)
+    c = _cfg_cache.get(key)
+    if c is not None:
+        return c
+    cd = lambda a, b: (a + b - 1) // b
+    if kind == "wgrad":
+        tiles = cd(Ngemm, 128) * cd(Kred, 128)   # Kout x (R*S*C), reduction over M
+        red = M
+    else:
+        tiles = cd(M, 128) * cd(Ngemm, 128)
+        red = Kred
+    s = 1
+    while tiles * s < 512 and red // (2 * s) >= 256 and s < (512 if kind == "wgrad" else 16):
+        s *= 2
+    c = (5, s, hw_small)
+    _cfg_cache[key] = c
+    return c
+
+
+class Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride: int, pad: int, impl: str):
+        N, H, W, C = x.shape
+        K, R, S, _ = w.shape
+        P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        ctx.geom = (N, H, W, C, K, R, S, stride, pad, P, Q)
+        ctx.impl = impl
+        if not _native(x):
+            z = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
+            ctx.save_for_backward(x, w)
+            return z.permute(0, 2, 3, 1).contiguous()
+        Kx = _ext.require()
+        np_ = NPLANES[impl]
+        xp, wp = split_planes(x, np_), split_planes(w, np_)
+        z = torch.empty(N, P, Q, K, device=x.device, dtype=torch.float32)
+        tile, s, pm = conv_config("fprop", N * P * Q, K, R * S * C, P * Q <= 16)
+        s = Kx.x3_splits(R * S * C, s)
+        slab = WS.get("slab", s * N * P * Q * K, x.device) if s > 1 else None
+        Kx.conv_x3_fprop(xp, wp, z, slab, stride, pad, s, tile, True, pm)
+        ctx.save_for_backward(xp, wp)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        N, H, W, C, K, R, S, stride, pad, P, Q = ctx.geom
+        a, b = ctx.saved_tensors
+        dz = dz.contiguous()
+        dx = dw = None
+        if not _native(dz):
+            x, w = a, b
+            xn, wn = x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2)
+            dzn = dz.permute(0, 3, 1, 2)
+            if ctx.needs_input_grad[0]:
+                dx = torch.nn.grad.conv2d_input(xn.shape, wn, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
+            if ctx.needs_input_grad[1]:
+                dw = torch.nn.grad.conv2d_weight(xn, wn.shape, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
+            return dx, dw, None, None, None
+        Kx = _ext.require()
+        xp, wp = a, b
+        dzp = split_planes(dz, xp.shape[0])
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(N, H, W, C, device=dz.device, dtype=torch.float32)
+            tile, s, pm = conv_config("dgrad", N * H * W, C, R * S * K, H * W <= 16)
+            s = Kx.x3_splits(R * S * K, s)
+            slab = WS.get("slab", s * N * H * W * C, dz.device) if s > 1 else None
+            Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
+            tile, s, pm = conv_config("wgrad", N * P * Q, K, R * S * C, P * Q <= 16)
+            s = Kx.x3_splits(N * P * Q, s)
+            slab = WS.get("slab", s * K * R * S * C, dz.device) if s > 1 else None
+            Kx.conv_x3_wgrad(xp, dzp, dw, slab, stride, pad, s, tile, pm)
+        return dx, dw, None, None, None
+
+
+def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, impl: str = "bf16"):
+    if impl not in NPLANES:
+        raise ValueError(f"impl must be one of {list(NPLANES)}")
+    return Conv2dNHWC.apply(x.contiguous(), w, int(stride), int(pad), impl)
+
+
+class BnActNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, gamma, beta, res, rmean, rvar, nbt, training: bool, momentum: float, eps: float, act: int):
+        N, H, W, C = z.shape
+        dev = z.device
+        K = _ext.require() if _native(z) else cpu_ref
+        f32 = dict(device=dev, dtype=z.dtype)  # fp32 on GPU; the CPU oracle also runs float64
+        mean, invstd, scale, shift = (torch.empty(C, **f32) for _ in range(4))
+        if training:
+            part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), dev, zero=True) if _native(z) else None
+            K.bn_fwd_stats(z, 1, z, part, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale, shift, momentum,
+                           eps)
+        else:
+            K.bn_eval_params(gamma, beta, None, rmean, rvar, scale, shift, eps)
+        a = torch.empty_like(z)
+        K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None)
+        ctx.act, ctx.training = act, training
+        ctx.save_for_backward(z, res if act == 2 else None, gamma, mean, invstd, scale, shift)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        z, res, gamma, mean, invstd, scale, shift = ctx.saved_tensors
+        if not ctx.training:
+            raise RuntimeError("bn_act_nhwc backward is only defined in training mode")
+        da = da.contiguous()
+        N, H, W, C = z.shape
+        native = _native(z)
+        K = _ext.require() if native else cpu_ref
+        f32 = dict(device=z.device, dtype=z.dtype)
+        dz = torch.empty_like(z)
+        dgamma, dbeta = torch.empty(C, **f32), torch.empty(C, **f32)
+        dres = torch.empty_like(z) if ctx.act == 2 else None
+        part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), z.device, zero=True) if native else None
+        coef = torch.empty(3 * C, **f32)
+        K.bn_bwd(da, 1, da, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, None, dz, False, ctx.act,
+                 res, dres)
+        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None
+
+
+def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, training: bool = True,
+                momentum: float = 0.1, eps: float = 1e-5, act: str = "relu", residual: Optional[torch.Tensor] = None):
+    a = ACT[act]
+    if a == 2 and residual is None:
+        raise ValueError("act='add_relu' needs a residual")
+    res = residual.contiguous() if residual is not None else None
+    return BnActNHWC.apply(z.contiguous(), gamma, beta, res, running_mean, running_var, num_batches_tracked,
+                           bool(training), float(momentum), float(eps), a)
+
+
+def max_pool_nhwc(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -> torch.Tensor:
+    """Max-pool on an NHWC tensor (channels_last view; stem pooling is a minor op)."""
+    y = F.max_pool2d(x.permute(0, 3, 1, 2), k, stride, pad)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def conv_out(h: int, k: int, stride: int, pad: int) -> int:
+    return (h + 2 * pad - k) // stride + 1
+
+
+def kaiming_uniform_krsc(K: int, R: int, S: int, C: int, c_true: Optional[int] = None) -> torch.Tensor:
+    """torch's default Conv2d init (kaiming_uniform, a=sqrt(5)) in KRSC layout; channels beyond
+    c_true (input padding) are zero."""
+    c_true = c_true or C
+    w = torch.empty(K, c_true, R, S)
+    torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    out = torch.zeros(K, R, S, C)
+    out[..., :c_true] = w.permute(0, 2, 3, 1)
+    return out

@@ -119,3 +119,46 @@ def run_uid_exchange(rank, world, port, outdir):
         f.write(uid)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_generic_ddp(rank, world, port, steps, outdir, impl="ours"):
+    """Generic DDP wrapper (parallel/ddp.py) on a small ResNet vs stock torch DDP on the same
+    network (float64, gloo)."""
+    from torch.nn.parallel import DistributedDataParallel as TorchDDP
+
+    from distributed_pytorch_amd.models.resnet import ResNet, ResNetRef
+    from distributed_pytorch_amd.parallel import TorchComm
+    from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel, FlatSGD
+
+    _init(rank, world, port)
+    torch.manual_seed(5 + rank)  # different init per rank: the wrap-time broadcast must unify them
+    ours = ResNet([1, 1, 1, 1], 10).double()
+    torch.manual_seed(5)
+    ref = ResNetRef([1, 1, 1, 1], 10).double()
+    if rank == 0:
+        ref.load_state_dict(ours.state_dict())
+    g = torch.Generator().manual_seed(40 + rank)
+    data = [(torch.randn(3, 3, 32, 32, generator=g, dtype=torch.float64), torch.randint(0, 10, (3,), generator=g))
+            for _ in range(steps)]
+    if impl == "ours":
+        m = DistributedDataParallel(ours, TorchComm(device=torch.device("cpu")), bucket_mb=0.5)
+        opt = FlatSGD(m, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        for x, t in data:
+            opt.zero_grad()
+            loss = F.cross_entropy(m(x.permute(0, 2, 3, 1).contiguous()), t)
+            loss.backward()
+            opt.step(m.finish())
+        sd = ours.state_dict()
+        nb = m.num_buckets()
+    else:
+        m = TorchDDP(ref)
+        opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        for x, t in data:
+            opt.zero_grad()
+            F.cross_entropy(m(x), t).backward()
+            opt.step()
+        sd = ref.state_dict()
+        nb = 0
+    torch.save({"sd": sd, "nb": nb}, os.path.join(outdir, f"gddp_{impl}_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
