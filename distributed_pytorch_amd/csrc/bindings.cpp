@@ -19,34 +19,34 @@ int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int 
                    int R, int S, int stride, int pad, int splits, int tile, int posmajor, hipStream_t st);
 int dpa_wflip(const float* w, float* wd, int K, int R, int S, int C, hipStream_t st);
 long dpa_bn_part_floats(int M, int C, int bwd);
-int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M, int C, const float* gamma,
+int dpa_bn_fwd_stats(const void* src, int nsplit, void* z, float* part, int M, int C, const float* gamma,
                      const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
-                     float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st);
+                     float* invstd, float* scale, float* shift, float momentum, float eps, int zbf, hipStream_t st);
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
                        const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st);
-int dpa_bn_apply(const float* z, float* a, unsigned short* a3, int np, const float* scale, const float* shift, int N,
-                 int H, int W, int C, int pool, int act, const float* res, hipStream_t st);
-int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
+int dpa_bn_apply(const void* z, float* a, unsigned short* a3, int np, const float* scale, const float* shift, int N,
+                 int H, int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st);
+int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
-               int pool, int act, const float* res, float* dres, hipStream_t st);
+               int pool, int act, const void* res, void* dres, int zbf, hipStream_t st);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st);
 int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                    int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st);
 int dpa_x3_splits(int Kred, int splits);
-int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w, long wps, float* out, float* slab,
+int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w, long wps, void* out, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
-                      int reduce, int posmajor, int np, hipStream_t st);
+                      int reduce, int posmajor, int np, int obf, hipStream_t st);
 int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* dz, long dzps, float* dw, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
                       int posmajor, int np, hipStream_t st);
 int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
 int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
-int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, float* dx, float* slab,
+int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
                       int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
-                      int tile, int reduce, int posmajor, int np, hipStream_t st);
+                      int tile, int reduce, int posmajor, int np, int obf, hipStream_t st);
 int dpa_augment(const unsigned char* img, const long long* idx, const long long* labels, float* out,
                 long long* target, int B, int Hs, int Ws, int pad, int train, unsigned long long seed,
                 unsigned long long salt, const float* mean, const float* std, hipStream_t st);
@@ -195,14 +195,28 @@ void need_planes(const Tensor& t, const char* name) {
 
 int64_t x3_splits(int64_t Kred, int64_t splits) { return dpa_x3_splits((int)Kred, (int)splits); }
 
-// x3 [NP,N,H,W,C], w3 [NP,K,R,S,C], out [N,P,Q,K] fp32
+// fp32 conv output, or bf16 (one-plane convs only: the generic bf16-activation path)
+void* conv_out_ptr(const Tensor& out, int np, const char* name, int& obf) {
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous(), name, " must be a contiguous GPU tensor");
+  if (out.scalar_type() == at::kBFloat16) {
+    TORCH_CHECK(np == 1, name, ": bf16 output needs bf16 (1-plane) operands");
+    obf = 1;
+  } else {
+    TORCH_CHECK(out.scalar_type() == at::kFloat, name, " must be float32 or bfloat16");
+    obf = 0;
+  }
+  return out.data_ptr();
+}
+
+// x3 [NP,N,H,W,C], w3 [NP,K,R,S,C], out [N,P,Q,K] fp32 (or bf16 when NP == 1)
 void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits,
                    int64_t tile, bool reduce, bool posmajor) {
   need_planes(x3, "x3");
   need_planes(w3, "w3");
-  need(out, "out");
   const int np = x3.size(0);
   TORCH_CHECK(w3.size(0) == np, "plane count mismatch");
+  int obf = 0;
+  void* op = conv_out_ptr(out, np, "out", obf);
   const int N = x3.size(1), H = x3.size(2), W = x3.size(3), C = x3.size(4);
   const int K = w3.size(1), R = w3.size(2), S = w3.size(3);
   TORCH_CHECK(w3.size(4) == C, "conv_x3_fprop: channel mismatch");
@@ -216,8 +230,8 @@ void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, 
     TORCH_CHECK(slab->numel() >= (int64_t)eff * N * P * Q * K, "conv_x3_fprop: slab too small");
     sl = fp(*slab);
   }
-  chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), fp(out), sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, cur_stream()),
+  chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), op, sl, N, H, W, C, K, R, S, (int)stride,
+                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf, cur_stream()),
       "conv_x3_fprop");
 }
 
@@ -253,9 +267,10 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
                    int64_t tile, bool reduce, bool posmajor) {
   need_planes(dz3, "dz3");
   need_planes(w3, "w3");
-  need(dx, "dx");
   const int np = dz3.size(0);
   TORCH_CHECK(w3.size(0) == np, "plane count mismatch");
+  int obf = 0;
+  void* op = conv_out_ptr(dx, np, "dx", obf);
   const int N = dz3.size(1), Hd = dz3.size(2), Wd = dz3.size(3), K = dz3.size(4);
   const int R = w3.size(2), S = w3.size(3), C = w3.size(4);
   TORCH_CHECK(w3.size(1) == K, "conv_x3_dgrad: weight K mismatch");
@@ -271,8 +286,9 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
     TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * C, "conv_x3_dgrad: slab too small");
     sl = fp(*slab);
   }
-  chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), fp(dx), sl, N, Hd, Wd, K, C, R, S, (int)stride,
-                        (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, cur_stream()),
+  chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), op, sl, N, Hd, Wd, K, C, R, S, (int)stride,
+                        (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf,
+                        cur_stream()),
       "conv_x3_dgrad");
 }
 
@@ -296,14 +312,22 @@ void split_planes(Tensor x, Tensor out) {
 
 
 // ---------------- batch norm ----------------
+// Activation-like BN operands (z, grads, residuals) are fp32 or bf16; all of one call share a dtype.
+void* act_ptr(const Tensor& t, const char* name, bool bf) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  TORCH_CHECK(t.scalar_type() == (bf ? at::kBFloat16 : at::kFloat), name, " must be ",
+              bf ? "bfloat16" : "float32", " like z");
+  return t.data_ptr();
+}
 int64_t bn_part_floats(int64_t M, int64_t C, bool bwd) { return dpa_bn_part_floats((int)M, (int)C, bwd ? 1 : 0); }
 
 // src: z [M][C], or nsplit slabs of it (then the summed z is written to z)
 void bn_fwd_stats(Tensor src, int64_t nsplit, Tensor z, Tensor part, Tensor gamma, Tensor beta, OptT bias, OptT rmean,
                   OptT rvar, OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum,
                   double eps) {
-  need(src, "src");
-  need(z, "z");
+  const bool bf = z.scalar_type() == at::kBFloat16;
+  void* zp = act_ptr(z, "z", bf);
+  const void* sp = act_ptr(src, "src", bf);
   need(part, "part");
   const int C = z.size(-1);
   const int M = z.numel() / C;
@@ -314,8 +338,8 @@ void bn_fwd_stats(Tensor src, int64_t nsplit, Tensor z, Tensor part, Tensor gamm
     need(*nbt, "nbt", at::kLong);
     nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
   }
-  chk(dpa_bn_fwd_stats(fp(src), (int)nsplit, fp(z), fp(part), M, C, fp(gamma), fp(beta), ofp(bias), ofp(rmean),
-                       ofp(rvar), nb, fp(mean), fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps,
+  chk(dpa_bn_fwd_stats(sp, (int)nsplit, zp, fp(part), M, C, fp(gamma), fp(beta), ofp(bias), ofp(rmean), ofp(rvar),
+                       nb, fp(mean), fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps, bf ? 1 : 0,
                        cur_stream()),
       "bn_fwd_stats");
 }
@@ -328,27 +352,35 @@ void bn_eval_params(Tensor gamma, Tensor beta, OptT bias, Tensor rmean, Tensor r
 }
 
 // a: fp32 [N,Ho,Wo,C] or bf16 planes [NP,N,Ho,Wo,C].  act: 0 relu, 1 none, 2 relu(. + res)
+// z (and res): fp32 or bf16 [N,H,W,C]; a: fp32 [N,Ho,Wo,C], bf16 [N,Ho,Wo,C] (one plane) or bf16
+// planes [NP,N,Ho,Wo,C]
 void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t act, OptT res) {
-  need(z, "z");
-  const float* rp = nullptr;
+  const bool bf = z.scalar_type() == at::kBFloat16;
+  const void* zp = act_ptr(z, "z", bf);
+  const void* rp = nullptr;
   if (act == 2) {
     TORCH_CHECK(res.has_value() && res->defined(), "bn_apply: act=2 needs the residual");
-    need(*res, "res");
     TORCH_CHECK(res->numel() == z.numel(), "bn_apply: residual shape");
-    rp = fp(*res);
+    rp = act_ptr(*res, "res", bf);
   }
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
   const int64_t outn = (int64_t)N * (pool ? (H / 2) * (W / 2) : H * W) * C;
   if (a.scalar_type() == at::kBFloat16) {
-    need_planes(a, "a3");
-    TORCH_CHECK(a.numel() == a.size(0) * outn, "bn_apply: a3 shape");
-    chk(dpa_bn_apply(fp(z), nullptr, up(a), a.size(0), fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp,
-                     cur_stream()),
+    int np = 1;
+    if (a.numel() != outn) {
+      need_planes(a, "a3");
+      TORCH_CHECK(a.numel() == a.size(0) * outn, "bn_apply: a3 shape");
+      np = a.size(0);
+    } else {
+      TORCH_CHECK(a.is_cuda() && a.is_contiguous(), "bn_apply: a must be contiguous");
+    }
+    chk(dpa_bn_apply(zp, nullptr, up(a), np, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp,
+                     bf ? 1 : 0, cur_stream()),
         "bn_apply");
   } else {
     need(a, "a");
     TORCH_CHECK(a.numel() == outn, "bn_apply: a shape");
-    chk(dpa_bn_apply(fp(z), fp(a), nullptr, 0, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp,
+    chk(dpa_bn_apply(zp, fp(a), nullptr, 0, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp, bf ? 1 : 0,
                      cur_stream()),
         "bn_apply");
   }
@@ -359,28 +391,32 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
             int64_t act, OptT res, OptT dres) {
-  need(gsrc, "gsrc");
-  const float* rp = nullptr;
-  float* drp = nullptr;
+  const bool bf = z.scalar_type() == at::kBFloat16;
+  const void* zp = act_ptr(z, "z", bf);
+  const void* gsp = act_ptr(gsrc, "gsrc", bf);
+  void* gp = act_ptr(g, "g", bf);
+  const void* rp = nullptr;
+  void* drp = nullptr;
   if (act == 2) {
     TORCH_CHECK(res.has_value() && res->defined() && dres.has_value() && dres->defined(),
                 "bn_bwd: act=2 needs res and dres");
-    need(*res, "res");
-    need(*dres, "dres");
     TORCH_CHECK(res->numel() == z.numel() && dres->numel() == z.numel(), "bn_bwd: residual shape");
-    rp = fp(*res);
-    drp = fp(*dres);
+    rp = act_ptr(*res, "res", bf);
+    drp = act_ptr(*dres, "dres", bf);
   }
-  need(g, "g");
-  need(z, "z");
   float* dzf = nullptr;
   u16* dz3 = nullptr;
   int np = 0;
   if (dz.scalar_type() == at::kBFloat16) {
-    need_planes(dz, "dz3");
-    TORCH_CHECK(dz.numel() == dz.size(0) * z.numel(), "bn_bwd: dz3 shape");
+    if (dz.numel() == z.numel()) {  // one plane, [N,H,W,C]
+      TORCH_CHECK(dz.is_cuda() && dz.is_contiguous(), "bn_bwd: dz must be contiguous");
+      np = 1;
+    } else {
+      need_planes(dz, "dz3");
+      TORCH_CHECK(dz.numel() == dz.size(0) * z.numel(), "bn_bwd: dz3 shape");
+      np = dz.size(0);
+    }
     dz3 = up(dz);
-    np = dz.size(0);
   } else {
     need(dz, "dz");
     dzf = fp(dz);
@@ -391,9 +427,9 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_bwd: gsrc too small");
   TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd: part too small");
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
-  chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
-                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 cur_stream()),
+  chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
+                 fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
+                 bf ? 1 : 0, cur_stream()),
       "bn_bwd");
 }
 

@@ -34,6 +34,18 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
+// element-4 accessors: activations / gradients are fp32 (VGG engine, x3) or bf16 (generic bf16
+// path: z, g, residual and their gradients stored in bf16, math in fp32)
+__device__ __forceinline__ float4 ld4(const float* p, long i4) { return reinterpret_cast<const float4*>(p)[i4]; }
+__device__ __forceinline__ float4 ld4(const u16* p, long i4) {
+  const ushort4 h = reinterpret_cast<const ushort4*>(p)[i4];
+  return make_float4(bf16_f(h.x), bf16_f(h.y), bf16_f(h.z), bf16_f(h.w));
+}
+__device__ __forceinline__ void st4(float* p, long i4, float4 v) { reinterpret_cast<float4*>(p)[i4] = v; }
+__device__ __forceinline__ void st4(u16* p, long i4, float4 v) {
+  reinterpret_cast<ushort4*>(p)[i4] = make_ushort4(bf16_rne(v.x), bf16_rne(v.y), bf16_rne(v.z), bf16_rne(v.w));
+}
+
 struct RedGeom {
   int C4, TPR, RPI, CG;  // float4 lanes per row, threads per row, rows per iteration, channel groups/thread
 };
@@ -102,8 +114,9 @@ __device__ __forceinline__ void store4(float* f, u16* pl, long ps, long i4, floa
 // ---- forward statistics: per (row-block, channel) (mean, M2) via sums shifted by the block's
 // first row.  If nsplit > 1, src holds nsplit slabs of [M][C] that are summed here and written
 // to z (the split-K reduction of the producing conv, fused).
-__global__ __launch_bounds__(RT) void bn_stats_kernel(const float* __restrict__ src, float* __restrict__ z,
-                                                      int nsplit, float2* __restrict__ part, int M, int C, int rpb) {
+template <typename TZ>
+__global__ __launch_bounds__(RT) void bn_stats_kernel(const TZ* __restrict__ src, TZ* __restrict__ z, int nsplit,
+                                                      float2* __restrict__ part, int M, int C, int rpb) {
   const RedGeom g = red_geom(C);
   const int t = threadIdx.x;
   const int lane_c = t % g.TPR, lane_r = t / g.TPR;
@@ -111,7 +124,6 @@ __global__ __launch_bounds__(RT) void bn_stats_kernel(const float* __restrict__ 
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(M, r0 + rpb);
   const long slab4 = (long)M * g.C4;
-  const float4* s4 = reinterpret_cast<const float4*>(src);
   __shared__ float4 sh[2][RT];
   auto acc = [](float4 v, float4 K, float4& a1, float4& a2) {
     const float d0 = v.x - K.x, d1 = v.y - K.y, d2 = v.z - K.z, d3 = v.w - K.w;
@@ -130,23 +142,23 @@ __global__ __launch_bounds__(RT) void bn_stats_kernel(const float* __restrict__ 
     float4 K = make_float4(0.f, 0.f, 0.f, 0.f), a1 = K, a2 = K;
     if (cval) {
       // shift = the block's first row (summed over splits)
-      K = s4[(long)r0 * g.C4 + c4];
-      for (int s = 1; s < nsplit; ++s) K = f4add(K, s4[s * slab4 + (long)r0 * g.C4 + c4]);
+      K = ld4(src, (long)r0 * g.C4 + c4);
+      for (int s = 1; s < nsplit; ++s) K = f4add(K, ld4(src, s * slab4 + (long)r0 * g.C4 + c4));
       int r = r0 + lane_r;
       if (nsplit == 1) {  // 4 rows' loads in flight
         for (; r + 3 * g.RPI < r1; r += 4 * g.RPI) {
           float4 v[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] = s4[(long)(r + u * g.RPI) * g.C4 + c4];
+          for (int u = 0; u < 4; ++u) v[u] = ld4(src, (long)(r + u * g.RPI) * g.C4 + c4);
 #pragma unroll
           for (int u = 0; u < 4; ++u) acc(v[u], K, a1, a2);
         }
       }
       for (; r < r1; r += g.RPI) {
         const long i = (long)r * g.C4 + c4;
-        float4 v = s4[i];
-        for (int s = 1; s < nsplit; ++s) v = f4add(v, s4[s * slab4 + i]);
-        if (nsplit > 1) reinterpret_cast<float4*>(z)[i] = v;
+        float4 v = ld4(src, i);
+        for (int s = 1; s < nsplit; ++s) v = f4add(v, ld4(src, s * slab4 + i));
+        if (nsplit > 1) st4(z, i, v);
         acc(v, K, a1, a2);
       }
     }
@@ -260,30 +272,29 @@ __device__ __forceinline__ float4 affine_relu(float4 v, float4 sc, float4 sh) {
 
 // a = act(z*scale + shift [+ res]), optionally 2x2/s2 max-pooled (ACT 0 only).
 // z: [N,H,W,C]  a: [N,H/2,W/2,C] or [N,H,W,C]
-template <bool POOL, int NP, int ACT>
-__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, float* __restrict__ a,
+template <bool POOL, int NP, int ACT, typename TZ>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z, float* __restrict__ a,
                                                        u16* __restrict__ a3, long ps,
                                                        const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, const float* __restrict__ res,
+                                                       const float* __restrict__ shift, const TZ* __restrict__ res,
                                                        int N, int H, int W, int C) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
   const long stride = (long)gridDim.x * blockDim.x;
-  const float4* z4 = reinterpret_cast<const float4*>(z);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int c4 = (int)(i % C4);
     const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
     const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
     if (!POOL) {
       if constexpr (ACT == 0) {
-        store4<NP>(a, a3, ps, i, affine_relu(z4[i], sc, sh));
+        store4<NP>(a, a3, ps, i, affine_relu(ld4(z, i), sc, sh));
       } else {
-        const float4 v = z4[i];
+        const float4 v = ld4(z, i);
         float4 u = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
                                fmaf(v.w, sc.w, sh.w));
         if constexpr (ACT == 2) {
-          const float4 r = reinterpret_cast<const float4*>(res)[i];
+          const float4 r = ld4(res, i);
           u = make_float4(fmaxf(u.x + r.x, 0.f), fmaxf(u.y + r.y, 0.f), fmaxf(u.z + r.z, 0.f), fmaxf(u.w + r.w, 0.f));
         }
         store4<NP>(a, a3, ps, i, u);
@@ -295,10 +306,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
       const int oh = (int)(t % Ho);
       const int n = (int)(t / Ho);
       const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * C4 + c4;
-      const float4 v00 = affine_relu(z4[base], sc, sh);
-      const float4 v01 = affine_relu(z4[base + C4], sc, sh);
-      const float4 v10 = affine_relu(z4[base + (long)W * C4], sc, sh);
-      const float4 v11 = affine_relu(z4[base + (long)W * C4 + C4], sc, sh);
+      const float4 v00 = affine_relu(ld4(z, base), sc, sh);
+      const float4 v01 = affine_relu(ld4(z, base + C4), sc, sh);
+      const float4 v10 = affine_relu(ld4(z, base + (long)W * C4), sc, sh);
+      const float4 v11 = affine_relu(ld4(z, base + (long)W * C4 + C4), sc, sh);
       store4<NP>(a, a3, ps, i,
                  make_float4(fmaxf(fmaxf(v00.x, v01.x), fmaxf(v10.x, v11.x)),
                              fmaxf(fmaxf(v00.y, v01.y), fmaxf(v10.y, v11.y)),
@@ -335,10 +346,10 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat.  Rows are OUTPUT rows of
 // the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
 // the summed g is written to gout (consumed by the apply pass).  part layout: [block][3][C]
-template <bool POOL, int ACT>
-__global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restrict__ gsrc, float* __restrict__ gout,
-                                                            int nsplit, const float* __restrict__ z,
-                                                            const float* __restrict__ res,
+template <bool POOL, int ACT, typename TZ>
+__global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
+                                                            int nsplit, const TZ* __restrict__ z,
+                                                            const TZ* __restrict__ res,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
@@ -354,8 +365,6 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restri
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(Mo, r0 + rpb);
   const long slab4 = (long)Mo * gg.C4;
-  const float4* z4 = reinterpret_cast<const float4*>(z);
-  const float4* g4 = reinterpret_cast<const float4*>(gsrc);
   __shared__ float4 sh[3][RT];
   for (int cg = 0; cg < gg.CG; ++cg) {
     const int c4 = lane_c + cg * gg.TPR;
@@ -368,12 +377,12 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restri
       const float4 is = reinterpret_cast<const float4*>(invstd)[c4];
       for (int r = r0 + lane_r; r < r1; r += gg.RPI) {
         const long gi = (long)r * gg.C4 + c4;
-        float4 gv = g4[gi];
-        for (int s = 1; s < nsplit; ++s) gv = f4add(gv, g4[s * slab4 + gi]);
-        if (nsplit > 1) reinterpret_cast<float4*>(gout)[gi] = gv;
+        float4 gv = ld4(gsrc, gi);
+        for (int s = 1; s < nsplit; ++s) gv = f4add(gv, ld4(gsrc, s * slab4 + gi));
+        if (nsplit > 1) st4(gout, gi, gv);
         if (!POOL) {
-          const float4 zv = z4[gi];
-          const float4 rv = ACT == 2 ? reinterpret_cast<const float4*>(res)[gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 zv = ld4(z, gi);
+          const float4 rv = ACT == 2 ? ld4(res, gi) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float zz = F4GET(zv, k);
@@ -389,8 +398,8 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const float* __restri
           const int oh = tt % Ho;
           const int n = tt / Ho;
           const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * gg.C4 + c4;
-          const float4 z00 = z4[base], z01 = z4[base + gg.C4], z10 = z4[base + (long)W * gg.C4],
-                       z11 = z4[base + (long)W * gg.C4 + gg.C4];
+          const float4 z00 = ld4(z, base), z01 = ld4(z, base + gg.C4), z10 = ld4(z, base + (long)W * gg.C4),
+                       z11 = ld4(z, base + (long)W * gg.C4 + gg.C4);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             float d00, d01, d10, d11;
@@ -486,20 +495,18 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-template <bool POOL, int NP, int ACT>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ z,
+template <bool POOL, int NP, int ACT, typename TZ>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict__ g, const TZ* __restrict__ z,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ coef, float* __restrict__ dz,
                                                            u16* __restrict__ dz3, long ps,
-                                                           const float* __restrict__ res, float* __restrict__ dres,
+                                                           const TZ* __restrict__ res, TZ* __restrict__ dres,
                                                            int N, int H, int W, int C) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
   const long stride = (long)gridDim.x * blockDim.x;
-  const float4* z4 = reinterpret_cast<const float4*>(z);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int c4 = (int)(i % C4);
     const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
@@ -507,10 +514,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     const float4 k1 = reinterpret_cast<const float4*>(coef)[c4];
     const float4 k2 = reinterpret_cast<const float4*>(coef + C)[c4];
     const float4 k3 = reinterpret_cast<const float4*>(coef + 2 * C)[c4];
-    const float4 gv = g4[i];
+    const float4 gv = ld4(g, i);
     if (!POOL) {
-      const float4 zv = z4[i];
-      const float4 rv = ACT == 2 ? reinterpret_cast<const float4*>(res)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 zv = ld4(z, i);
+      const float4 rv = ACT == 2 ? ld4(res, i) : make_float4(0.f, 0.f, 0.f, 0.f);
       float r[4], dyv[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -520,7 +527,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         r[k] = F4GET(k1, k) * dy + F4GET(k2, k) * zz + F4GET(k3, k);
       }
       store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]));
-      if constexpr (ACT == 2) reinterpret_cast<float4*>(dres)[i] = make_float4(dyv[0], dyv[1], dyv[2], dyv[3]);
+      if constexpr (ACT == 2) st4(dres, i, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
     } else {
       long t = i / C4;
       const int ow = (int)(t % Wo);
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       const long idx[4] = {base, base + C4, base + (long)W * C4, base + (long)W * C4 + C4};
       float4 zq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) zq[q] = z4[idx[q]];
+      for (int q = 0; q < 4; ++q) zq[q] = ld4(z, idx[q]);
       float out[4][4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -553,10 +560,115 @@ int grid_1d(long n) {
   return (int)(g < 1 ? 1 : g);
 }
 
+
+// ---------------- host launchers (TZ = float: fp32 activations; u16: bf16 activations) ----------------
+template <typename TZ>
+int bn_fwd_stats_host(const TZ* src, int nsplit, TZ* z, float* part, int M, int C, const float* gamma,
+                      const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
+                      float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st) {
+  const int rpb = red_rows_per_block(M, C);
+  const int nblk = (M + rpb - 1) / rpb;
+  bn_stats_kernel<TZ><<<nblk, RT, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C,
+                                           rpb);
+  bn_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
+                                                  bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
+  return (int)hipGetLastError();
+}
+
+template <bool POOL, int NP, typename TZ>
+void bn_apply_launch(int act, int grid, hipStream_t st, const TZ* z, float* a, u16* a3, long ps, const float* scale,
+                     const float* shift, const TZ* res, int N, int H, int W, int C) {
+  if constexpr (POOL) {
+    bn_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+  } else {
+    if (act == 0)
+      bn_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+    else if (act == 1)
+      bn_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+    else
+      bn_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+  }
+}
+
+template <typename TZ>
+int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H, int W,
+                  int C, int pool, int act, const TZ* res, hipStream_t st) {
+  const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
+  const long ps = total * 4;
+  const int grid = grid_1d(total);
+  if (pool) {
+    if (np == 0) bn_apply_launch<true, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+    else if (np == 1) bn_apply_launch<true, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+    else bn_apply_launch<true, 3, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+  } else {
+    if (np == 0) bn_apply_launch<false, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+    else if (np == 1) bn_apply_launch<false, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+    else bn_apply_launch<false, 3, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+  }
+  return (int)hipGetLastError();
+}
+
+template <bool POOL, int NP, typename TZ>
+void bn_bwd_apply_launch(int act, int grid, hipStream_t st, const TZ* g, const TZ* z, const float* scale,
+                         const float* shift, const float* coef, float* dz, u16* dz3, long ps, const TZ* res, TZ* dres,
+                         int N, int H, int W, int C) {
+  if constexpr (POOL) {
+    bn_bwd_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H,
+                                                                W, C);
+  } else {
+    if (act == 0)
+      bn_bwd_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
+                                                                   H, W, C);
+    else if (act == 1)
+      bn_bwd_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
+                                                                   H, W, C);
+    else
+      bn_bwd_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
+                                                                   H, W, C);
+  }
+}
+
+template <typename TZ>
+int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
+                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
+                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
+                const TZ* res, TZ* dres, hipStream_t st) {
+  if (nsplit < 1) nsplit = 1;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const int Mo = N * Ho * Wo;
+  const int rpb = red_rows_per_block(Mo, C);
+  const int nblk = (Mo + rpb - 1) / rpb;
+#define RED(P, A) \
+  bn_bwd_reduce_kernel<P, A, TZ><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N, H, \
+                                                      W, C, rpb)
+  if (pool) RED(true, 0);
+  else if (act == 0) RED(false, 0);
+  else if (act == 1) RED(false, 1);
+  else RED(false, 2);
+#undef RED
+  bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
+                                                      dbeta, dbias, coef);
+  const TZ* gg = nsplit > 1 ? g : gsrc;
+  const long total = (long)Mo * (C / 4);
+  const long ps = (long)N * H * W * C;
+  const int grid = grid_1d(total);
+#define BAP(P, NPT) bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C)
+  if (pool) {
+    if (np == 0) BAP(true, 0);
+    else if (np == 1) BAP(true, 1);
+    else BAP(true, 3);
+  } else {
+    if (np == 0) BAP(false, 0);
+    else if (np == 1) BAP(false, 1);
+    else BAP(false, 3);
+  }
+#undef BAP
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
-
 // floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (3 per ...)
 long dpa_bn_part_floats(int M, int C, int bwd) {
   const int rpb = red_rows_per_block(M, C);
@@ -564,17 +676,17 @@ long dpa_bn_part_floats(int M, int C, int bwd) {
   return nblk * C * (bwd ? 3 : 2);
 }
 
-// z [M][C] (or nsplit slabs of it in src; then z is written) -> partials -> finalize
-int dpa_bn_fwd_stats(const float* src, int nsplit, float* z, float* part, int M, int C, const float* gamma,
+// z [M][C] (or nsplit fp32 slabs of it in src; then z is written) -> partials -> finalize.
+// zbf: z/src are bf16 (nsplit must be 1).
+int dpa_bn_fwd_stats(const void* src, int nsplit, void* z, float* part, int M, int C, const float* gamma,
                      const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
-                     float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st) {
-  if (C % 4) return -2;
-  const int rpb = red_rows_per_block(M, C);
-  const int nblk = (M + rpb - 1) / rpb;
-  bn_stats_kernel<<<nblk, RT, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C, rpb);
-  bn_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
-                                                  bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
-  return (int)hipGetLastError();
+                     float* invstd, float* scale, float* shift, float momentum, float eps, int zbf, hipStream_t st) {
+  if (C % 4 || (zbf && nsplit > 1)) return -2;
+  if (zbf)
+    return bn_fwd_stats_host<u16>((const u16*)src, nsplit, (u16*)z, part, M, C, gamma, beta, bias, rmean, rvar, nbt,
+                                  mean, invstd, scale, shift, momentum, eps, st);
+  return bn_fwd_stats_host<float>((const float*)src, nsplit, (float*)z, part, M, C, gamma, beta, bias, rmean, rvar,
+                                  nbt, mean, invstd, scale, shift, momentum, eps, st);
 }
 
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
@@ -583,84 +695,32 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
   return (int)hipGetLastError();
 }
 
-#define BN_DISPATCH_NP(NPV, POOLV, LAUNCH) \
-  do {                                      \
-    if (NPV == 0) {                         \
-      if (POOLV) LAUNCH(true, 0); else LAUNCH(false, 0); \
-    } else if (NPV == 1) {                  \
-      if (POOLV) LAUNCH(true, 1); else LAUNCH(false, 1); \
-    } else {                                \
-      if (POOLV) LAUNCH(true, 3); else LAUNCH(false, 3); \
-    }                                       \
-  } while (0)
-
 // out: fp32 a (np == 0) or bf16 planes a3 [np][...] (np in {1, 3}).  act: 0 relu (pool allowed),
-// 1 none, 2 relu(. + res)
-int dpa_bn_apply(const float* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
-                 int W, int C, int pool, int act, const float* res, hipStream_t st) {
+// 1 none, 2 relu(. + res).  zbf: z and res are bf16.
+int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
+                 int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && !res)) return -2;
-  const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
-  const long ps = total * 4;
-  const int grid = grid_1d(total);
-#define L_APPLY(P, NPT)                                                                                           \
-  do {                                                                                                            \
-    if (act == 0)                                                                                                 \
-      bn_apply_kernel<P, NPT, 0><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);              \
-    else if (!(P) && act == 1)                                                                                    \
-      bn_apply_kernel<false, NPT, 1><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);          \
-    else if (!(P))                                                                                                \
-      bn_apply_kernel<false, NPT, 2><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);          \
-  } while (0)
-  BN_DISPATCH_NP(np, pool, L_APPLY);
-#undef L_APPLY
-  return (int)hipGetLastError();
+  if (zbf)
+    return bn_apply_host<u16>((const u16*)z, a, a3, np, scale, shift, N, H, W, C, pool, act, (const u16*)res, st);
+  return bn_apply_host<float>((const float*)z, a, a3, np, scale, shift, N, H, W, C, pool, act, (const float*)res, st);
 }
 
-// gsrc: grad of the layer output (pooled shape if pool), or nsplit slabs of it (then the sum is
-// written to g).  Writes dz [N,H,W,C] and dgamma/dbeta/dbias.
-int dpa_bn_bwd(const float* gsrc, int nsplit, float* g, const float* z, const float* scale, const float* shift,
+// gsrc: grad of the layer output (pooled shape if pool), or nsplit fp32 slabs of it (then the sum is
+// written to g).  Writes dz [N,H,W,C] (fp32, or bf16 planes dz3) and dgamma/dbeta/dbias; act 2 also
+// the residual gradient dres.  zbf: gsrc/g/z/res/dres are bf16 (nsplit must be 1).
+int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-               const float* res, float* dres, hipStream_t st) {
+               const void* res, void* dres, int zbf, hipStream_t st) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && (!res || !dres))) return -2;
-  if (nsplit < 1) nsplit = 1;
-  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
-  const int Mo = N * Ho * Wo;
-  const int rpb = red_rows_per_block(Mo, C);
-  const int nblk = (Mo + rpb - 1) / rpb;
-  if (pool)
-    bn_bwd_reduce_kernel<true, 0><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N, H,
-                                                        W, C, rpb);
-  else if (act == 0)
-    bn_bwd_reduce_kernel<false, 0><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N,
-                                                         H, W, C, rpb);
-  else if (act == 1)
-    bn_bwd_reduce_kernel<false, 1><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N,
-                                                         H, W, C, rpb);
-  else
-    bn_bwd_reduce_kernel<false, 2><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N,
-                                                         H, W, C, rpb);
-  bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
-                                                      dbeta, dbias, coef);
-  const float* gg = nsplit > 1 ? g : gsrc;
-  const long total = (long)Mo * (C / 4);
-  const long ps = (long)N * H * W * C;
-  const int grid = grid_1d(total);
-#define L_BAPPLY(P, NPT)                                                                                           \
-  do {                                                                                                             \
-    if (act == 0)                                                                                                  \
-      bn_bwd_apply_kernel<P, NPT, 0><<<grid, 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, \
-                                                            W, C);                                                 \
-    else if (!(P) && act == 1)                                                                                     \
-      bn_bwd_apply_kernel<false, NPT, 1><<<grid, 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, \
-                                                                H, W, C);                                          \
-    else if (!(P))                                                                                                 \
-      bn_bwd_apply_kernel<false, NPT, 2><<<grid, 256, 0, st>>>(gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, \
-                                                                H, W, C);                                          \
-  } while (0)
-  BN_DISPATCH_NP(np, pool, L_BAPPLY);
-#undef L_BAPPLY
-  return (int)hipGetLastError();
+  if (zbf && nsplit > 1) return -2;
+  if (zbf)
+    return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
+                            coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
+                            (u16*)dres, st);
+  return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
+                            part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
+                            (float*)dres, st);
 }
 
 }  // extern "C"

@@ -64,9 +64,13 @@ __device__ __forceinline__ void split_val(float v, u16* o) {
 // Block = 64 float4 columns x G split lanes: lane g sums splits g, g+G, ... and the G partials are
 // combined in LDS in a fixed order.  G > 1 gives small outputs with many splits (e.g. first-layer
 // weight gradients: 1152 float4 x 512 splits) enough parallel loads to stream at HBM rate.
-template <int G>
+__device__ __forceinline__ void st_out4(float4* o, long i, float4 v) { o[i] = v; }
+__device__ __forceinline__ void st_out4(ushort4* o, long i, float4 v) {
+  o[i] = make_ushort4(bf16_rne(v.x), bf16_rne(v.y), bf16_rne(v.z), bf16_rne(v.w));
+}
+template <int G, typename TO>
 __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __restrict__ slabs,
-                                                               float4* __restrict__ out, long n4, int splits) {
+                                                               TO* __restrict__ out, long n4, int splits) {
   __shared__ float4 part[G > 1 ? G : 1][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const long i = (long)blockIdx.x * 64 + c;
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __r
     }
   }
   if constexpr (G == 1) {
-    if (i < n4) out[i] = s;
+    if (i < n4) st_out4(out, i, s);
   } else {
     part[g][c] = s;
     __syncthreads();
@@ -94,20 +98,25 @@ __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __r
         s.z += part[j][c].z;
         s.w += part[j][c].w;
       }
-      out[i] = s;
+      st_out4(out, i, s);
     }
   }
 }
 
-inline int launch_splitk_reduce(const float* slabs, float* out, long n4, int splits, hipStream_t st) {
+// out: float4 (fp32) or ushort4 (bf16, round-to-nearest-even)
+template <typename TO>
+inline int launch_splitk_reduce_t(const float* slabs, TO* o4, long n4, int splits, hipStream_t st) {
   const long blocks = (n4 + 63) / 64;
   const float4* in4 = reinterpret_cast<const float4*>(slabs);
-  float4* o4 = reinterpret_cast<float4*>(out);
   if (splits >= 16 && blocks < 4096)
-    splitk_reduce_kernel<16><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits);
+    splitk_reduce_kernel<16, TO><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits);
   else if (splits >= 4 && blocks < 16384)
-    splitk_reduce_kernel<4><<<blocks, 256, 0, st>>>(in4, o4, n4, splits);
+    splitk_reduce_kernel<4, TO><<<blocks, 256, 0, st>>>(in4, o4, n4, splits);
   else
-    splitk_reduce_kernel<1><<<blocks, 64, 0, st>>>(in4, o4, n4, splits);
+    splitk_reduce_kernel<1, TO><<<blocks, 64, 0, st>>>(in4, o4, n4, splits);
   return (int)hipGetLastError();
 }
+inline int launch_splitk_reduce(const float* slabs, float* out, long n4, int splits, hipStream_t st) {
+  return launch_splitk_reduce_t(slabs, reinterpret_cast<float4*>(out), n4, splits, st);
+}
+

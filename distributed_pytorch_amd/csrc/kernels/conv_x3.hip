@@ -65,6 +65,7 @@ struct Args {
   const u16* w;     // FPROP: weight planes [Nout][R][S][C]; WGRAD: dZ planes [N,P,Q,Kout]
   long wps;
   float* out;       // FPROP: NHWC [N,P,Q,Nout] or slabs; WGRAD: dW [Kout][R*S*C] or slabs
+  u16* outb;        // bf16 output (OB kernels, single split): FPROP/DGRAD NHWC
   long slab;
   int N, H, W, C, P, Q, R, S, stride, pad;
   int M, Nout, Ktot;
@@ -103,7 +104,8 @@ enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
 // the 256-B bank row: conflict-free transpose reads).
 // NSTAGE: 2 = double-buffered LDS (one barrier per k step); 1 = single LDS stage + register
 // prefetch (two barriers per step, half the LDS -> more resident blocks to hide load latency).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK, int NSTAGE>
+// OB: epilogue stores bf16 (round-to-nearest-even) to a.outb instead of fp32 (bf16 activations).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK, int NSTAGE, bool OB = false>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
   constexpr bool WG = MODE == XM_WGRAD;
   constexpr bool DG = MODE == XM_DGRAD;
@@ -433,7 +435,10 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
               const unsigned pos = fdiv((unsigned)row, a.fd_N);
               mrow = (long)(row - (int)pos * a.N) * PQ + pos;
             }
-            out[mrow * ldc + col] = acc[i][j][r];
+            if constexpr (OB)
+              a.outb[mrow * ldc + col] = bf16_rne(acc[i][j][r]);
+            else
+              out[mrow * ldc + col] = acc[i][j][r];
           }
         }
       }
@@ -484,28 +489,35 @@ __global__ __launch_bounds__(256) void pad_split_kernel(const float* __restrict_
   }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK, int NS>
+template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK, int NS, bool OB>
 int launch_x3(const Args& a, hipStream_t st) {
   dim3 grid(a.gm * a.gn, a.splits);
-  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS><<<grid, WM * WN * 64, 0, st>>>(a);
+  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS, OB><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 
 // tile id -> (block tile, stage depth, LDS stages):
 //   0: 128x128/k32/2  1: 64x64/k32/2  2: 128x128/k16/2  3: 64x64/k64/2
 //   4: 128x128/k16/1  5: 128x128/k32/1  6: 64x64/k32/1  7: 256x128/k32/1 (8 waves)
-template <int MODE, int NP>
+template <int MODE, int NP, bool OB = false>
 int launch_tile(const Args& a, int tile, hipStream_t st) {
   switch (tile) {
-    case 7: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 1>(a, st);
-    case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 2>(a, st);
-    case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 2>(a, st);
-    case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 2>(a, st);
-    case 3: return launch_x3<64, 64, 1, 2, MODE, NP, 64, 2>(a, st);
-    case 4: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 1>(a, st);
-    case 5: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 1>(a, st);
-    default: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 1>(a, st);
+    case 7: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 1, OB>(a, st);
+    case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 2, OB>(a, st);
+    case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 2, OB>(a, st);
+    case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 2, OB>(a, st);
+    case 3: return launch_x3<64, 64, 1, 2, MODE, NP, 64, 2, OB>(a, st);
+    case 4: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 1, OB>(a, st);
+    case 5: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 1, OB>(a, st);
+    default: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 1, OB>(a, st);
   }
+}
+
+// fp32 output, or bf16 output (np == 1 only) for the generic bf16-activation path
+template <int MODE>
+int launch_any(const Args& a, int tile, int np, int obf, hipStream_t st) {
+  if (obf) return launch_tile<MODE, 1, true>(a, tile, st);
+  return np == 3 ? launch_tile<MODE, 3>(a, tile, st) : launch_tile<MODE, 1>(a, tile, st);
 }
 int tile_rows(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : (tile == 7 ? 256 : 128); }
 int tile_cols(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : 128; }
@@ -552,9 +564,9 @@ int dpa_x3_splits(int Kred, int splits) { return xsplits(Kred, splits); }
 // x planes [NP][N,H,W,C] (plane stride xps), w planes [NP][Kout][R][S][C] (stride wps; for a data
 // gradient pass the flipped/transposed Wd planes), out fp32 [N,P,Q,Kout] (or slabs, see
 // conv_gemm.hip).  np: 1 (bf16) or 3 (fp32 via bf16x6).  tile: 0 = 128x128, 1 = 64x64.
-int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out, float* slab, int N, int H, int W,
+int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
-                      int posmajor, int np, hipStream_t st) {
+                      int posmajor, int np, int obf, hipStream_t st) {
   Args a{};
   a.x = x;
   a.xps = xps;
@@ -567,13 +579,16 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out
   a.gn = cdiv(Kout, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor ? 1 : 0;
-  a.out = a.splits > 1 ? slab : out;
+  if (obf && (np != 1 || (a.splits > 1 && !reduce))) return -4;
+  a.out = a.splits > 1 ? slab : (float*)out;
+  a.outb = (u16*)out;
   a.slab = a.splits > 1 ? (long)a.M * Kout : 0;
-  const int rc = np == 3 ? launch_tile<XM_FPROP, 3>(a, tile, st) : launch_tile<XM_FPROP, 1>(a, tile, st);
+  const int rc = launch_any<XM_FPROP>(a, tile, np, obf && a.splits == 1, st);
   if (rc) return rc;
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * Kout / 4;
-    return launch_splitk_reduce(slab, out, n4, a.splits, st);
+    if (obf) return launch_splitk_reduce_t(slab, (ushort4*)out, n4, a.splits, st);
+    return launch_splitk_reduce(slab, (float*)out, n4, a.splits, st);
   }
   return 0;
 }
@@ -581,9 +596,9 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, float* out
 // Data gradient of conv(x [N,H,W,C], w [K,R,S,C], stride, pad) -> dZ [N,Hd,Wd,K]:
 // dx [N,H,W,C] fp32 (or slabs) from dz planes [NP][N,Hd,Wd,K] and the forward weight planes.
 // stride must be a power of two.
-int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, float* dx, float* slab, int N, int Hd, int Wd,
+int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx, float* slab, int N, int Hd, int Wd,
                       int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
-                      int posmajor, int np, hipStream_t st) {
+                      int posmajor, int np, int obf, hipStream_t st) {
   Args a{};
   a.x = dz;
   a.xps = dzps;
@@ -604,13 +619,16 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, float* d
   a.gn = cdiv(C, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor ? 1 : 0;
-  a.out = a.splits > 1 ? slab : dx;
+  if (obf && (np != 1 || (a.splits > 1 && !reduce))) return -4;
+  a.out = a.splits > 1 ? slab : (float*)dx;
+  a.outb = (u16*)dx;
   a.slab = a.splits > 1 ? (long)a.M * C : 0;
-  const int rc = np == 3 ? launch_tile<XM_DGRAD, 3>(a, tile, st) : launch_tile<XM_DGRAD, 1>(a, tile, st);
+  const int rc = launch_any<XM_DGRAD>(a, tile, np, obf && a.splits == 1, st);
   if (rc) return rc;
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * C / 4;
-    return launch_splitk_reduce(slab, dx, n4, a.splits, st);
+    if (obf) return launch_splitk_reduce_t(slab, (ushort4*)dx, n4, a.splits, st);
+    return launch_splitk_reduce(slab, (float*)dx, n4, a.splits, st);
   }
   return 0;
 }

@@ -44,7 +44,8 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    """Input NHWC fp32 [N,H,W,3]; output logits [N, num_classes]."""
+    """Input NHWC fp32 [N,H,W,3]; output logits [N, num_classes] (fp32).  With impl "bf16" the
+    activations between layers are bf16 tensors; parameters, BN statistics and the head are fp32."""
 
     def __init__(self, layers: List[int], num_classes: int = 1000, impl: str = "bf16"):
         super().__init__()
@@ -76,7 +77,7 @@ class ResNet(nn.Module):
     def forward(self, x):
         x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        return self.fc(x.mean(dim=(1, 2)))
+        return self.fc(x.to(self.fc.weight.dtype).mean(dim=(1, 2)))
 
 
 def resnet50(num_classes: int = 1000, impl: str = "bf16") -> ResNet:

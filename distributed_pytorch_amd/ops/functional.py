@@ -5,13 +5,16 @@ exposes the same kernels to PyTorch autograd so arbitrary NHWC conv/BN networks 
 them ("autograd.Functions over the kernels, used for generic nn.Module paths").
 
 Layout and precision contract (all tensors NHWC, contiguous):
-  conv2d_nhwc   x fp32 [N,H,W,C] (C % 8 == 0), w fp32 [K,R,S,C] -> z fp32 [N,P,Q,K]
-                The operands are split into bf16 planes inside the op: impl "bf16" = one plane
-                (mixed precision, fp32 accumulation), "x3" = three planes (fp32-grade, see
-                conv_x3.hip).  No conv bias (every conv here feeds a BatchNorm).
-  bn_act_nhwc   z fp32 -> act(BN(z) [+ residual]) fp32; act 0 = ReLU, 1 = none, 2 = ReLU(. + res).
-                Training mode updates running stats in place (momentum, unbiased var) and
-                num_batches_tracked; backward recomputes the activation mask from z (+res).
+  conv2d_nhwc   x [N,H,W,C] (C % 8 == 0), w fp32 [K,R,S,C] (master weights) -> z [N,P,Q,K].
+                impl "bf16": activations, conv outputs and their gradients are bf16 tensors that
+                the MFMA kernels read/write directly (one bf16 plane; fp32 accumulation; the
+                weight is rounded to bf16 per call); fp32 inputs are rounded on entry.
+                impl "x3": fp32 activations, split into three bf16 planes inside the op
+                (fp32-grade results, see conv_x3.hip).  No conv bias (every conv feeds a BN).
+  bn_act_nhwc   z (bf16 or fp32) -> act(BN(z) [+ residual]) in z's dtype; statistics and affine in
+                fp32; act 0 = ReLU, 1 = none, 2 = ReLU(. + res).  Training mode updates running
+                stats in place (momentum, unbiased var) and num_batches_tracked; backward
+                recomputes the activation mask from z (+res).
 On CPU the same functions run the fp32 CPU oracle (ops/cpu_ref.py) so models are testable here;
 on a GPU the native extension is required (loud failure, no silent fallback).
 """
@@ -54,8 +57,13 @@ WS = _Workspace()
 
 
 def split_planes(x: torch.Tensor, np_: int) -> torch.Tensor:
+    """[NP, *x.shape] bf16 operand planes of x (a bf16 x with NP == 1 is used as is)."""
+    if x.dtype == torch.bfloat16:
+        if np_ != 1:
+            raise ValueError("a bf16 tensor only provides one operand plane")
+        return x.contiguous().unsqueeze(0)
     out = torch.empty((np_,) + tuple(x.shape), device=x.device, dtype=torch.bfloat16)
-    _ext.require().split_planes(x.contiguous(), out)
+    _ext.require().split_planes(x.contiguous().float(), out)
     return out
 
 
@@ -100,7 +108,9 @@ class Conv2dNHWC(torch.autograd.Function):
         Kx = _ext.require()
         np_ = NPLANES[impl]
         xp, wp = split_planes(x, np_), split_planes(w, np_)
-        z = torch.empty(N, P, Q, K, device=x.device, dtype=torch.float32)
+        act_dtype = torch.bfloat16 if np_ == 1 else torch.float32
+        ctx.x_dtype = x.dtype if np_ == 3 else torch.bfloat16
+        z = torch.empty(N, P, Q, K, device=x.device, dtype=act_dtype)
         tile, s, pm = conv_config("fprop", N * P * Q, K, R * S * C, P * Q <= 16)
         s = Kx.x3_splits(R * S * C, s)
         slab = WS.get("slab", s * N * P * Q * K, x.device) if s > 1 else None
@@ -125,9 +135,12 @@ class Conv2dNHWC(torch.autograd.Function):
             return dx, dw, None, None, None
         Kx = _ext.require()
         xp, wp = a, b
-        dzp = split_planes(dz, xp.shape[0])
+        np_ = xp.shape[0]
+        if np_ == 1 and dz.dtype != torch.bfloat16:
+            dz = dz.to(torch.bfloat16)
+        dzp = split_planes(dz, np_)
         if ctx.needs_input_grad[0]:
-            dx = torch.empty(N, H, W, C, device=dz.device, dtype=torch.float32)
+            dx = torch.empty(N, H, W, C, device=dz.device, dtype=ctx.x_dtype)
             tile, s, pm = conv_config("dgrad", N * H * W, C, R * S * K, H * W <= 16)
             s = Kx.x3_splits(R * S * K, s)
             slab = WS.get("slab", s * N * H * W * C, dz.device) if s > 1 else None
@@ -153,7 +166,8 @@ class BnActNHWC(torch.autograd.Function):
         N, H, W, C = z.shape
         dev = z.device
         K = _ext.require() if _native(z) else cpu_ref
-        f32 = dict(device=dev, dtype=z.dtype)  # fp32 on GPU; the CPU oracle also runs float64
+        # per-channel statistics in fp32 on GPU (bf16 activations too); the CPU oracle also runs fp64
+        f32 = dict(device=dev, dtype=torch.float32 if _native(z) else z.dtype)
         mean, invstd, scale, shift = (torch.empty(C, **f32) for _ in range(4))
         if training:
             part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), dev, zero=True) if _native(z) else None
@@ -176,7 +190,7 @@ class BnActNHWC(torch.autograd.Function):
         N, H, W, C = z.shape
         native = _native(z)
         K = _ext.require() if native else cpu_ref
-        f32 = dict(device=z.device, dtype=z.dtype)
+        f32 = dict(device=z.device, dtype=torch.float32 if native else z.dtype)
         dz = torch.empty_like(z)
         dgamma, dbeta = torch.empty(C, **f32), torch.empty(C, **f32)
         dres = torch.empty_like(z) if ctx.act == 2 else None
@@ -192,7 +206,7 @@ def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, 
     a = ACT[act]
     if a == 2 and residual is None:
         raise ValueError("act='add_relu' needs a residual")
-    res = residual.contiguous() if residual is not None else None
+    res = residual.to(z.dtype).contiguous() if residual is not None else None
     return BnActNHWC.apply(z.contiguous(), gamma, beta, res, running_mean, running_var, num_batches_tracked,
                            bool(training), float(momentum), float(eps), a)
 
