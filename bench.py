@@ -20,7 +20,6 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -88,8 +87,7 @@ def main():
     def barrier():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
-        if ctx.world > 1:
-            dist.barrier()
+        ctx.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
@@ -99,10 +97,7 @@ def main():
         step()
     barrier()
     el = time.perf_counter() - t0
-    if ctx.world > 1:
-        tt = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt[0])
+    el = ctx.all_max(el)  # slowest rank
     loss = float(engine.loss.item())
     ms = el / a.steps * 1e3
     img_s = a.batch * ctx.world * a.steps / el

@@ -18,7 +18,6 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -62,8 +61,7 @@ def main():
     def barrier():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
-        if ctx.world > 1:
-            dist.barrier()
+        ctx.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
@@ -73,10 +71,7 @@ def main():
         loss = step()
     barrier()
     el = time.perf_counter() - t0
-    if ctx.world > 1:
-        tt = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt[0])
+    el = ctx.all_max(el)  # slowest rank
     img_s = a.batch * ctx.world * a.steps / el
     if ctx.rank == 0:
         print(json.dumps({

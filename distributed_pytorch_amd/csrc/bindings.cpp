@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 
 #include "runtime/rccl_comm.h"
+#include "runtime/tcp_store.h"
 
 extern "C" {
 int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd, float gscale,
@@ -620,6 +621,29 @@ PYBIND11_MODULE(_C, m) {
   m.def("augment", &augment);
   m.def("rccl_unique_id", []() { return py::bytes(dpa::RcclComm::unique_id()); });
   m.def("rccl_version", &dpa::RcclComm::version);
+  // native rendezvous store (bootstrap without torch.distributed); blocking calls release the GIL
+  py::class_<dpa::TcpStoreServer>(m, "TcpStoreServer")
+      .def(py::init<const std::string&, int>(), py::arg("host"), py::arg("port"))
+      .def_property_readonly("port", &dpa::TcpStoreServer::port);
+  py::class_<dpa::TcpStoreClient>(m, "TcpStoreClient")
+      .def(py::init<const std::string&, int, double>(), py::arg("host"), py::arg("port"), py::arg("timeout_s") = 600.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("set", [](dpa::TcpStoreClient& c, const std::string& k, py::bytes v) {
+        std::string sv(v);
+        py::gil_scoped_release nogil;
+        c.set(k, sv);
+      })
+      .def("get", [](dpa::TcpStoreClient& c, const std::string& k) {
+        std::string v;
+        {
+          py::gil_scoped_release nogil;
+          v = c.get(k);
+        }
+        return py::bytes(v);
+      })
+      .def("add", &dpa::TcpStoreClient::add, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &dpa::TcpStoreClient::wait, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &dpa::TcpStoreClient::barrier, py::call_guard<py::gil_scoped_release>());
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool>(), py::arg("rank"),
            py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("high_priority") = false,

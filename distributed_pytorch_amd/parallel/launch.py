@@ -5,10 +5,13 @@
 * torchrun style (main_ddp.py:93-104, start_ddp.sh): MASTER_ADDR/MASTER_PORT/WORLD_SIZE/RANK/
   LOCAL_RANK from the environment (``env://``).
 
-One process per GPU: LOCAL_RANK (or rank mod #GPUs) selects the device.  The torch.distributed
-process group (gloo) carries the rendezvous store and CPU-side barriers; on GPU the gradient
-collectives go through the native RCCL communicator bootstrapped from that store (``comm="rccl"``),
-or through torch's own nccl group (``comm="torch"``) for A/B comparison.
+One process per GPU: LOCAL_RANK (or rank mod #GPUs) selects the device.  Rendezvous:
+* ``DPA_RENDEZVOUS=torch`` (default): a torch.distributed gloo group carries the rendezvous store
+  and CPU-side barriers; the native RCCL communicator is bootstrapped from that store;
+* ``DPA_RENDEZVOUS=native``: no torch.distributed at all — the native C++ TCP store
+  (parallel/store.py) on MASTER_ADDR:DPA_STORE_PORT bootstraps RCCL and provides barriers.
+On GPU the gradient collectives go through the native RCCL communicator (``comm="rccl"``), or
+through torch's own nccl group (``comm="torch"``, torch rendezvous only) for A/B comparison.
 """
 from __future__ import annotations
 
@@ -21,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from .comm import Comm, NullComm, RcclComm, TorchComm
+from .store import NativeStore
 
 DEFAULT_PORT = 6585  # main_gather.py:107
 
@@ -33,6 +37,26 @@ class DistContext:
     device: torch.device
     comm: Comm
     initialized_pg: bool
+    store: Optional[NativeStore] = None
+    _nbar: int = 0
+
+    def barrier(self):
+        """CPU-side barrier over all ranks (gloo group or native store)."""
+        if self.initialized_pg:
+            dist.barrier()
+        elif self.store is not None:
+            self._nbar += 1
+            self.store.barrier(f"ctx_barrier_{self._nbar}")
+
+    def all_max(self, value: float) -> float:
+        if self.initialized_pg:
+            t = torch.tensor([float(value)], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t[0])
+        if self.store is not None:
+            self._nbar += 1
+            return self.store.all_max(f"ctx_max_{self._nbar}", value)
+        return float(value)
 
     def shutdown(self):
         try:
@@ -40,6 +64,8 @@ class DistContext:
         finally:
             if self.initialized_pg and dist.is_initialized():
                 dist.destroy_process_group()
+            if self.store is not None:
+                self.store.close()
 
 
 def _timeout():
@@ -57,7 +83,18 @@ def pick_device(local_rank: int, want: str = "auto") -> torch.device:
     return d
 
 
-def _make_comm(kind: str, rank: int, world: int, device: torch.device) -> Comm:
+def _rendezvous() -> str:
+    r = os.environ.get("DPA_RENDEZVOUS", "torch")
+    if r not in ("torch", "native"):
+        raise ValueError("DPA_RENDEZVOUS must be 'torch' or 'native'")
+    return r
+
+
+def _native_store(host: str, port: int, rank: int, world: int) -> NativeStore:
+    return NativeStore(host, port, rank, world, timeout_s=_timeout().total_seconds())
+
+
+def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=None) -> Comm:
     if world == 1:
         # DPA_FORCE_COMM=1 runs the real RCCL communicator even on one GPU (a 1-rank communicator:
         # every collective is an identity), exercising the stream/event/bucket path on a 1-GPU box
@@ -67,11 +104,16 @@ def _make_comm(kind: str, rank: int, world: int, device: torch.device) -> Comm:
             return RcclComm(0, 1, device, uid=_ext.require().rccl_unique_id())
         return NullComm()
     if device.type != "cuda":
+        if store is not None:
+            raise RuntimeError("native rendezvous drives RCCL only: use DPA_RENDEZVOUS=torch (gloo) on CPU")
         return TorchComm(device=device)
     if kind == "torch":
+        if store is not None:
+            raise RuntimeError("--comm torch needs the torch rendezvous")
         group = dist.new_group(backend="nccl")
         return TorchComm(group=group, device=device)
-    store = dist.distributed_c10d._get_default_store()
+    if store is None:
+        store = dist.distributed_c10d._get_default_store()
     comm = RcclComm(rank, world, device, store=store)
     # correctness-by-construction check of the fresh communicator: sum of (rank+1)
     t = torch.full((8,), float(rank + 1), device=device)
@@ -88,12 +130,15 @@ def init_cli(master_ip: str, num_nodes: int, rank: int, port: int = DEFAULT_PORT
              comm: str = "rccl") -> DistContext:
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
     dev = pick_device(local_rank, device)
-    init = False
+    init, store = False, None
     if num_nodes > 1:
-        dist.init_process_group(backend="gloo", init_method=f"tcp://{master_ip}:{port}", world_size=num_nodes,
-                                rank=rank, timeout=_timeout())
-        init = True
-    return DistContext(rank, num_nodes, local_rank, dev, _make_comm(comm, rank, num_nodes, dev), init)
+        if _rendezvous() == "native":
+            store = _native_store(master_ip, port, rank, num_nodes)
+        else:
+            dist.init_process_group(backend="gloo", init_method=f"tcp://{master_ip}:{port}", world_size=num_nodes,
+                                    rank=rank, timeout=_timeout())
+            init = True
+    return DistContext(rank, num_nodes, local_rank, dev, _make_comm(comm, rank, num_nodes, dev, store), init, store)
 
 
 def env_dict():
@@ -106,11 +151,15 @@ def init_env(device: str = "auto", comm: str = "rccl") -> DistContext:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = pick_device(local_rank, device)
-    init = False
+    init, store = False, None
     if world > 1:
-        dist.init_process_group(backend="gloo", init_method="env://", timeout=_timeout())
-        init = True
-    return DistContext(rank, world, local_rank, dev, _make_comm(comm, rank, world, dev), init)
+        if _rendezvous() == "native":
+            port = int(os.environ.get("DPA_STORE_PORT", int(os.environ["MASTER_PORT"]) + 1))
+            store = _native_store(os.environ["MASTER_ADDR"], port, rank, world)
+        else:
+            dist.init_process_group(backend="gloo", init_method="env://", timeout=_timeout())
+            init = True
+    return DistContext(rank, world, local_rank, dev, _make_comm(comm, rank, world, dev, store), init, store)
 
 
 def init_single(device: str = "auto") -> DistContext:

@@ -162,3 +162,21 @@ def run_generic_ddp(rank, world, port, steps, outdir, impl="ours"):
     torch.save({"sd": sd, "nb": nb}, os.path.join(outdir, f"gddp_{impl}_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_native_store(rank, world, port, outdir):
+    """Native C++ TCP store: RCCL-id exchange, barrier and max-reduce without torch.distributed."""
+    import json
+
+    from distributed_pytorch_amd.parallel.comm import exchange_unique_id
+    from distributed_pytorch_amd.parallel.store import NativeStore
+
+    st = NativeStore("127.0.0.1", port, rank, world, timeout_s=60)
+    uid = exchange_unique_id(st, rank, lambda: bytes(range(128)), tag="uid")
+    st.barrier("b1")
+    mx = st.all_max("m", 1.5 * rank + 0.25)
+    cnt = st.add("c", 1)
+    st.barrier("b2")
+    with open(os.path.join(outdir, f"ns_{rank}.json"), "w") as f:
+        json.dump({"uid": list(uid), "max": mx, "cnt": cnt}, f)
+    st.close()  # rank 0 keeps serving until every client checked out

@@ -132,3 +132,15 @@ def test_generic_ddp_matches_torch_ddp(tmp_path):
             assert torch.equal(a, b), f"{k}: replicas diverged"
         err = (a.double() - v.double()).abs().max() / v.double().abs().max().clamp_min(1e-12)
         assert err < 1e-6, (k, float(err))
+
+
+def test_native_tcp_store(tmp_path):
+    import json
+
+    d = str(tmp_path)
+    _spawn(H.run_native_store, d)
+    res = [json.load(open(os.path.join(d, f"ns_{r}.json"))) for r in range(WORLD)]
+    for r in res:
+        assert r["uid"] == list(range(128))
+        assert r["max"] == 1.5 * (WORLD - 1) + 0.25
+    assert sorted(r["cnt"] for r in res) == list(range(1, WORLD + 1))
