@@ -128,7 +128,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   constexpr int AROWS = ARC ? BK : BM, BROWS = BRC ? BK : BN;
   constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
   constexpr int STAGE = NP * (A_PLANE + B_PLANE);
-  __shared__ __attribute__((aligned(16))) u16 lds[NSTAGE * STAGE];
+  __shared__ __attribute__((aligned(16))) u16 lds[(NSTAGE == 2 ? 2 : 1) * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -228,9 +228,11 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     wb_ss = (int)(tap - rr * a.S) - a.pad;
   }
 
-  uint4 ra[NCA][NP], rb[NCB][NP];
+  // staging registers: one set (NSTAGE 1/2) or two alternating sets (NSTAGE 3: two tiles in flight)
+  uint4 ra0[NCA][NP], rb0[NCB][NP];
+  uint4 ra1[NSTAGE == 3 ? NCA : 1][NP], rb1[NSTAGE == 3 ? NCB : 1][NP];
 
-  auto load_tile = [&](int v) {
+  auto load_into = [&](int v, auto& ra, auto& rb) {
     const int kb = tile_off(vbeg + v);
     if constexpr (!WG) {
       const int k = kb + a_c8;
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     }
   };
 
-  auto store_tile = [&](int stage) {
+  auto store_from = [&](int stage, auto& ra, auto& rb) {
     u16* As = lds + stage * STAGE;
     u16* Bs = As + NP * A_PLANE;
 #pragma unroll
@@ -390,7 +392,34 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     }
   };
 
-  if (ntiles > 0) {
+  auto load_tile = [&](int v) { load_into(v, ra0, rb0); };
+  auto store_tile = [&](int stage) { store_from(stage, ra0, rb0); };
+
+  if (NSTAGE == 3 && ntiles > 0) {
+    // single LDS stage, two register tiles in flight: while tile t is consumed from LDS, tiles
+    // t+1 and t+2 are loading (uses the VGPR headroom left by the LDS-limited occupancy)
+    load_into(0, ra0, rb0);
+    store_from(0, ra0, rb0);
+    __syncthreads();
+    if (1 < ntiles) load_into(1, ra1, rb1);
+    if (2 < ntiles) load_into(2, ra0, rb0);
+    for (int kt = 0; kt < ntiles; kt += 2) {
+      compute_tile(0);
+      if (kt + 1 < ntiles) {
+        __syncthreads();
+        store_from(0, ra1, rb1);
+        __syncthreads();
+        if (kt + 3 < ntiles) load_into(kt + 3, ra1, rb1);
+        compute_tile(0);
+        if (kt + 2 < ntiles) {
+          __syncthreads();
+          store_from(0, ra0, rb0);
+          __syncthreads();
+          if (kt + 4 < ntiles) load_into(kt + 4, ra0, rb0);
+        }
+      }
+    }
+  } else if (ntiles > 0) {
     load_tile(0);
     store_tile(0);
     __syncthreads();
@@ -499,10 +528,16 @@ int launch_x3(const Args& a, hipStream_t st) {
 // tile id -> (block tile, stage depth, LDS stages):
 //   0: 128x128/k32/2  1: 64x64/k32/2  2: 128x128/k16/2  3: 64x64/k64/2
 //   4: 128x128/k16/1  5: 128x128/k32/1  6: 64x64/k32/1  7: 256x128/k32/1 (8 waves)
+//   8-11: the 128x128/k32, 128x128/k16, 256x128/k32, 64x64/k32 single-stage tiles with two register
+//   tiles in flight (NSTAGE 3)
 template <int MODE, int NP, bool OB = false>
 int launch_tile(const Args& a, int tile, hipStream_t st) {
   switch (tile) {
     case 7: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 1, OB>(a, st);
+    case 8: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 3, OB>(a, st);
+    case 9: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 3, OB>(a, st);
+    case 10: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 3, OB>(a, st);
+    case 11: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 3, OB>(a, st);
     case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 2, OB>(a, st);
     case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 2, OB>(a, st);
     case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 2, OB>(a, st);
@@ -519,8 +554,10 @@ int launch_any(const Args& a, int tile, int np, int obf, hipStream_t st) {
   if (obf) return launch_tile<MODE, 1, true>(a, tile, st);
   return np == 3 ? launch_tile<MODE, 3>(a, tile, st) : launch_tile<MODE, 1>(a, tile, st);
 }
-int tile_rows(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : (tile == 7 ? 256 : 128); }
-int tile_cols(int tile) { return (tile == 1 || tile == 3 || tile == 6) ? 64 : 128; }
+int tile_rows(int tile) {
+  return (tile == 1 || tile == 3 || tile == 6 || tile == 11) ? 64 : ((tile == 7 || tile == 10) ? 256 : 128);
+}
+int tile_cols(int tile) { return (tile == 1 || tile == 3 || tile == 6 || tile == 11) ? 64 : 128; }
 
 int grid_1d(long n) {
   long g = (n + 255) / 256;
