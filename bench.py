@@ -27,6 +27,7 @@ from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_c
 from distributed_pytorch_amd.engine import VGGEngine  # noqa: E402
 from distributed_pytorch_amd.parallel import init_env, make_sync  # noqa: E402
 
+BASELINE_METRIC = "images/sec whole-node VGG-11 CIFAR-10 at 1/2/4/8 MI355X; scaling efficiency"  # BASELINE.json
 # BASELINE.md (reference harness measured on CPU — the only numbers the reference has)
 BASELINE_IMG_S = {1: 397.8, 2: 601.8}
 # stock PyTorch-ROCm eager fp32 on one MI355X (tools/torch_baseline.py, profiles/)
@@ -104,7 +105,7 @@ def main():
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(ctx.world)
         rec = {
-            "metric": "images/sec whole-node VGG-11 CIFAR-10 training (batch 256/GPU)",
+            "metric": BASELINE_METRIC,
             "value": round(img_s, 1),
             "unit": "images/sec",
             "n_gpus": ctx.world,

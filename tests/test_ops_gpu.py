@@ -379,3 +379,34 @@ def test_rccl_watchdog_tracks_and_retires_ops():
     c.abort()
     with pytest.raises(RuntimeError, match="aborted"):
         c.all_reduce(t, "sum")
+
+
+@pytest.mark.parametrize("impl", ["fp32", "x3"])
+def test_engine_eval_matches_torch_after_training(impl):
+    """After real training steps (running stats moved, weights updated), the engine's eval forward
+    equals stock torch eval on its exported state_dict."""
+    from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_cifar
+    from distributed_pytorch_amd.engine import VGGEngine
+    from distributed_pytorch_amd.models import VGG11
+
+    ds = synthetic_cifar(2048, 0)
+    ld = DeviceLoader(ds, 256, "cuda", sampler=ShardSampler(2048, 1, 0), train=True, seed=1)
+    e = VGGEngine("VGG11", "cuda", max_batch=256, impl=impl, lr=0.1)
+    e.init_parameters(seed=1)
+    for x, t in ld:
+        e.forward_backward(x, t)
+        e.sgd_step()
+        e.finish_step()
+    m = VGG11()
+    m.load_state_dict(e.state_dict())
+    m.eval()
+    test = DeviceLoader(synthetic_cifar(512, 1), 256, "cuda", train=False)
+    e.begin_eval()
+    for x, t in test:
+        logits = torch.zeros(x.shape[0], 10, device="cuda")
+        e.eval_batch(x, t, logits)
+        with torch.no_grad():
+            ref = m(x[..., :3].permute(0, 3, 1, 2).cpu())
+        torch.cuda.synchronize()
+        err = (logits.cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 1e-3, err
