@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--impl", default="bf16", choices=["bf16", "x3"])
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--autotune", action="store_true",
+                    help="time every conv kernel config during warmup and save tuning/generic_mi355x.json")
     a = ap.parse_args()
     ctx = init_env(comm=a.comm)
     dev = ctx.device
@@ -55,6 +57,14 @@ def main():
         opt.step(ddp.finish())
         return loss
 
+    if a.autotune:
+        from distributed_pytorch_amd.ops import functional as Fn
+
+        Fn.set_autotune(True)
+        step()  # tunes every conv call of the step (outside the timed region)
+        Fn.set_autotune(False)
+        if ctx.rank == 0:
+            Fn.save_tuning_table()
     for _ in range(a.warmup):
         step()
 

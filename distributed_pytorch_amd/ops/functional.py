@@ -20,8 +20,10 @@ on a GPU the native extension is required (loud failure, no silent fallback).
 """
 from __future__ import annotations
 
+import json
 import math
-from typing import Dict, Optional, Tuple
+import os
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -68,6 +70,91 @@ def split_planes(x: torch.Tensor, np_: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ conv launch configuration
+# Per-call (tile, splits, posmajor): measured table (tuning/generic_mi355x.json, written by the
+# autotuner: ``set_autotune(True)``, e.g. ``bench_resnet.py --autotune``), else a heuristic.
+TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                          "generic_mi355x.json")
+_table: Optional[Dict[str, list]] = None
+_chosen: Dict[str, Tuple[int, int, bool]] = {}
+_AUTOTUNE = {"on": os.environ.get("DPA_AUTOTUNE", "0") == "1", "dirty": False}
+N_TILES = 12
+
+
+def set_autotune(on: bool):
+    _AUTOTUNE["on"] = bool(on)
+
+
+def _table_get() -> Dict[str, list]:
+    global _table
+    if _table is None:
+        _table = {}
+        if os.environ.get("DPA_NO_TUNING", "0") != "1" and os.path.exists(TABLE_PATH):
+            with open(TABLE_PATH) as f:
+                _table = json.load(f)
+    return _table
+
+
+def save_tuning_table(path: Optional[str] = None):
+    """Merge the autotuned entries into the JSON table (atomic replace)."""
+    path = path or TABLE_PATH
+    cur = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            cur = json.load(f)
+    cur.update(_table_get())
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(dict(sorted(cur.items())), f, indent=0)
+    os.replace(tmp, path)
+    _AUTOTUNE["dirty"] = False
+
+
+def _autotune(key: str, kind: str, red: int, run: Callable[[int, int, bool], None],
+              slab_bytes: Callable[[int], int]) -> Tuple[int, int, bool]:
+    Kx = _ext.require()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = None
+    splits = (1, 2, 4, 8, 16, 32, 64, 128, 256) if kind == "wgrad" else (1, 2, 4, 8, 16)
+    seen = set()
+    for tile in range(N_TILES):
+        for s0 in splits:
+            s = Kx.x3_splits(red, s0)
+            for pm in (False, True):
+                if (tile, s, pm) in seen or slab_bytes(s) > (512 << 20):
+                    continue
+                seen.add((tile, s, pm))
+                run(tile, s, pm)
+                ev0.record()
+                for _ in range(3):
+                    run(tile, s, pm)
+                ev1.record()
+                ev1.synchronize()
+                ms = ev0.elapsed_time(ev1) / 3
+                if best is None or ms < best[3]:
+                    best = [tile, s, pm, ms]
+    _table_get()[key] = best
+    _AUTOTUNE["dirty"] = True
+    return best[0], best[1], best[2]
+
+
+def choose_config(impl: str, kind: str, geom: tuple, M: int, Ngemm: int, Kred: int, hw_small: bool,
+                  run: Optional[Callable[[int, int, bool], None]] = None,
+                  slab_bytes: Optional[Callable[[int], int]] = None) -> Tuple[int, int, bool]:
+    key = "|".join(str(v) for v in (impl, kind) + tuple(geom))
+    c = _chosen.get(key)
+    if c is not None:
+        return c
+    t = _table_get().get(key)
+    if t is not None:
+        c = (int(t[0]), int(t[1]), bool(t[2]))
+    elif _AUTOTUNE["on"] and run is not None:
+        c = _autotune(key, kind, M if kind == "wgrad" else Kred, run, slab_bytes)
+    else:
+        c = conv_config(kind, M, Ngemm, Kred, hw_small)
+    _chosen[key] = c
+    return c
+
+
 _cfg_cache: Dict[tuple, Tuple[int, int, bool]] = {}
 
 
@@ -111,16 +198,22 @@ class Conv2dNHWC(torch.autograd.Function):
         act_dtype = torch.bfloat16 if np_ == 1 else torch.float32
         ctx.x_dtype = x.dtype if np_ == 3 else torch.bfloat16
         z = torch.empty(N, P, Q, K, device=x.device, dtype=act_dtype)
-        tile, s, pm = conv_config("fprop", N * P * Q, K, R * S * C, P * Q <= 16)
-        s = Kx.x3_splits(R * S * C, s)
-        slab = WS.get("slab", s * N * P * Q * K, x.device) if s > 1 else None
-        Kx.conv_x3_fprop(xp, wp, z, slab, stride, pad, s, tile, True, pm)
+        geom = (N, H, W, C, K, R, S, stride, pad)
+
+        def run(tile, s, pm):
+            slab = WS.get("slab", s * N * P * Q * K, x.device) if s > 1 else None
+            Kx.conv_x3_fprop(xp, wp, z, slab, stride, pad, s, tile, True, pm)
+
+        cfg = choose_config(impl, "fprop", geom, N * P * Q, K, R * S * C, P * Q <= 16, run,
+                            lambda s: 4 * s * N * P * Q * K)
+        run(cfg[0], Kx.x3_splits(R * S * C, cfg[1]), cfg[2])
         ctx.save_for_backward(xp, wp)
         return z
 
     @staticmethod
     def backward(ctx, dz):
         N, H, W, C, K, R, S, stride, pad, P, Q = ctx.geom
+        geom = (N, H, W, C, K, R, S, stride, pad)
         a, b = ctx.saved_tensors
         dz = dz.contiguous()
         dx = dw = None
@@ -141,16 +234,24 @@ class Conv2dNHWC(torch.autograd.Function):
         dzp = split_planes(dz, np_)
         if ctx.needs_input_grad[0]:
             dx = torch.empty(N, H, W, C, device=dz.device, dtype=ctx.x_dtype)
-            tile, s, pm = conv_config("dgrad", N * H * W, C, R * S * K, H * W <= 16)
-            s = Kx.x3_splits(R * S * K, s)
-            slab = WS.get("slab", s * N * H * W * C, dz.device) if s > 1 else None
-            Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm)
+
+            def run_d(tile, s, pm):
+                slab = WS.get("slab", s * N * H * W * C, dz.device) if s > 1 else None
+                Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm)
+
+            cfg = choose_config(ctx.impl, "dgrad", geom, N * H * W, C, R * S * K, H * W <= 16, run_d,
+                                lambda s: 4 * s * N * H * W * C)
+            run_d(cfg[0], Kx.x3_splits(R * S * K, cfg[1]), cfg[2])
         if ctx.needs_input_grad[1]:
             dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
-            tile, s, pm = conv_config("wgrad", N * P * Q, K, R * S * C, P * Q <= 16)
-            s = Kx.x3_splits(N * P * Q, s)
-            slab = WS.get("slab", s * K * R * S * C, dz.device) if s > 1 else None
-            Kx.conv_x3_wgrad(xp, dzp, dw, slab, stride, pad, s, tile, pm)
+
+            def run_w(tile, s, pm):
+                slab = WS.get("slab", s * K * R * S * C, dz.device) if s > 1 else None
+                Kx.conv_x3_wgrad(xp, dzp, dw, slab, stride, pad, s, tile, pm)
+
+            cfg = choose_config(ctx.impl, "wgrad", geom, N * P * Q, K, R * S * C, P * Q <= 16, run_w,
+                                lambda s: 4 * s * K * R * S * C)
+            run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
         return dx, dw, None, None, None
 
 
