@@ -62,8 +62,10 @@ __device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) {
 struct Args {
   const u16* x;     // FPROP: GEMM input planes NHWC [N,H,W,C]; WGRAD: conv input planes (B operand)
   long xps;         // plane stride (elements)
+  unsigned xbytes;  // bytes of ONE plane of x (buffer-descriptor range; < 2^31)
   const u16* w;     // FPROP: weight planes [Nout][R][S][C]; WGRAD: dZ planes [N,P,Q,Kout]
   long wps;
+  unsigned wbytes;  // bytes of one plane of w
   float* out;       // FPROP: NHWC [N,P,Q,Nout] or slabs; WGRAD: dW [Kout][R*S*C] or slabs
   u16* outb;        // bf16 output (OB kernels, single split): FPROP/DGRAD NHWC
   long slab;
@@ -87,13 +89,21 @@ __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& 
   ow = pos - oh * (unsigned)a.Q;
 }
 
-// 16-byte operand-plane load; always issued (from the plane base when masked off), selected after:
-// branch-free (a "valid ? load : 0" becomes a branch + vmcnt drain per load) and 16-B aligned
-// (every chunk starts on a multiple of 8 bf16), so it lowers to one global_load_dwordx4.
-__device__ __forceinline__ uint4 ld16m(const u16* base, long off, bool valid) {
-  const uint4* p = reinterpret_cast<const uint4*>(__builtin_assume_aligned(base + (valid ? off : 0), 16));
-  const uint4 v = *p;
-  return valid ? v : make_uint4(0u, 0u, 0u, 0u);
+// 16-byte operand-plane loads through buffer descriptors: a masked-off lane gets an offset beyond
+// the descriptor's range and the hardware returns zeros.  The load is unconditional and there is no
+// select on its result, so hipcc cannot turn the mask into an exec branch around each load (a
+// pointer-select + value-select formulation compiled to s_and_saveexec/s_cbranch per load).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const u16* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, long elem_off, bool valid) {
+  const unsigned vo = valid ? (unsigned)(elem_off * 2) : OOB;
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vo, 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
@@ -228,6 +238,13 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     wb_ss = (int)(tap - rr * a.S) - a.pad;
   }
 
+  __amdgpu_buffer_rsrc_t rx[NP], rw[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    rx[p] = plane_rsrc(a.x + p * a.xps, a.xbytes);
+    rw[p] = plane_rsrc(a.w + p * a.wps, a.wbytes);
+  }
+
   // staging registers: one set (NSTAGE 1/2) or two alternating sets (NSTAGE 3: two tiles in flight)
   uint4 ra0[NCA][NP], rb0[NCB][NP];
   uint4 ra1[NSTAGE == 3 ? NCA : 1][NP], rb1[NSTAGE == 3 ? NCB : 1][NP];
@@ -253,7 +270,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         va = va && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const long aoff = (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) ra[j][p] = ld16m(a.x + p * a.xps, aoff, va);
+        for (int p = 0; p < NP; ++p) ra[j][p] = bload(rx[p], aoff, va);
       }
       if constexpr (DG) {  // weight rows (r,s,k) of the flipped filter, c-contiguous
 #pragma unroll
@@ -267,7 +284,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
           const int ss = (int)(tp - rr * a.S);
           const long boff = (((long)ko * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + col;
 #pragma unroll
-          for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.w + p * a.wps, boff, vb);
+          for (int p = 0; p < NP; ++p) rb[j][p] = bload(rw[p], boff, vb);
         }
       } else {
 #pragma unroll
@@ -276,7 +293,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
           const bool vb = kv && n < a.Nout;
           const long boff = (long)n * a.Ktot + k;
 #pragma unroll
-          for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.w + p * a.wps, boff, vb);
+          for (int p = 0; p < NP; ++p) rb[j][p] = bload(rw[p], boff, vb);
         }
       }
     } else {
@@ -286,22 +303,22 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         const int col = m0 + a_c8;
         const bool v = m < KMAX && col < a.Nout;
         unsigned img = 0, oh = 0, ow = 0;
-        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        decode_row(a, (unsigned)m, img, oh, ow);  // unconditional: no branch (masked lanes read OOB)
         const long off = (((long)img * a.P + oh) * a.Q + ow) * a.Nout + col;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) ra[j][p] = ld16m(a.w + p * a.wps, off, v);
+        for (int p = 0; p < NP; ++p) ra[j][p] = bload(rw[p], off, v);
       }
 #pragma unroll
       for (int j = 0; j < NCB; ++j) {
         const int m = kb + b_r0 + j * BROWSTEP;
         bool v = m < KMAX && wb_valid;
         unsigned img = 0, oh = 0, ow = 0;
-        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        decode_row(a, (unsigned)m, img, oh, ow);  // unconditional: no branch (masked lanes read OOB)
         const int ih = (int)oh * a.stride + wb_rr, iw = (int)ow * a.stride + wb_ss;
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const long off = (((long)img * a.H + ih) * a.W + iw) * a.C + wb_c;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) rb[j][p] = ld16m(a.x + p * a.xps, off, v);
+        for (int p = 0; p < NP; ++p) rb[j][p] = bload(rx[p], off, v);
       }
     }
   };
@@ -585,6 +602,14 @@ void fill(Args& a, int N, int H, int W, int C, int R, int S, int stride, int pad
   a.fd_N = make_fastdiv(N);
 }
 
+// descriptor ranges (bytes of one plane); the 32-bit buffer offsets need planes < 2 GiB
+int set_bytes(Args& a, long xelems, long welems) {
+  if (xelems * 2 >= (1L << 31) || welems * 2 >= (1L << 31)) return 1;
+  a.xbytes = (unsigned)(xelems * 2);
+  a.wbytes = (unsigned)(welems * 2);
+  return 0;
+}
+
 int xsplits(int Kred, int splits) {
   const int nt = cdiv(Kred, BKMIN);
   if (splits < 1) splits = 1;
@@ -612,6 +637,7 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   fill(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
   if (C % 8 || Kout % 8) return -2;
+  if (set_bytes(a, (long)N * H * W * C, (long)Kout * a.Ktot)) return -5;
   a.gm = cdiv(a.M, tile_rows(tile));
   a.gn = cdiv(Kout, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
@@ -643,6 +669,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   a.wps = wps;
   if (stride < 1 || (stride & (stride - 1)) || R - 1 - pad < 0) return -3;
   fill(a, N, Hd, Wd, K, R, S, 1, R - 1 - pad);
+  if (set_bytes(a, (long)N * Hd * Wd * K, (long)K * R * S * C)) return -5;
   a.P = H;
   a.Q = W;
   a.M = N * H * W;
@@ -680,6 +707,7 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   a.w = dz;
   a.wps = dzps;
   fill(a, N, H, W, C, R, S, stride, pad);
+  if (set_bytes(a, (long)N * H * W * C, (long)a.M * Kout)) return -5;
   a.Nout = Kout;
   if (C % 8 || Kout % 8) return -2;
   a.gm = cdiv(Kout, tile_rows(tile));
