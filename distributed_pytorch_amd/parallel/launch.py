@@ -112,9 +112,17 @@ def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=Non
             raise RuntimeError("--comm torch needs the torch rendezvous")
         group = dist.new_group(backend="nccl")
         return TorchComm(group=group, device=device)
-    if store is None:
+    torch_store = store is None
+    if torch_store:
         store = dist.distributed_c10d._get_default_store()
-    comm = RcclComm(rank, world, device, store=store)
+    try:
+        comm = RcclComm(rank, world, device, store=store)
+    except Exception as e:  # noqa: BLE001 — keep the job alive on torch's own RCCL group
+        if not torch_store or os.environ.get("DPA_COMM_FALLBACK", "1") != "1":
+            raise
+        print(f"[rank {rank}] native RCCL communicator failed ({e}); falling back to torch's nccl (RCCL) group",
+              flush=True)
+        return TorchComm(group=dist.new_group(backend="nccl"), device=device)
     # correctness-by-construction check of the fresh communicator: sum of (rank+1)
     t = torch.full((8,), float(rank + 1), device=device)
     with comm.region():
