@@ -133,8 +133,13 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
                     : (BM * CPR) % THREADS == 0 && THREADS % CPR == 0, "A slot mapping");
   static_assert(BRC ? (BK * BN / 8) % THREADS == 0 && THREADS % (BN / 8) == 0
                     : (BN * CPR) % THREADS == 0 && THREADS % CPR == 0, "B slot mapping");
-  constexpr int APITCH = ARC ? BM + 32 : BK + 8;  // bf16 per LDS row
-  constexpr int BPITCH = BRC ? BN + 32 : BK + 8;
+  // k-contiguous images are unpadded (BK bf16 per row) with the 16-B chunk index XOR-swizzled by
+  // the row's position in the 256-B bank row (conflict-free ds_read_b128 fragment reads, 20 % less
+  // LDS than the old +8 padding -> more resident blocks); row-contiguous images keep +32 padding
+  constexpr int APITCH = ARC ? BM + 32 : BK;  // bf16 per LDS row
+  constexpr int BPITCH = BRC ? BN + 32 : BK;
+  constexpr int RPB = 16 / CPR;  // k-contiguous rows per 256-B bank row
+  auto swz = [](int row) { return (row / RPB) & (CPR - 1); };
   constexpr int AROWS = ARC ? BK : BM, BROWS = BRC ? BK : BN;
   constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
   constexpr int STAGE = NP * (A_PLANE + B_PLANE);
@@ -330,12 +335,14 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     for (int j = 0; j < NCA; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        *reinterpret_cast<uint4*>(As + p * A_PLANE + (a_r0 + j * AROWSTEP) * APITCH + a_c8) = ra[j][p];
+        *reinterpret_cast<uint4*>(As + p * A_PLANE + (a_r0 + j * AROWSTEP) * APITCH +
+                                  (ARC ? a_c8 : ((a_c8 >> 3) ^ swz(a_r0 + j * AROWSTEP)) << 3)) = ra[j][p];
 #pragma unroll
     for (int j = 0; j < NCB; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + (b_r0 + j * BROWSTEP) * BPITCH + b_c8) = rb[j][p];
+        *reinterpret_cast<uint4*>(Bs + p * B_PLANE + (b_r0 + j * BROWSTEP) * BPITCH +
+                                  (BRC ? b_c8 : ((b_c8 >> 3) ^ swz(b_r0 + j * BROWSTEP)) << 3)) = rb[j][p];
   };
 
   f32x16 acc[TM][TN];
@@ -350,7 +357,8 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   // ([m][col]): two ds_read_b64_tr_b16; lane 4q+p of each 16-lane group addresses row q of its
   // 4-row block, columns 4p..4p+3, and receives its own column (kout/rsc = l&31) of the block.
   auto frag_k = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
-    const uint4 v = *reinterpret_cast<const uint4*>(base + (row0 + li) * pitch + 16 * ks + 8 * lh);
+    const int row = row0 + li;
+    const uint4 v = *reinterpret_cast<const uint4*>(base + row * pitch + (((2 * ks + lh) ^ swz(row)) << 3));
     return __builtin_bit_cast(bf16x8, v);
   };
   auto frag_r = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
