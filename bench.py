@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (reference: 256 per node)")
-    ap.add_argument("--mode", default="ddp", choices=["ddp", "allreduce", "gather"])
+    ap.add_argument("--mode", default="ddp", choices=["ddp", "allreduce", "gather", "zero1"])
     ap.add_argument("--model", default="VGG11")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=None)
@@ -78,8 +78,7 @@ def main():
         x, t = next(it)
         sync.begin_step()
         engine.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
-        gs = sync.finish()
-        engine.sgd_step(gs)
+        sync.update(sync.finish())
         engine.finish_step()
 
     for _ in range(a.warmup):

@@ -142,6 +142,11 @@ class TorchComm(Comm):
         self._w(dist.reduce_scatter_tensor(recv, send, _TORCH_OPS[op], group=self.group, async_op=True))
 
     def all_gather(self, send, recv):
+        if self.device.type == "cpu":  # gloo: list form (send may alias its slot of recv)
+            src = send.clone()
+            self._w(dist.all_gather(list(recv.view(self.world, -1).unbind(0)), src.view(-1), group=self.group,
+                                    async_op=True))
+            return
         self._w(dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True))
 
     def wait(self):

@@ -6,6 +6,10 @@
   mode "ddp"       (main_ddp.py:137)          DDP semantics: initial broadcast of params+buffers
                    from rank 0, BN buffers broadcast before every training forward, bucketed
                    all_reduce(SUM) overlapped with backward, /W fused into SGD.
+  mode "zero1"     (new scope)                DDP semantics with a sharded optimizer step (ZeRO
+                   stage 1): each bucket is reduce-scattered during backward, every rank updates
+                   only its 1/W of the parameters (fused SGD on its slices), then the buckets are
+                   all-gathered.  Same numerics as "ddp"; the optimizer's memory traffic is 1/W.
 
 Differences from the reference, all by design:
 * every mode works on contiguous slices of the flat grad arena (no per-step allocation, no
@@ -160,6 +164,10 @@ class GradSync:
     def grad_scale(self) -> float:
         return 1.0
 
+    def update(self, grad_scale: float):
+        """Apply the optimizer step to the synchronised gradients (the whole arena by default)."""
+        self.engine.sgd_step(grad_scale)
+
 
 class GatherScatterSync(GradSync):
     """Mode A: gather → mean on rank 0 → broadcast (main_gather.py:42-59)."""
@@ -222,8 +230,51 @@ class DDPSync(GradSync):
         return 1.0 / self.world
 
 
-MODES = {"gather": GatherScatterSync, "allreduce": AllReduceSync, "ddp": DDPSync}
-DEFAULT_BUCKET_MB = {"gather": 0.0, "allreduce": 0.0, "ddp": 10.0}
+class ZeroSync(DDPSync):
+    """ZeRO-1 on the flat arenas: reduce_scatter(SUM) per bucket during backward (in place: the
+    rank's shard of the bucket receives the sum), SGD on the owned shards only, all_gather of
+    every bucket's parameters, then one split kernel refreshes the bf16 weight planes.  Bucket
+    spans are multiples of 64 elements, so W | 16 keeps every shard float4-aligned."""
+
+    mode = "zero1"
+
+    def __init__(self, engine, comm, bucket_mb: float = 10.0, overlap: bool = True, broadcast_init: bool = True,
+                 broadcast_buffers: bool = True):
+        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init, broadcast_buffers)
+        if self.active:
+            for b in self.buckets:
+                if b.numel % (4 * self.world):
+                    raise ValueError(f"zero1: bucket of {b.numel} elements does not split into 4-aligned shards "
+                                     f"over {self.world} ranks")
+
+    def _shard(self, b: Bucket):
+        sb = b.numel // self.world
+        lo = b.lo + self.comm.rank * sb
+        return lo, sb
+
+    def reduce_bucket(self, b: Bucket):
+        g = self.engine.grads.flat
+        lo, sb = self._shard(b)
+        self.comm.reduce_scatter(g[b.lo:b.hi], g[lo:lo + sb], "sum")
+
+    def update(self, grad_scale: float):
+        e = self.engine
+        if not self.active:
+            e.sgd_step(grad_scale)
+            return
+        for b in self.buckets:  # the owned shards (compute stream, after finish()'s wait)
+            lo, sb = self._shard(b)
+            e.sgd_step(grad_scale, lo, sb)
+        with self.comm.region():
+            for b in self.buckets:
+                lo, sb = self._shard(b)
+                self.comm.all_gather(e.params.flat[lo:lo + sb], e.params.flat[b.lo:b.hi])
+        self.comm.wait()
+        e.refresh_weight_planes()
+
+
+MODES = {"gather": GatherScatterSync, "allreduce": AllReduceSync, "ddp": DDPSync, "zero1": ZeroSync}
+DEFAULT_BUCKET_MB = {"gather": 0.0, "allreduce": 0.0, "ddp": 10.0, "zero1": 10.0}
 
 
 def make_sync(mode: str, engine, comm: Comm, bucket_mb: Optional[float] = None, overlap: bool = True,

@@ -54,7 +54,7 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
             with trace_range("sync"):
                 gscale = sync.finish()
             with trace_range("sgd"):
-                engine.sgd_step(gscale)
+                sync.update(gscale)
             engine.finish_step()
         n_iters += 1
         if batch_idx == start_batch:

@@ -51,8 +51,7 @@ def run_engine_mode(rank, world, port, mode, steps, outdir, bucket_mb=None, over
     for x, t in _batches(rank, steps):
         sync.begin_step()
         e.forward_backward(_x4(x), t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
-        gs = sync.finish()
-        e.sgd_step(gs)
+        sync.update(sync.finish())
         e.finish_step()
         losses.append(float(e.loss.item()))
     if mode == "ddp":

@@ -22,16 +22,16 @@ def _spawn(fn, *args):
 @pytest.fixture(scope="module")
 def mode_results(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("modes"))
-    for mode in ("gather", "allreduce", "ddp"):
+    for mode in ("gather", "allreduce", "ddp", "zero1"):
         _spawn(H.run_engine_mode, mode, STEPS, d)
     _spawn(H.run_torch_ddp, STEPS, d)
     out = {}
-    for name in ("gather", "allreduce", "ddp", "torchddp"):
+    for name in ("gather", "allreduce", "ddp", "zero1", "torchddp"):
         out[name] = [torch.load(os.path.join(d, f"{name}_{r}.pt"), weights_only=True) for r in range(WORLD)]
     return out
 
 
-@pytest.mark.parametrize("mode", ["gather", "allreduce", "ddp"])
+@pytest.mark.parametrize("mode", ["gather", "allreduce", "ddp", "zero1"])
 def test_replicas_identical(mode_results, mode):
     r0, r1 = mode_results[mode]
     assert torch.equal(r0["params"], r1["params"]), f"{mode}: parameters diverged across ranks"
@@ -39,13 +39,13 @@ def test_replicas_identical(mode_results, mode):
 
 def test_modes_agree(mode_results):
     a = mode_results["gather"][0]["params"]
-    for m in ("allreduce", "ddp"):
+    for m in ("allreduce", "ddp", "zero1"):
         b = mode_results[m][0]["params"]
         assert (a - b).abs().max().item() < 1e-5 * max(1.0, a.abs().max().item()), m
     # per-rank losses identical across modes (same data, same params each step)
     for r in range(WORLD):
         la = mode_results["gather"][r]["losses"]
-        for m in ("allreduce", "ddp"):
+        for m in ("allreduce", "ddp", "zero1"):
             lb = mode_results[m][r]["losses"]
             assert all(abs(x - y) < 1e-4 for x, y in zip(la, lb))
 

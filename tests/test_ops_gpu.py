@@ -299,7 +299,7 @@ def test_engine_training_converges_and_evaluates(impl):
 
 
 @pytest.mark.parametrize("debug_sync", [False, True])
-@pytest.mark.parametrize("mode", ["ddp", "allreduce", "gather"])
+@pytest.mark.parametrize("mode", ["ddp", "allreduce", "gather", "zero1"])
 def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatch):
     """A 1-rank native RCCL communicator (every collective is an identity) driving the real
     bucket / comm-stream / event path: results must equal the no-communication run bit for bit."""
@@ -324,8 +324,7 @@ def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatc
             x[..., 3] = 0
             sync.begin_step()
             e.forward_backward(x, t.cuda(), grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
-            gs = sync.finish()
-            e.sgd_step(gs)
+            sync.update(sync.finish())
             e.finish_step()
         torch.cuda.synchronize()
         comm.check()

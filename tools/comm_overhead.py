@@ -73,7 +73,7 @@ def run(comm, mode, steps, warmup, batch):
     def step():
         sync.begin_step()
         e.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
-        e.sgd_step(sync.finish())
+        sync.update(sync.finish())
         e.finish_step()
 
     for _ in range(warmup):
