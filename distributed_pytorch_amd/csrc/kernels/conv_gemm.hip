@@ -73,6 +73,7 @@ struct ConvArgs {
   int splits;       // split-K factor (tiles of the reduction are partitioned over blockIdx.y)
   int posmajor;     // row order (oh,ow,img) + tap skipping (see header)
   long slab;        // elements per split slab (0 when splits==1)
+  unsigned xbytes, wbytes;  // buffer-descriptor ranges of x and w (< 2 GiB)
   FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
 };
 
@@ -97,9 +98,16 @@ __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cas
 
 // Branch-free masked load: always issue the load (from the tensor base when masked off) and select
 // afterwards — a per-slot "valid ? load : 0" makes hipcc branch around each load and drain vmcnt.
-__device__ __forceinline__ float4 ldg4m(const float* base, long off, bool valid) {
-  const float4 v = *reinterpret_cast<const float4*>(base + (valid ? off : 0));
-  return valid ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+// 16-byte operand load through a buffer descriptor: a masked-off lane reads past the range and
+// gets zeros (unconditional load, no select: see conv_x3.hip)
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const float* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 ldg4m(__amdgpu_buffer_rsrc_t r, long off, bool valid) {
+  const unsigned vo = valid ? (unsigned)(off * 4) : 0x80000000u;
+  const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vo, 0, 0);
+  return make_float4(v.x, v.y, v.z, v.w);
 }
 
 // logical GEMM row m -> (img, oh, ow)
@@ -121,6 +129,7 @@ enum { MODE_FPROP = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvArgs a) {
+  const __amdgpu_buffer_rsrc_t rx = rsrc_of(a.x, a.xbytes), rw = rsrc_of(a.w, a.wbytes);
   constexpr bool WGRAD = MODE == MODE_WGRAD;
   constexpr bool B_ROWC = MODE != MODE_FPROP;  // B operand row-contiguous in global memory
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
       for (int j = 0; j < NA; ++j) {
         const int ih = a_ih0[j] + (int)r, iw = a_iw0[j] + s;
         const bool v = kval && a_img[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        ra[j] = ldg4m(a.x, (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c, v);
+        ra[j] = ldg4m(rx, (((long)a_img[j] * a.H + ih) * a.W + iw) * a.C + c, v);
       }
       if constexpr (MODE == MODE_FPROP) {
         const int kb4 = kb + b_k4 * 4;
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         for (int j = 0; j < NB; ++j) {
           const int n = n0 + b_row0 + j * BSl::ROW_STEP;
           const bool v = kbv && n < a.Nout;
-          rb[j] = ldg4m(a.w, (long)n * a.Ktot + kb4, v);
+          rb[j] = ldg4m(rw, (long)n * a.Ktot + kb4, v);
         }
       } else {
         // DGRAD: B[n=c][k=(r',s',kk)] = W[kk][R-1-r'][S-1-s'][c], W stored [Kout=a.C][R][S][Nout]
@@ -289,7 +298,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
           const unsigned rr = fdiv(tp, a.fd_S);
           const int ss = (int)(tp - rr * a.S);
           const bool v = k < KMAX && b_colvalid;
-          rb[j] = ldg4m(a.w, (((long)kk * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + b_c, v);
+          rb[j] = ldg4m(rw, (((long)kk * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + b_c, v);
         }
       }
     } else {
@@ -299,19 +308,19 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(ConvAr
         const int m = kb + a_krow + j * ASl::K_STEP;
         bool v = m < KMAX && a_col < a.Nout;
         unsigned img = 0, oh = 0, ow = 0;
-        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        decode_row(a, (unsigned)m, img, oh, ow);  // unconditional: masked lanes read out of range
         const long row = ((long)img * a.P + oh) * a.Q + ow;
-        ra[j] = ldg4m(a.w, row * a.Nout + a_col, v);
+        ra[j] = ldg4m(rw, row * a.Nout + a_col, v);
       }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int m = kb + b_krow + j * BSl::K_STEP;
         bool v = m < KMAX && b_colvalid;
         unsigned img = 0, oh = 0, ow = 0;
-        if (v) decode_row(a, (unsigned)m, img, oh, ow);
+        decode_row(a, (unsigned)m, img, oh, ow);  // unconditional: masked lanes read out of range
         const int ih = (int)oh * a.stride + b_rr, iw = (int)ow * a.stride + b_ss;
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        rb[j] = ldg4m(a.x, (((long)img * a.H + ih) * a.W + iw) * a.C + b_c, v);
+        rb[j] = ldg4m(rx, (((long)img * a.H + ih) * a.W + iw) * a.C + b_c, v);
       }
     }
   };
@@ -487,6 +496,15 @@ static void fill_geom(ConvArgs& a, int N, int H, int W, int C, int R, int S, int
   a.fd_N = make_fastdiv(N);
 }
 
+namespace {
+int set_ranges(ConvArgs& a, long xelems, long welems) {
+  if (xelems * 4 >= (1L << 31) || welems * 4 >= (1L << 31)) return 1;
+  a.xbytes = (unsigned)(xelems * 4);
+  a.wbytes = (unsigned)(welems * 4);
+  return 0;
+}
+}  // namespace
+
 extern "C" {
 
 // effective split count the launcher will use for a reduction of `ntiles_k` BK-tiles
@@ -514,6 +532,7 @@ int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int 
   a.Nout = Kout;
   if (C % 4 || Kout % 4) return -2;
   if (dgrad && (stride != 1 || a.P != H || a.Q != W)) return -3;
+  if (set_ranges(a, (long)N * H * W * C, (long)Kout * a.Ktot)) return -5;
   const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
   a.gm = cdiv(a.M, BMv);
   a.gn = cdiv(Kout, BNv);
@@ -543,6 +562,7 @@ int dpa_conv_wgrad(const float* x, const float* dz, float* dw, float* slab, int 
   fill_geom(a, N, H, W, C, R, S, stride, pad);
   a.Nout = Kout;
   if (C % 4 || Kout % 4) return -2;
+  if (set_ranges(a, (long)N * H * W * C, (long)a.M * Kout)) return -5;
   const int BMv = tile == 0 ? 128 : 64, BNv = tile == 0 ? 128 : 64;
   a.gm = cdiv(Kout, BMv);
   a.gn = cdiv(a.Ktot, BNv);

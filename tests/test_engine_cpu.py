@@ -213,3 +213,30 @@ def test_checkpoint_roundtrip(tmp_path):
         eng.sgd_step()
         eng.finish_step()
     assert torch.allclose(e2.params.flat, e.params.flat, atol=0, rtol=0)
+
+
+def test_cifar10_binary_reader(tmp_path):
+    """The CIFAR-10 binary release layout (label byte + 3072 CHW bytes per record) is read into
+    HWC uint8 images with int64 labels; a missing dataset falls back to synthetic data."""
+    import numpy as np
+
+    from distributed_pytorch_amd.data import cifar
+
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    rng = np.random.default_rng(0)
+    recs = {}
+    for name, n in [(f"data_batch_{i}.bin", 3) for i in range(1, 6)] + [("test_batch.bin", 4)]:
+        r = rng.integers(0, 256, size=(n, 3073), dtype=np.uint8)
+        r[:, 0] = rng.integers(0, 10, size=n)
+        r.tofile(d / name)
+        recs[name] = r
+    tr = cifar.load_cifar10(str(tmp_path), True)
+    te = cifar.load_cifar10(str(tmp_path), False)
+    assert tr.images.shape == (15, 32, 32, 3) and te.images.shape == (4, 32, 32, 3)
+    r0 = recs["data_batch_1.bin"][0]
+    assert int(tr.labels[0]) == int(r0[0])
+    chw = r0[1:].reshape(3, 32, 32)
+    assert np.array_equal(tr.images[0].numpy(), chw.transpose(1, 2, 0))
+    a, b = cifar.get_datasets(str(tmp_path / "nope"), False, 64, 32)
+    assert len(a) == 64 and len(b) == 32
