@@ -108,12 +108,13 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, long elem_off, 
 
 enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
 
-// BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  k-contiguous LDS rows are
-// BK+8 bf16 long (48/80/144 B: the 16 rows of every ds_read_b128 lane group hit 16 distinct 16-B
-// slots); row-contiguous ([m][col]) rows are cols+32 bf16 (4 consecutive rows 64 B apart modulo
-// the 256-B bank row: conflict-free transpose reads).
+// BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  LDS image layouts: see the
+// APITCH/BPITCH comment in the kernel (XOR swizzles, conflict-free fragment reads).
 // NSTAGE: 2 = double-buffered LDS (one barrier per k step); 1 = single LDS stage + register
-// prefetch (two barriers per step, half the LDS -> more resident blocks to hide load latency).
+// prefetch (two barriers per step, half the LDS -> more resident blocks to hide load latency);
+// 3 = single LDS stage, two register tiles in flight; 4 = double-buffered LDS AND two register
+// tiles in flight: the ds_writes of tile t+1 and the global loads of tile t+3 are issued before
+// the MFMAs of tile t, one barrier per step (for grids too small to put 2 blocks on a CU).
 // OB: epilogue stores bf16 (round-to-nearest-even) to a.outb instead of fp32 (bf16 activations).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK, int NSTAGE, bool OB = false>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
@@ -135,15 +136,20 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
                     : (BN * CPR) % THREADS == 0 && THREADS % CPR == 0, "B slot mapping");
   // k-contiguous images are unpadded (BK bf16 per row) with the 16-B chunk index XOR-swizzled by
   // the row's position in the 256-B bank row (conflict-free ds_read_b128 fragment reads, 20 % less
-  // LDS than the old +8 padding -> more resident blocks); row-contiguous images keep +32 padding
-  constexpr int APITCH = ARC ? BM + 32 : BK;  // bf16 per LDS row
-  constexpr int BPITCH = BRC ? BN + 32 : BK;
+  // LDS than the old +8 padding -> more resident blocks).  Row-contiguous images >= 128 columns are
+  // unpadded too, with the 64-B column segment XOR-swizzled by (row & 3): the 4 rows x 64 B that a
+  // ds_read_b64_tr_b16 lane group reads land in 4 distinct bank quarters.  64-column images keep
+  // +32 bf16 of padding (rows 64 B apart modulo the bank row).
+  constexpr bool ASWZ = ARC && BM >= 128, BSWZ = BRC && BN >= 128;
+  constexpr int APITCH = ARC ? (ASWZ ? BM : BM + 32) : BK;  // bf16 per LDS row
+  constexpr int BPITCH = BRC ? (BSWZ ? BN : BN + 32) : BK;
   constexpr int RPB = 16 / CPR;  // k-contiguous rows per 256-B bank row
   auto swz = [](int row) { return (row / RPB) & (CPR - 1); };
+  auto rswz = [](int row, int col, bool on) { return on ? col ^ ((row & 3) << 5) : col; };
   constexpr int AROWS = ARC ? BK : BM, BROWS = BRC ? BK : BN;
   constexpr int A_PLANE = AROWS * APITCH, B_PLANE = BROWS * BPITCH;
   constexpr int STAGE = NP * (A_PLANE + B_PLANE);
-  __shared__ __attribute__((aligned(16))) u16 lds[(NSTAGE == 2 ? 2 : 1) * STAGE];
+  __shared__ __attribute__((aligned(16))) u16 lds[(NSTAGE == 2 || NSTAGE == 4 ? 2 : 1) * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -252,7 +258,8 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
 
   // staging registers: one set (NSTAGE 1/2) or two alternating sets (NSTAGE 3: two tiles in flight)
   uint4 ra0[NCA][NP], rb0[NCB][NP];
-  uint4 ra1[NSTAGE == 3 ? NCA : 1][NP], rb1[NSTAGE == 3 ? NCB : 1][NP];
+  constexpr bool TWO = NSTAGE >= 3;
+  uint4 ra1[TWO ? NCA : 1][NP], rb1[TWO ? NCB : 1][NP];
 
   auto load_into = [&](int v, auto& ra, auto& rb) {
     const int kb = tile_off(vbeg + v);
@@ -336,13 +343,15 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
 #pragma unroll
       for (int p = 0; p < NP; ++p)
         *reinterpret_cast<uint4*>(As + p * A_PLANE + (a_r0 + j * AROWSTEP) * APITCH +
-                                  (ARC ? a_c8 : ((a_c8 >> 3) ^ swz(a_r0 + j * AROWSTEP)) << 3)) = ra[j][p];
+                                  (ARC ? rswz(a_r0 + j * AROWSTEP, a_c8, ASWZ)
+                                       : ((a_c8 >> 3) ^ swz(a_r0 + j * AROWSTEP)) << 3)) = ra[j][p];
 #pragma unroll
     for (int j = 0; j < NCB; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p)
         *reinterpret_cast<uint4*>(Bs + p * B_PLANE + (b_r0 + j * BROWSTEP) * BPITCH +
-                                  (BRC ? b_c8 : ((b_c8 >> 3) ^ swz(b_r0 + j * BROWSTEP)) << 3)) = rb[j][p];
+                                  (BRC ? rswz(b_r0 + j * BROWSTEP, b_c8, BSWZ)
+                                       : ((b_c8 >> 3) ^ swz(b_r0 + j * BROWSTEP)) << 3)) = rb[j][p];
   };
 
   f32x16 acc[TM][TN];
@@ -361,15 +370,16 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     const uint4 v = *reinterpret_cast<const uint4*>(base + row * pitch + (((2 * ks + lh) ^ swz(row)) << 3));
     return __builtin_bit_cast(bf16x8, v);
   };
-  auto frag_r = [&](const u16* base, int pitch, int row0, int ks) -> bf16x8 {
+  auto frag_r = [&](const u16* base, int pitch, int row0, int ks, bool sw) -> bf16x8 {
     {
       const int g = lane >> 4, idx = lane & 15;
       const int q = idx >> 2, p4 = idx & 3;
       const int col = row0 + 16 * (g & 1) + 4 * p4;
       const int mrow = 16 * ks + 8 * (g >> 1) + q;
       typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + mrow * pitch + col));
-      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (mrow + 4) * pitch + col));
+      const int scol = rswz(mrow, col, sw);  // rows mrow and mrow + 4 share (row & 3)
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + mrow * pitch + scol));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (mrow + 4) * pitch + scol));
       typedef short s16x8 __attribute__((ext_vector_type(8)));
       const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       return __builtin_bit_cast(bf16x8, v);
@@ -387,7 +397,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         if constexpr (ARC)
-          fa[i][p] = frag_r(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks);
+          fa[i][p] = frag_r(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks, ASWZ);
         else
           fa[i][p] = frag_k(As + p * A_PLANE, APITCH, wr * WTM + i * 32, ks);
       }
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         if constexpr (BRC)
-          fb[j][p] = frag_r(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
+          fb[j][p] = frag_r(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks, BSWZ);
         else
           fb[j][p] = frag_k(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
       }
@@ -420,7 +430,30 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   auto load_tile = [&](int v) { load_into(v, ra0, rb0); };
   auto store_tile = [&](int stage) { store_from(stage, ra0, rb0); };
 
-  if (NSTAGE == 3 && ntiles > 0) {
+  if (NSTAGE == 4 && ntiles > 0) {
+    // LDS stage t & 1 holds tile t; ra0/rb0 carry the even tiles, ra1/rb1 the odd ones
+    load_into(0, ra0, rb0);
+    if (1 < ntiles) load_into(1, ra1, rb1);
+    store_from(0, ra0, rb0);
+    if (2 < ntiles) load_into(2, ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; kt += 2) {
+      if (kt + 1 < ntiles) {
+        store_from(1, ra1, rb1);
+        if (kt + 3 < ntiles) load_into(kt + 3, ra1, rb1);
+      }
+      compute_tile(0);
+      __syncthreads();
+      if (kt + 1 < ntiles) {
+        if (kt + 2 < ntiles) {
+          store_from(0, ra0, rb0);
+          if (kt + 4 < ntiles) load_into(kt + 4, ra0, rb0);
+        }
+        compute_tile(1);
+        __syncthreads();
+      }
+    }
+  } else if (NSTAGE == 3 && ntiles > 0) {
     // single LDS stage, two register tiles in flight: while tile t is consumed from LDS, tiles
     // t+1 and t+2 are loading (uses the VGPR headroom left by the LDS-limited occupancy)
     load_into(0, ra0, rb0);
@@ -555,6 +588,8 @@ int launch_x3(const Args& a, hipStream_t st) {
 //   4: 128x128/k16/1  5: 128x128/k32/1  6: 64x64/k32/1  7: 256x128/k32/1 (8 waves)
 //   8-11: the 128x128/k32, 128x128/k16, 256x128/k32, 64x64/k32 single-stage tiles with two register
 //   tiles in flight (NSTAGE 3)
+//   12-15: 128x128/k32, 128x128/k16, 256x128/k32, 64x64/k32 double-buffered with two register
+//   tiles in flight (NSTAGE 4)
 template <int MODE, int NP, bool OB = false>
 int launch_tile(const Args& a, int tile, hipStream_t st) {
   switch (tile) {
@@ -563,6 +598,10 @@ int launch_tile(const Args& a, int tile, hipStream_t st) {
     case 9: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 3, OB>(a, st);
     case 10: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 3, OB>(a, st);
     case 11: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 3, OB>(a, st);
+    case 12: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 4, OB>(a, st);
+    case 13: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 4, OB>(a, st);
+    case 14: return launch_x3<256, 128, 4, 2, MODE, NP, 32, 4, OB>(a, st);
+    case 15: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 4, OB>(a, st);
     case 0: return launch_x3<128, 128, 2, 2, MODE, NP, 32, 2, OB>(a, st);
     case 1: return launch_x3<64, 64, 1, 2, MODE, NP, 32, 2, OB>(a, st);
     case 2: return launch_x3<128, 128, 2, 2, MODE, NP, 16, 2, OB>(a, st);
@@ -579,10 +618,9 @@ int launch_any(const Args& a, int tile, int np, int obf, hipStream_t st) {
   if (obf) return launch_tile<MODE, 1, true>(a, tile, st);
   return np == 3 ? launch_tile<MODE, 3>(a, tile, st) : launch_tile<MODE, 1>(a, tile, st);
 }
-int tile_rows(int tile) {
-  return (tile == 1 || tile == 3 || tile == 6 || tile == 11) ? 64 : ((tile == 7 || tile == 10) ? 256 : 128);
-}
-int tile_cols(int tile) { return (tile == 1 || tile == 3 || tile == 6 || tile == 11) ? 64 : 128; }
+bool small_tile(int tile) { return tile == 1 || tile == 3 || tile == 6 || tile == 11 || tile == 15; }
+int tile_rows(int tile) { return small_tile(tile) ? 64 : ((tile == 7 || tile == 10 || tile == 14) ? 256 : 128); }
+int tile_cols(int tile) { return small_tile(tile) ? 64 : 128; }
 
 int grid_1d(long n) {
   long g = (n + 255) / 256;

@@ -357,7 +357,7 @@ class VGGEngine:
 
     def conv_candidates(self, i: int, kind: str):
         impl = self._layer_impl(i)
-        tiles = (0, 1) if impl == "fp32" else tuple(range(12))
+        tiles = (0, 1) if impl == "fp32" else tuple(range(16))
         splits = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if kind == "wgrad" else (1, 2, 4, 8, 16)
         return [(t, s, pm) for t in tiles for s in splits for pm in (False, True)]
 

@@ -77,7 +77,7 @@ TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file
 _table: Optional[Dict[str, list]] = None
 _chosen: Dict[str, Tuple[int, int, bool]] = {}
 _AUTOTUNE = {"on": os.environ.get("DPA_AUTOTUNE", "0") == "1", "dirty": False}
-N_TILES = 12
+N_TILES = 16
 
 
 def set_autotune(on: bool):

@@ -162,7 +162,7 @@ def test_split_planes_exact():
 
 @pytest.mark.parametrize("shape", X3_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", list(range(12)))
+@pytest.mark.parametrize("tile", list(range(16)))
 @pytest.mark.parametrize("posmajor", [False, True])
 @pytest.mark.parametrize("np_", [3, 1])
 def test_conv_x3_fprop(shape, splits, tile, posmajor, np_):
@@ -191,7 +191,7 @@ X3_DGRAD_SHAPES = X3_SHAPES + [
 
 @pytest.mark.parametrize("shape", X3_DGRAD_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", [0, 1, 5, 6, 7, 8, 11])
+@pytest.mark.parametrize("tile", [0, 1, 5, 6, 7, 8, 11, 12, 14, 15])
 @pytest.mark.parametrize("posmajor", [False, True])
 @pytest.mark.parametrize("np_", [3, 1])
 def test_conv_x3_dgrad(shape, splits, tile, posmajor, np_):
@@ -232,7 +232,7 @@ def test_conv_x3_planes_as_arena_views():
 
 @pytest.mark.parametrize("shape", X3_SHAPES)
 @pytest.mark.parametrize("splits", [1, 7])
-@pytest.mark.parametrize("tile", list(range(12)))
+@pytest.mark.parametrize("tile", list(range(16)))
 @pytest.mark.parametrize("posmajor", [False, True])
 @pytest.mark.parametrize("np_", [3, 1])
 def test_conv_x3_wgrad(shape, splits, tile, posmajor, np_):
