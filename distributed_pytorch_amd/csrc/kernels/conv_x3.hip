@@ -532,6 +532,477 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     }
 }
 
+// ---------------- halo-staged direct 3x3 convolution (stride 1, pad 1) ----------------
+// conv_x3_kernel gathers its A operand afresh for every filter tap: each input pixel crosses the
+// L2 -> CU path once per tap and per column tile, and that gather traffic -- not the matrix cores
+// -- bounds it (the one-plane bf16 build streams operand bytes at the same rate as x3).  Here a
+// block owns BM consecutive output pixels (NHWC order).  Per chunk of BC reduction channels it
+// stages the pixel range [m0 - W - 1, m0 + BM + W + 1) ONCE into LDS -- the block's pixels plus
+// one image row and one pixel of halo on each side -- and one zero slot, then runs the 9 taps
+// against shifted views of that image: tap (r, s) of local pixel m reads slot m + r*W + s, or the
+// zero slot when (y + r - 1, x + s - 1) leaves the image.  Only the per-tap weight tile streams
+// (double-buffered LDS, one barrier per tap).  A is loaded once per chunk instead of 9 times.
+//   FPROP  out[p][n] = sum_{tap,c} x[p + d(tap)][c] * W[n][tap][c]
+//   DGRAD  dx[p][c]  = sum_{tap,k} dz[p + d(tap)][k] * W[k][8 - tap][c]   (stride 1: the flipped
+//          weights are read in place, row-contiguous, fragments through ds_read_b64_tr_b16)
+// Operand planes, plane products, split-K slabs (a split without chunks writes zeros) and the
+// epilogue are those of conv_x3_kernel; output rows are NHWC pixel indices.
+struct HArgs {
+  const u16* x;  // A planes [NP][N,H,W,C] (DGRAD: dz)
+  long xps;
+  unsigned xbytes;
+  const u16* w;  // weight planes [Kf][3][3][Cf]
+  long wps;
+  unsigned wbytes;
+  float* out;  // [N,H,W,Nout] fp32, or split-K slabs
+  u16* outb;   // bf16 output (OB)
+  long slab;
+  int N, H, W, C, Nout, M;  // C: reduction channels
+  int gm, gn, cps;          // row / column tiles, reduction chunks per split
+};
+
+// staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
+__host__ __device__ constexpr int halo_slots(int BM) { return BM + BM / 2 + 1; }
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, bool OB>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs a) {
+  constexpr int THREADS = WAVES_M * WAVES_N * 64;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
+  constexpr int CPR = BC / 8;    // 16-B chunks per staged row
+  constexpr int RPB = 16 / CPR;  // staged rows per 256-B bank row
+  constexpr int SLOTS = halo_slots(BM), ZS = SLOTS - 1;
+  constexpr int A_PLANE = SLOTS * BC;
+  constexpr bool BSWZ = DG && BN >= 128;
+  constexpr int BPITCH = DG ? (BSWZ ? BN : BN + 32) : BC;
+  constexpr int B_PLANE = (DG ? BC : BN) * BPITCH;
+  constexpr int ACH = SLOTS * CPR;                  // 16-B chunks per plane of the staged image
+  constexpr int BCH = DG ? BC * BN / 8 : BN * CPR;  // ... of one tap's weight tile
+  constexpr int NCA = (ACH + THREADS - 1) / THREADS;
+  constexpr int NCB = (BCH + THREADS - 1) / THREADS;
+  __shared__ __attribute__((aligned(16))) u16 lds[NP * A_PLANE + 2 * NP * B_PLANE];
+  u16* const As = lds;
+  u16* const Bs = lds + NP * A_PLANE;
+  auto swz = [](int row) { return (row / RPB) & (CPR - 1); };
+  auto rswz = [](int row, int col) { return BSWZ ? col ^ ((row & 3) << 5) : col; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WAVES_N, wc = wid % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+  const int tile = xcd_remap(blockIdx.x, a.gm * a.gn);
+  const int bm = tile / a.gn, bn = tile % a.gn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int HW = a.H * a.W;
+  const int nst = BM + 2 * a.W + 2;  // staged pixels: slot j holds pixel m0 - W - 1 + j
+
+  __amdgpu_buffer_rsrc_t rx[NP], rw[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    rx[p] = plane_rsrc(a.x + p * a.xps, a.xbytes);
+    rw[p] = plane_rsrc(a.w + p * a.wps, a.wbytes);
+  }
+
+  // staging slots: chunk q = tid + j * THREADS is 16-B piece q % CPR of slot q / CPR
+  long a_off[NCA];
+  bool a_ok[NCA];
+#pragma unroll
+  for (int j = 0; j < NCA; ++j) {
+    const int q = tid + j * THREADS;
+    const int slot = q / CPR, cc = q - slot * CPR;
+    const int gp = m0 - a.W - 1 + slot;
+    a_ok[j] = slot < nst && gp >= 0 && gp < a.M;
+    a_off[j] = (long)gp * a.C + cc * 8;
+  }
+  // weight staging (one tap tile): FPROP rows n with pieces along c; DGRAD rows k of the chunk
+  // with pieces along the output channel
+  long b_off[NCB];
+  bool b_ok[NCB];
+#pragma unroll
+  for (int j = 0; j < NCB; ++j) {
+    const int q = tid + j * THREADS;
+    if constexpr (DG) {
+      const int k = q / (BN / 8), col = (q - k * (BN / 8)) * 8;
+      b_ok[j] = q < BCH && n0 + col < a.Nout;
+      b_off[j] = (long)k * 9 * a.Nout + n0 + col;
+    } else {
+      const int n = q / CPR, cc = q - n * CPR;
+      b_ok[j] = q < BCH && n0 + n < a.Nout;
+      b_off[j] = (long)(n0 + n) * 9 * a.C + cc * 8;
+    }
+  }
+
+  uint4 ra[NCA][NP], rb[NCB][NP];
+  auto load_a = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < NCA; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) ra[j][p] = bload(rx[p], a_off[j] + c0, a_ok[j]);
+  };
+  auto store_a = [&]() {
+#pragma unroll
+    for (int j = 0; j < NCA; ++j) {
+      const int q = tid + j * THREADS;
+      const int slot = q / CPR, cc = q - slot * CPR;
+      if ((ACH % THREADS == 0 || q < ACH) && (slot < nst || slot == ZS)) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          *reinterpret_cast<uint4*>(As + p * A_PLANE + slot * BC + ((cc ^ swz(slot)) << 3)) = ra[j][p];
+      }
+    }
+  };
+  auto load_b = [&](int tap, int c0) {
+    const long d = DG ? ((long)c0 * 9 + 8 - tap) * a.Nout : (long)tap * a.C + c0;
+#pragma unroll
+    for (int j = 0; j < NCB; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rb[j][p] = bload(rw[p], b_off[j] + d, b_ok[j]);
+  };
+  auto store_b = [&](int stage) {
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+      const int q = tid + j * THREADS;
+      if (BCH % THREADS == 0 || q < BCH) {
+        int idx;
+        if constexpr (DG) {
+          const int k = q / (BN / 8), col = (q - k * (BN / 8)) * 8;
+          idx = k * BPITCH + rswz(k, col);
+        } else {
+          const int n = q / CPR, cc = q - n * CPR;
+          idx = n * BC + ((cc ^ swz(n)) << 3);
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<uint4*>(Bs + (stage * NP + p) * B_PLANE + idx) = rb[j][p];
+      }
+    }
+  };
+
+  // A fragment rows: local pixel m at image position (y, x)
+  int fr_m[TM], fr_y[TM], fr_x[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wr * WTM + i * 32 + li;
+    const int pix = (m0 + m) % HW;
+    fr_m[i] = m;
+    fr_y[i] = pix / a.W;
+    fr_x[i] = pix - fr_y[i] * a.W;
+  }
+
+  auto frag_k = [&](const u16* base, int row, int ks) -> bf16x8 {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + row * BC + (((2 * ks + lh) ^ swz(row)) << 3));
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto frag_r = [&](const u16* base, int col0, int ks) -> bf16x8 {
+    const int g = lane >> 4, idx = lane & 15;
+    const int q = idx >> 2, p4 = idx & 3;
+    const int col = col0 + 16 * (g & 1) + 4 * p4;
+    const int krow = 16 * ks + 8 * (g >> 1) + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const int scol = rswz(krow, col);  // rows krow and krow + 4 share (row & 3)
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + krow * BPITCH + scol));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (krow + 4) * BPITCH + scol));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int tap, int stage) {
+    const int r = tap / 3, s = tap - 3 * (tap / 3);
+    int sl[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const bool v = (unsigned)(fr_y[i] + r - 1) < (unsigned)a.H && (unsigned)(fr_x[i] + s - 1) < (unsigned)a.W;
+      sl[i] = v ? fr_m[i] + r * a.W + s : ZS;
+    }
+    const u16* Bst = Bs + stage * NP * B_PLANE;
+#pragma unroll
+    for (int ks = 0; ks < BC / 16; ++ks) {
+      bf16x8 fa[TM][NP], fb[TN][NP];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fa[i][p] = frag_k(As + p * A_PLANE, sl[i], ks);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          if constexpr (DG)
+            fb[j][p] = frag_r(Bst + p * B_PLANE, wc * WTN + j * 32, ks);
+          else
+            fb[j][p] = frag_k(Bst + p * B_PLANE, wc * WTN + j * 32 + li, ks);
+        }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (NP == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  // ---- main loop: step = (chunk, tap).  The weight tile of step st+1 is written to the other
+  // buffer after step st's MFMAs (its loads were issued a step earlier); the next chunk's pixels
+  // sit in registers during the 9 taps and replace the staged image at the chunk boundary.
+  const int nch = a.C / BC;
+  const int cb = blockIdx.y * a.cps, ce = min(nch, cb + a.cps);
+  const int nsteps = max(0, ce - cb) * 9;
+  if (nsteps > 0) {
+    load_a(cb * BC);
+    load_b(0, cb * BC);
+    store_a();
+    store_b(0);
+    if (nsteps > 1) load_b(1, cb * BC);
+    if (cb + 1 < ce) load_a((cb + 1) * BC);
+    __syncthreads();
+    int tap = 0, ch = cb;
+    for (int st = 0; st < nsteps; ++st) {
+      compute(tap, st & 1);
+      const bool last_tap = tap == 8;
+      const int tap1 = last_tap ? 0 : tap + 1, ch1 = last_tap ? ch + 1 : ch;  // step st + 1
+      if (st + 1 < nsteps) {
+        store_b((st + 1) & 1);
+        if (st + 2 < nsteps) load_b(tap1 == 8 ? 0 : tap1 + 1, (tap1 == 8 ? ch1 + 1 : ch1) * BC);
+        if (last_tap) {  // every wave is done with this chunk's image before it is replaced
+          __syncthreads();
+          store_a();
+          if (ch + 2 < ce) load_a((ch + 2) * BC);
+        }
+      }
+      __syncthreads();
+      tap = tap1;
+      ch = ch1;
+    }
+  }
+
+  // ---------------- epilogue (rows are NHWC pixels) ----------------
+  float* out = a.out + (long)blockIdx.y * a.slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc * WTN + j * 32 + li;
+      if (col < a.Nout) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M) {
+            if constexpr (OB)
+              a.outb[(long)row * a.Nout + col] = bf16_rne(acc[i][j][r]);
+            else
+              out[(long)row * a.Nout + col] = acc[i][j][r];
+          }
+        }
+      }
+    }
+}
+
+// ---------------- halo-staged 3x3 weight gradient (stride 1, pad 1) ----------------
+// dW[k][tap][c] = sum_p dZ[p][k] * X[p + d(tap)][c].  A block owns a 128 (k) x 32 (c) tile of all
+// 9 taps -- four waves, each a 32-row k slice with nine accumulators -- and reduces over chunks of
+// P consecutive pixels.  Per chunk it stages dZ [P][128] and the X halo image (pixels
+// [pb - W - 1, pb + P + W + 1) and a zero slot) once, double-buffered, fetches each dZ^T fragment
+// once per k-step and reuses it for all 9 taps.  Both images are row-contiguous and read with
+// ds_read_b64_tr_b16; the X rows are per-lane slot addresses (the tap shift, or the zero slot),
+// so the 9-fold im2col re-gather of conv_x3_kernel's WGRAD is gone.
+struct WHArgs {
+  const u16* x;  // X planes [NP][N,H,W,C]
+  long xps;
+  unsigned xbytes;
+  const u16* dz;  // dZ planes [NP][N,H,W,K]
+  long dzps;
+  unsigned dzbytes;
+  float* out;  // dW [K][3][3][C] fp32, or split-K slabs
+  long slab;
+  int N, H, W, C, K, M;
+  int gk, gc, nchunks, cps;
+  FastDiv fd_HW, fd_W;
+};
+
+__host__ __device__ constexpr int halo_wslots(int P) { return 2 * P + 4; }  // P + 2W + 2 (W <= P/2) + zero slot
+
+template <int NP, int P>
+__global__ __launch_bounds__(256) void conv_halo_wgrad_kernel(WHArgs a) {
+  constexpr int THREADS = 256, BKO = 128, BCW = 32;
+  constexpr int SLOTS = halo_wslots(P), ZS = SLOTS - 1;
+  constexpr int Z_PLANE = P * BKO, X_PLANE = SLOTS * BCW;
+  constexpr int STAGE = NP * (Z_PLANE + X_PLANE);
+  constexpr int ZCH = P * BKO / 8, XCH = SLOTS * BCW / 8;  // 16-B pieces per plane
+  constexpr int NZ = (ZCH + THREADS - 1) / THREADS, NX = (XCH + THREADS - 1) / THREADS;
+  constexpr int KS = P / 16;
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int tile = xcd_remap(blockIdx.x, a.gk * a.gc);
+  const int bk = tile / a.gc, bcol = tile - bk * a.gc;
+  const int k0 = bk * BKO, c0 = bcol * BCW;
+  const int cb = blockIdx.y * a.cps, ce = min(a.nchunks, cb + a.cps);
+  const int nst = P + 2 * a.W + 2;
+
+  __amdgpu_buffer_rsrc_t rx[NP], rz[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    rx[p] = plane_rsrc(a.x + p * a.xps, a.xbytes);
+    rz[p] = plane_rsrc(a.dz + p * a.dzps, a.dzbytes);
+  }
+
+  uint4 rzr[NZ][NP], rxr[NX][NP];
+  auto load_chunk = [&](int ch) {
+    const int pb = ch * P;
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int qq = tid + j * THREADS;
+      const int prow = qq / (BKO / 8), col = (qq % (BKO / 8)) * 8;
+      const bool v = (ZCH % THREADS == 0 || qq < ZCH) && pb + prow < a.M && k0 + col < a.K;
+      const long off = (long)(pb + prow) * a.K + k0 + col;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rzr[j][p] = bload(rz[p], off, v);
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int qq = tid + j * THREADS;
+      const int slot = qq >> 2, cc = qq & 3;
+      const int gp = pb - a.W - 1 + slot;
+      const bool v = slot < nst && gp >= 0 && gp < a.M && c0 + cc * 8 < a.C;
+      const long off = (long)gp * a.C + c0 + cc * 8;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rxr[j][p] = bload(rx[p], off, v);
+    }
+  };
+  auto store_chunk = [&](int stage) {
+    u16* Zs = lds + stage * STAGE;
+    u16* Xs = Zs + NP * Z_PLANE;
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int qq = tid + j * THREADS;
+      if (ZCH % THREADS == 0 || qq < ZCH) {
+        const int prow = qq / (BKO / 8), col = (qq % (BKO / 8)) * 8;
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          *reinterpret_cast<uint4*>(Zs + p * Z_PLANE + prow * BKO + (col ^ ((prow & 3) << 5))) = rzr[j][p];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int qq = tid + j * THREADS;
+      const int slot = qq >> 2;
+      if ((XCH % THREADS == 0 || qq < XCH) && (slot < nst || slot == ZS)) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<uint4*>(Xs + p * X_PLANE + qq * 8) = rxr[j][p];
+      }
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  const int zc = wid * 32 + 16 * (g & 1) + 4 * p4;  // dZ column (k) this lane addresses
+  const int xc = 16 * (g & 1) + 4 * p4;             // X column (c)
+  auto compute = [&](int stage, int pb) {
+    const u16* Zs = lds + stage * STAGE;
+    const u16* Xs = Zs + NP * Z_PLANE;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int zr = 16 * ks + 8 * (g >> 1) + q;  // reduction rows zr (lo) and zr + 4 (hi)
+      bf16x8 fa[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const u16* zb = Zs + p * Z_PLANE + (zc ^ ((zr & 3) << 5));
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(zb + zr * BKO));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(zb + (zr + 4) * BKO));
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fa[p] = __builtin_bit_cast(bf16x8, v);
+      }
+      // image positions of the two pixels this lane addresses
+      int py[2], px[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const unsigned gp = (unsigned)(pb + zr + 4 * h2);
+        const unsigned img = fdiv(gp, a.fd_HW);
+        const unsigned pix = gp - img * (unsigned)(a.H * a.W);
+        const unsigned y = fdiv(pix, a.fd_W);
+        py[h2] = (int)y;
+        px[h2] = (int)(pix - y * (unsigned)a.W);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        int sl[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const bool v = (unsigned)(py[h2] + r - 1) < (unsigned)a.H && (unsigned)(px[h2] + s - 1) < (unsigned)a.W;
+          sl[h2] = v ? zr + 4 * h2 + r * a.W + s : ZS;
+        }
+        bf16x8 fb[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const u16* xb = Xs + p * X_PLANE + xc;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb + sl[0] * BCW));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb + sl[1] * BCW));
+          const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          fb[p] = __builtin_bit_cast(bf16x8, v);
+        }
+        if constexpr (NP == 3) {
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[tap], 0, 0, 0);
+        }
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[tap], 0, 0, 0);
+      }
+    }
+  };
+
+  if (ce > cb) {
+    load_chunk(cb);
+    store_chunk(0);
+    if (cb + 1 < ce) load_chunk(cb + 1);
+    __syncthreads();
+    for (int ch = cb; ch < ce; ++ch) {
+      const int st = (ch - cb) & 1;
+      compute(st, ch * P);
+      if (ch + 1 < ce) {
+        store_chunk(st ^ 1);
+        if (ch + 2 < ce) load_chunk(ch + 2);
+      }
+      __syncthreads();
+    }
+  }
+
+  float* out = a.out + (long)blockIdx.y * a.slab;
+  const int col = c0 + li;
+  if (col < a.C) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = k0 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.K) out[((long)row * 9 + t) * a.C + col] = acc[t][r];
+      }
+  }
+}
 
 // ---------------- fp32 -> bf16 planes ----------------
 // x [n] fp32 -> planes [NP][n] (n % 4 == 0)
@@ -663,6 +1134,94 @@ int xsplits(int Kred, int splits) {
   return splits < 1 ? 1 : splits;
 }
 
+// ---- halo tiles: ids 16-19 follow the 16 implicit-GEMM tiles (3x3, stride 1, pad 1 only) ----
+//   FPROP / DGRAD: 16 = 256x128 with 16-channel chunks (8 waves), 17 = 256x128 / 32,
+//                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32
+//   WGRAD:         16 = 64-pixel chunks, 17 = 32-pixel chunks
+bool is_halo(int tile) { return tile >= 16 && tile <= 19; }
+int halo_bm(int tile) { return tile <= 17 ? 256 : 128; }
+int halo_bc(int tile) { return (tile & 1) ? 32 : 16; }
+
+template <int BM, int BN, int WM, int WN, bool DG, int NP, int BC, bool OB>
+int launch_halo(const HArgs& a, int splits, hipStream_t st) {
+  dim3 grid(a.gm * a.gn, splits);
+  conv_halo_kernel<BM, BN, WM, WN, DG, NP, BC, OB><<<grid, WM * WN * 64, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+template <bool DG, int NP, bool OB>
+int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
+  switch (tile) {
+    case 16: return launch_halo<256, 128, 4, 2, DG, NP, 16, OB>(a, splits, st);
+    case 17: return launch_halo<256, 128, 4, 2, DG, NP, 32, OB>(a, splits, st);
+    case 18: return launch_halo<128, 128, 2, 2, DG, NP, 16, OB>(a, splits, st);
+    default: return launch_halo<128, 128, 2, 2, DG, NP, 32, OB>(a, splits, st);
+  }
+}
+
+// -6: the conv does not fit the halo tile (channels, or rows wider than BM/4 - 1 pixels)
+template <bool DG>
+int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st) {
+  const int BM = halo_bm(tile), BC = halo_bc(tile);
+  if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM) - 1) return -6;
+  if (obf && (np != 1 || (splits > 1 && !reduce))) return -4;
+  a.M = a.N * a.H * a.W;
+  a.gm = cdiv(a.M, BM);
+  a.gn = cdiv(a.Nout, 128);
+  a.cps = cdiv(a.C / BC, splits);
+  a.out = splits > 1 ? slab : (float*)out;
+  a.outb = (u16*)out;
+  a.slab = splits > 1 ? (long)a.M * a.Nout : 0;
+  int rc;
+  if (obf && splits == 1)
+    rc = launch_halo_tile<DG, 1, true>(a, tile, splits, st);
+  else if (np == 3)
+    rc = launch_halo_tile<DG, 3, false>(a, tile, splits, st);
+  else
+    rc = launch_halo_tile<DG, 1, false>(a, tile, splits, st);
+  if (rc || splits == 1 || !reduce) return rc;
+  const long n4 = (long)a.M * a.Nout / 4;
+  if (obf) return launch_splitk_reduce_t(slab, (ushort4*)out, n4, splits, st);
+  return launch_splitk_reduce(slab, (float*)out, n4, splits, st);
+}
+
+int halo_bytes(unsigned& xb, long xel, unsigned& wb, long wel) {
+  if (xel * 2 >= (1L << 31) || wel * 2 >= (1L << 31)) return -5;
+  xb = (unsigned)(xel * 2);
+  wb = (unsigned)(wel * 2);
+  return 0;
+}
+
+template <int NP, int P>
+int launch_halo_wgrad(const WHArgs& a, int splits, hipStream_t st) {
+  dim3 grid(a.gk * a.gc, splits);
+  conv_halo_wgrad_kernel<NP, P><<<grid, 256, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+int run_halo_wgrad(WHArgs& a, int tile, int splits, int np, float* dw, float* slab, hipStream_t st) {
+  if (tile != 16 && tile != 17) return -6;
+  const int P = tile == 16 ? 64 : 32;
+  if (a.C % 8 || a.K % 8 || P + 2 * a.W + 2 > halo_wslots(P) - 1) return -6;
+  a.M = a.N * a.H * a.W;
+  if (halo_bytes(a.xbytes, (long)a.M * a.C, a.dzbytes, (long)a.M * a.K)) return -5;
+  a.nchunks = cdiv(a.M, P);
+  a.gk = cdiv(a.K, 128);
+  a.gc = cdiv(a.C, 32);
+  a.cps = cdiv(a.nchunks, splits);
+  a.fd_HW = make_fastdiv(a.H * a.W);
+  a.fd_W = make_fastdiv(a.W);
+  a.out = splits > 1 ? slab : dw;
+  a.slab = splits > 1 ? (long)a.K * 9 * a.C : 0;
+  int rc;
+  if (np == 3)
+    rc = P == 64 ? launch_halo_wgrad<3, 64>(a, splits, st) : launch_halo_wgrad<3, 32>(a, splits, st);
+  else
+    rc = P == 64 ? launch_halo_wgrad<1, 64>(a, splits, st) : launch_halo_wgrad<1, 32>(a, splits, st);
+  if (rc || splits == 1) return rc;
+  return launch_splitk_reduce(slab, dw, (long)a.K * 9 * a.C / 4, splits, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -675,6 +1234,21 @@ int dpa_x3_splits(int Kred, int splits) { return xsplits(Kred, splits); }
 int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
                       int posmajor, int np, int obf, hipStream_t st) {
+  if (is_halo(tile)) {
+    if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
+    HArgs h{};
+    h.x = x;
+    h.xps = xps;
+    h.w = w;
+    h.wps = wps;
+    h.N = N;
+    h.H = H;
+    h.W = W;
+    h.C = C;
+    h.Nout = Kout;
+    if (halo_bytes(h.xbytes, (long)N * H * W * C, h.wbytes, (long)Kout * 9 * C)) return -5;
+    return run_halo<false>(h, tile, xsplits(9 * C, splits), np, obf, slab, out, reduce, st);
+  }
   Args a{};
   a.x = x;
   a.xps = xps;
@@ -708,6 +1282,21 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
 int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx, float* slab, int N, int Hd, int Wd,
                       int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
                       int posmajor, int np, int obf, hipStream_t st) {
+  if (is_halo(tile)) {
+    if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
+    HArgs h{};
+    h.x = dz;
+    h.xps = dzps;
+    h.w = w;
+    h.wps = wps;
+    h.N = N;
+    h.H = H;
+    h.W = W;
+    h.C = K;
+    h.Nout = C;
+    if (halo_bytes(h.xbytes, (long)N * H * W * K, h.wbytes, (long)K * 9 * C)) return -5;
+    return run_halo<true>(h, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st);
+  }
   Args a{};
   a.x = dz;
   a.xps = dzps;
@@ -747,6 +1336,20 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
 int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* dw, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int posmajor, int np,
                       hipStream_t st) {
+  if (is_halo(tile)) {
+    if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
+    WHArgs h{};
+    h.x = x;
+    h.xps = xps;
+    h.dz = dz;
+    h.dzps = dzps;
+    h.N = N;
+    h.H = H;
+    h.W = W;
+    h.C = C;
+    h.K = Kout;
+    return run_halo_wgrad(h, tile, xsplits(N * H * W, splits), np, dw, slab, st);
+  }
   Args a{};
   a.x = x;
   a.xps = xps;

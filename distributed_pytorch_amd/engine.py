@@ -91,6 +91,25 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
     return f"{impl}|{kind}|{n}|{hw}|{cin}|{cout}"
 
 
+# Halo-staged 3x3/s1/p1 tiles of conv_x3.hip (ids after the 16 implicit-GEMM tiles): the block's
+# input pixels are staged once per channel chunk and the 9 taps read shifted views of them.
+HALO_TILES = (16, 17, 18, 19)        # fprop / dgrad: 256 or 128 pixels x 128 channels, 16 or 32-channel chunks
+HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
+
+
+def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
+    """Whether halo tile `tile` runs conv call `kind` of a 3x3/s1/p1 conv whose rows are w pixels
+    wide.  cred: channels reduced (fprop C_in, dgrad C_out; wgrad C_in), cout: output channels
+    (wgrad C_out).  Mirrors run_halo / run_halo_wgrad in conv_x3.hip (-6 otherwise)."""
+    if kind == "wgrad":
+        p = {16: 64, 17: 32}.get(tile)
+        return p is not None and cred % 8 == 0 and cout % 8 == 0 and p + 2 * w + 2 <= 2 * p + 3
+    if tile not in HALO_TILES:
+        return False
+    bm, bc = (256 if tile <= 17 else 128), (32 if tile & 1 else 16)
+    return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= bm + bm // 2
+
+
 class VGGEngine:
     """Static-schedule trainer.  ``impl`` selects the conv kernels of every layer whose input has a
     multiple of 8 channels (the 3-channel first layer always runs the fp32-MFMA kernel):
@@ -177,12 +196,20 @@ class VGGEngine:
             M, Mo = N * hw * hw, N * ho * ho
             part_need = max(part_need, self.K.bn_part_floats(M, l.cout, False),
                             self.K.bn_part_floats(Mo, l.cout, True))
+        # Weight gradients run on a second HIP stream (DPA_WGRAD_STREAM=0: one stream): wgrad(i) needs
+        # only dz(i) and the stored forward activation, so it runs beside dgrad(i) and the BN
+        # backward of layer i-1, whose reduce/finalize kernels leave most CUs idle.  It has its own
+        # split-K workspace.
+        self.wstream = (torch.cuda.Stream(dev) if dev.type == "cuda" and os.environ.get("DPA_WGRAD_STREAM", "1") == "1"
+                        else None)
+        self._wev = [torch.cuda.Event() for _ in L] if self.wstream is not None else None
         self.slab = torch.empty(1, **f32)
-        for i in range(len(L)):  # size the split-K workspace for the full-batch plan
+        self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
+        for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
             for kind in ("fprop", "dgrad", "wgrad"):
                 if kind == "dgrad" and i == 0:
                     continue
-                self._ensure_slab(self._slab_need(i, kind, N))
+                self._ensure_slab(self._slab_need(i, kind, N), wgrad=kind == "wgrad")
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -357,9 +384,18 @@ class VGGEngine:
 
     def conv_candidates(self, i: int, kind: str):
         impl = self._layer_impl(i)
+        l = self.spec.convs[i]
         tiles = (0, 1) if impl == "fp32" else tuple(range(16))
         splits = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if kind == "wgrad" else (1, 2, 4, 8, 16)
-        return [(t, s, pm) for t in tiles for s in splits for pm in (False, True)]
+        out = [(t, s, pm) for t in tiles for s in splits for pm in (False, True)]
+        if impl != "fp32":  # halo tiles ignore the row order flag
+            if kind == "wgrad":
+                ok = [t for t in HALO_WGRAD_TILES if halo_ok(kind, t, l.hw, l.cin_pad, l.cout)]
+            else:
+                cred, cout = (l.cin_pad, l.cout) if kind == "fprop" else (l.cout, l.cin_pad)
+                ok = [t for t in HALO_TILES if halo_ok(kind, t, l.hw, cred, cout)]
+            out += [(t, s, False) for t in ok for s in splits]
+        return out
 
     def autotune(self, n: Optional[int] = None, iters: int = 3, verbose: bool = False) -> Dict[str, list]:
         """Time every candidate (tile, splits, posmajor) of every conv call of the step at batch n on
@@ -403,8 +439,11 @@ class VGGEngine:
                     print(ck, best, flush=True)
         return res
 
-    def _ensure_slab(self, numel: int):
-        if numel > self.slab.numel():
+    def _ensure_slab(self, numel: int, wgrad: bool = False):
+        if wgrad and self.wslab is not None:
+            if numel > self.wslab.numel():
+                self.wslab = torch.empty(numel, device=self.device, dtype=torch.float32)
+        elif numel > self.slab.numel():
             self.slab = torch.empty(numel, device=self.device, dtype=torch.float32)
 
     def _in_planes(self, i: int, n: int) -> torch.Tensor:
@@ -442,8 +481,8 @@ class VGGEngine:
     def _conv_wgrad(self, i: int, x: torch.Tensor, n: int):
         l = self.spec.convs[i]
         tile, s, pm = self.conv_config(i, "wgrad", n)
-        self._ensure_slab(self._slab_need(i, "wgrad", n))
-        slab = self.slab if s > 1 else None
+        self._ensure_slab(self._slab_need(i, "wgrad", n), wgrad=True)
+        slab = (self.wslab if self.wslab is not None else self.slab) if s > 1 else None
         dw = self.grads[f"{l.conv_key}.weight"]
         if self.planes[i]:
             self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
@@ -486,6 +525,8 @@ class VGGEngine:
         if grad_ready is not None:
             grad_ready(["fc1.weight", "fc1.bias"])
         gsplit = 1  # split-K slabs of g[i] left unreduced by the previous dgrad (summed inside bn_bwd)
+        ws = self.wstream
+        main = torch.cuda.current_stream(self.device) if ws is not None else None
         for i in range(len(L) - 1, -1, -1):
             l = L[i]
             st = self.stats[i]
@@ -495,12 +536,29 @@ class VGGEngine:
             K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                      st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
                      G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool)
-            # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early
-            self._conv_wgrad(i, x, n)
-            if grad_ready is not None:
-                grad_ready([f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"])
+            names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
+            if ws is None:
+                # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early
+                self._conv_wgrad(i, x, n)
+                if grad_ready is not None:
+                    grad_ready(names)
+                if i > 0:
+                    gsplit = self._conv_dgrad(i, n)
+                continue
+            # two streams: the critical path (dgrad -> BN backward of layer i-1) is issued first on
+            # the main stream; wgrad(i) follows bn_bwd(i) on the wgrad stream, and the bucket's
+            # collective is ordered after it (the comm region waits on the stream current here)
+            ev = self._wev[i]
+            ev.record(main)
             if i > 0:
                 gsplit = self._conv_dgrad(i, n)
+            ws.wait_event(ev)
+            with torch.cuda.stream(ws):
+                self._conv_wgrad(i, x, n)
+                if grad_ready is not None:
+                    grad_ready(names)
+        if ws is not None:
+            main.wait_stream(ws)
         self._eval_dirty = True
         return self.loss
 

@@ -290,3 +290,91 @@ def test_pad_split8(np_):
     ref = torch.zeros(3, 5, 7, 8)
     ref[..., :4] = x
     assert torch.equal(out.cpu(), _planes(ref, np_).cpu())
+
+
+# ----------------------------------------------------------------- halo-staged 3x3 kernels
+HALO_SHAPES = [
+    # N, H, W, C, K   (3x3, stride 1, pad 1)
+    (2, 16, 16, 64, 128),
+    (5, 8, 8, 128, 256),    # the last 256-pixel block is partial
+    (19, 4, 4, 32, 64),     # blocks span many images
+    (3, 2, 2, 64, 32),
+    (1, 32, 32, 32, 48),    # blocks are bands of rows; 48 output channels (partial column tile)
+    (2, 7, 7, 32, 16),      # ResNet-style odd maps: blocks straddle image boundaries
+    (1, 56, 56, 16, 16),    # rows of 56 pixels (fits the 256-pixel tiles only)
+]
+
+
+def _halo_ok(kind, tile, w, cred, cout):
+    from distributed_pytorch_amd.engine import halo_ok
+
+    return halo_ok(kind, tile, w, cred, cout)
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES)
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("tile", [16, 17, 18, 19])
+@pytest.mark.parametrize("np_", [3, 1])
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_conv_halo(shape, splits, tile, np_, dgrad):
+    """Halo-staged 3x3 fprop / data gradient (tiles 16-19) against fp64: partial blocks, blocks
+    across image boundaries, bands of rows, partial column tiles and split-K."""
+    C = _C()
+    N, H, W, Cin, K = shape
+    cred, cout = (K, Cin) if dgrad else (Cin, K)
+    if not _halo_ok("dgrad" if dgrad else "fprop", tile, W, cred, cout):
+        pytest.skip("shape outside this halo tile")
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(dgrad)
+    w = torch.randn(K, Cin, 3, 3, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, padding=1)
+    w3 = _planes(w.float().permute(0, 2, 3, 1), np_)
+    tol = 1e-5 if np_ == 3 else 2e-2
+    if not dgrad:
+        out = torch.empty(N, H, W, K, device="cuda")
+        slab = torch.empty(splits * N * H * W * K, device="cuda") if splits > 1 else None
+        C.conv_x3_fprop(_planes(x.float().permute(0, 2, 3, 1), np_), w3, out, slab, 1, 1, splits, tile, True, False)
+        torch.cuda.synchronize()
+        assert rel_err(out.permute(0, 3, 1, 2), y.detach()) < tol
+    else:
+        dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+        (gx,) = torch.autograd.grad(y, x, dy)
+        dx = torch.empty(N, H, W, Cin, device="cuda")
+        slab = torch.empty(splits * N * H * W * Cin, device="cuda") if splits > 1 else None
+        C.conv_x3_dgrad(_planes(dy.float().permute(0, 2, 3, 1), np_), w3, dx, slab, 1, 1, splits, tile, True, False)
+        torch.cuda.synchronize()
+        assert rel_err(dx.permute(0, 3, 1, 2), gx) < tol
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES + [(4, 32, 32, 8, 64)])
+@pytest.mark.parametrize("splits", [1, 5])
+@pytest.mark.parametrize("tile", [16, 17])
+@pytest.mark.parametrize("np_", [3, 1])
+def test_conv_halo_wgrad(shape, splits, tile, np_):
+    """Halo-staged 3x3 weight gradient (tiles 16/17: 64/32-pixel chunks) against fp64."""
+    C = _C()
+    N, H, W, Cin, K = shape
+    if not _halo_ok("wgrad", tile, W, Cin, K):
+        pytest.skip("shape outside this halo tile")
+    g = torch.Generator().manual_seed(18)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
+    w = (torch.randn(K, Cin, 3, 3, generator=g, dtype=torch.float64) * 0.1).requires_grad_(True)
+    y = F.conv2d(x, w, padding=1)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gw,) = torch.autograd.grad(y, w, dy)
+    dw = torch.empty(K, 3, 3, Cin, device="cuda")
+    slab = torch.empty(splits * K * 9 * Cin, device="cuda") if splits > 1 else None
+    C.conv_x3_wgrad(_planes(x.float().permute(0, 2, 3, 1), np_), _planes(dy.float().permute(0, 2, 3, 1), np_), dw,
+                    slab, 1, 1, splits, tile, False)
+    torch.cuda.synchronize()
+    assert rel_err(dw.permute(0, 3, 1, 2), gw) < (1e-5 if np_ == 3 else 2e-2)
+
+
+def test_halo_rejects_unsupported_shapes():
+    """A halo tile on a conv it cannot run fails loudly (no silent substitute)."""
+    C = _C()
+    x3 = torch.zeros(1, 1, 8, 8, 24, device="cuda", dtype=torch.bfloat16)   # 24 channels: not a 16-multiple
+    w3 = torch.zeros(1, 16, 3, 3, 24, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(1, 8, 8, 16, device="cuda")
+    with pytest.raises(RuntimeError):
+        C.conv_x3_fprop(x3, w3, out, None, 1, 1, 1, 16, True, False)

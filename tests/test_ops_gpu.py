@@ -444,3 +444,28 @@ def test_other_vgg_depths_step_matches_torch(name):
             if dr.norm().item() < 1e-5:
                 continue  # conv biases: analytic gradient 0, the update is rounding noise + weight decay
             assert (du - dr).norm().item() <= 1e-2 * dr.norm().item(), k  # deep + batch 16: ill-conditioned
+
+
+def test_wgrad_stream_matches_single_stream(monkeypatch):
+    """Weight gradients on the second HIP stream (the default) train bit-identically to the
+    single-stream schedule: the event/stream ordering loses no dependency."""
+    from distributed_pytorch_amd.engine import VGGEngine
+
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(64, 32, 32, 4, generator=g) for _ in range(3)]
+    ts = [torch.randint(0, 10, (64,), generator=g) for _ in range(3)]
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DPA_WGRAD_STREAM", flag)
+        e = VGGEngine("VGG11", "cuda", max_batch=64, impl="x3", lr=0.01)
+        e.init_parameters(seed=3)
+        assert (e.wstream is not None) == (flag == "1")
+        for x, t in zip(xs, ts):
+            x = x.cuda()
+            x[..., 3] = 0
+            e.forward_backward(x, t.cuda())
+            e.sgd_step()
+            e.finish_step()
+        torch.cuda.synchronize()
+        outs.append(e.params.flat.clone())
+    assert torch.equal(outs[0], outs[1])
