@@ -77,7 +77,8 @@ def main():
     def step():
         x, t = next(it)
         sync.begin_step()
-        engine.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+        engine.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                                params_free=sync.params_free)
         sync.update(sync.finish())
         engine.finish_step()
 

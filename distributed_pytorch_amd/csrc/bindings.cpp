@@ -64,6 +64,35 @@ void chk(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed: rc=", rc, (rc > 0 ? std::string(" ") + hipGetErrorString((hipError_t)rc) : ""));
 }
 
+// Cross-stream dependency event with caller-chosen flags.  torch.cuda.Event records with a
+// system-scope release (L2 writeback + invalidate at every record); dependencies between streams of
+// ONE device only need device scope (hipEventReleaseToDevice), which keeps L2 warm and lets the
+// next kernel on the recording stream start sooner.
+struct DevEvent {
+  hipEvent_t ev{};
+  explicit DevEvent(int64_t flags) {
+    TORCH_CHECK(hipEventCreateWithFlags(&ev, (unsigned)flags) == hipSuccess, "hipEventCreateWithFlags failed");
+  }
+  ~DevEvent() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+  DevEvent(const DevEvent&) = delete;
+  DevEvent& operator=(const DevEvent&) = delete;
+  void record(int64_t stream) {
+    TORCH_CHECK(hipEventRecord(ev, reinterpret_cast<hipStream_t>(stream)) == hipSuccess, "hipEventRecord failed");
+  }
+  void wait(int64_t stream) {
+    TORCH_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev, 0) == hipSuccess,
+                "hipStreamWaitEvent failed");
+  }
+  void synchronize() { TORCH_CHECK(hipEventSynchronize(ev) == hipSuccess, "hipEventSynchronize failed"); }
+  bool query() {
+    const hipError_t q = hipEventQuery(ev);
+    TORCH_CHECK(q == hipSuccess || q == hipErrorNotReady, "hipEventQuery failed");
+    return q == hipSuccess;
+  }
+};
+
 void need(const Tensor& t, const char* name, at::ScalarType dt = at::kFloat) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
@@ -619,6 +648,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("fc_ce_train", &fc_ce_train);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);
+  py::class_<DevEvent>(m, "DevEvent")
+      .def(py::init<int64_t>(), py::arg("flags"))
+      .def("record", &DevEvent::record, py::arg("stream"))
+      .def("wait", &DevEvent::wait, py::arg("stream"))
+      .def("synchronize", &DevEvent::synchronize)
+      .def("query", &DevEvent::query);
+  m.attr("EVENT_DISABLE_TIMING") = (int64_t)hipEventDisableTiming;
+  m.attr("EVENT_RELEASE_TO_DEVICE") = (int64_t)hipEventReleaseToDevice;
+  m.attr("EVENT_DISABLE_SYSTEM_FENCE") = (int64_t)hipEventDisableSystemFence;
   m.def("rccl_unique_id", []() { return py::bytes(dpa::RcclComm::unique_id()); });
   m.def("rccl_version", &dpa::RcclComm::version);
   // native rendezvous store (bootstrap without torch.distributed); blocking calls release the GIL

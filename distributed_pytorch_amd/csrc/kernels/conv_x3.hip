@@ -1134,13 +1134,16 @@ int xsplits(int Kred, int splits) {
   return splits < 1 ? 1 : splits;
 }
 
-// ---- halo tiles: ids 16-19 follow the 16 implicit-GEMM tiles (3x3, stride 1, pad 1 only) ----
+// ---- halo tiles: ids 16-21 follow the 16 implicit-GEMM tiles (3x3, stride 1, pad 1 only) ----
 //   FPROP / DGRAD: 16 = 256x128 with 16-channel chunks (8 waves), 17 = 256x128 / 32,
-//                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32
+//                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32,
+//                  20 = 256x64 / 32 (8 waves of 64x32), 21 = 128x64 / 32 (4 waves of 64x32) for
+//                  64-channel outputs (e.g. the data gradient into a 64-channel layer)
 //   WGRAD:         16 = 64-pixel chunks, 17 = 32-pixel chunks
-bool is_halo(int tile) { return tile >= 16 && tile <= 19; }
-int halo_bm(int tile) { return tile <= 17 ? 256 : 128; }
-int halo_bc(int tile) { return (tile & 1) ? 32 : 16; }
+bool is_halo(int tile) { return tile >= 16 && tile <= 21; }
+int halo_bm(int tile) { return (tile <= 17 || tile == 20) ? 256 : 128; }
+int halo_bn(int tile) { return tile >= 20 ? 64 : 128; }
+int halo_bc(int tile) { return (tile & 1) || tile == 20 ? 32 : 16; }
 
 template <int BM, int BN, int WM, int WN, bool DG, int NP, int BC, bool OB>
 int launch_halo(const HArgs& a, int splits, hipStream_t st) {
@@ -1155,6 +1158,8 @@ int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
     case 16: return launch_halo<256, 128, 4, 2, DG, NP, 16, OB>(a, splits, st);
     case 17: return launch_halo<256, 128, 4, 2, DG, NP, 32, OB>(a, splits, st);
     case 18: return launch_halo<128, 128, 2, 2, DG, NP, 16, OB>(a, splits, st);
+    case 20: return launch_halo<256, 64, 4, 2, DG, NP, 32, OB>(a, splits, st);
+    case 21: return launch_halo<128, 64, 2, 2, DG, NP, 32, OB>(a, splits, st);
     default: return launch_halo<128, 128, 2, 2, DG, NP, 32, OB>(a, splits, st);
   }
 }
@@ -1167,7 +1172,7 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
   if (obf && (np != 1 || (splits > 1 && !reduce))) return -4;
   a.M = a.N * a.H * a.W;
   a.gm = cdiv(a.M, BM);
-  a.gn = cdiv(a.Nout, 128);
+  a.gn = cdiv(a.Nout, halo_bn(tile));
   a.cps = cdiv(a.C / BC, splits);
   a.out = splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;

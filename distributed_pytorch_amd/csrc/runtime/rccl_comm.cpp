@@ -29,6 +29,19 @@ int RcclComm::version() {
   return v;
 }
 
+namespace {
+// Fence / completion events only order streams of this device (and let the watchdog observe
+// completion), so they record with a device-scope release: a system-scope one writes back and
+// invalidates L2 under the compute kernels running beside the collective.  DPA_EVENT_SCOPE=torch
+// restores the default system scope for A/B runs.
+unsigned event_flags() {
+  const char* e = std::getenv("DPA_EVENT_SCOPE");
+  if (e && std::string(e) == "torch") return hipEventDisableTiming;
+  if (e && std::string(e) == "nofence") return hipEventDisableTiming | hipEventDisableSystemFence;
+  return hipEventDisableTiming | hipEventReleaseToDevice;
+}
+}  // namespace
+
 RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,
                    WatchdogConfig wd)
     : rank_(rank), world_(world), device_(device), stream_(comm_stream), wd_(wd) {
@@ -37,8 +50,8 @@ RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipS
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
   check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
-  hip_check(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
-  hip_check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&ev_in_, event_flags()), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&ev_out_, event_flags()), "hipEventCreate");
   if (wd_.enabled) watchdog_ = std::thread([this] { watchdog_loop(); });
 }
 
@@ -81,7 +94,7 @@ void RcclComm::end_op(const char* what) {
       ev = free_events_.back();
       free_events_.pop_back();
     } else {
-      hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&ev, event_flags()), "hipEventCreate");
     }
   }
   hip_check(hipEventRecord(ev, stream_), "hipEventRecord");

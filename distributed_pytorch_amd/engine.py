@@ -36,6 +36,7 @@ from . import _ext
 from .models.vgg import VGGSpec
 from .ops import cpu_ref
 from .utils.arena import Arena
+from .utils.streams import DevEvent, StreamJoin
 
 
 def _pow2_round(x: float) -> int:
@@ -93,7 +94,8 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
 
 # Halo-staged 3x3/s1/p1 tiles of conv_x3.hip (ids after the 16 implicit-GEMM tiles): the block's
 # input pixels are staged once per channel chunk and the 9 taps read shifted views of them.
-HALO_TILES = (16, 17, 18, 19)        # fprop / dgrad: 256 or 128 pixels x 128 channels, 16 or 32-channel chunks
+HALO_TILES = (16, 17, 18, 19, 20, 21)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19) or 64 (20, 21)
+                                       # output channels, 16 or 32-channel chunks
 HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
 
 
@@ -106,7 +108,7 @@ def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
         return p is not None and cred % 8 == 0 and cout % 8 == 0 and p + 2 * w + 2 <= 2 * p + 3
     if tile not in HALO_TILES:
         return False
-    bm, bc = (256 if tile <= 17 else 128), (32 if tile & 1 else 16)
+    bm, bc = (256 if tile in (16, 17, 20) else 128), (32 if tile & 1 or tile == 20 else 16)
     return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= bm + bm // 2
 
 
@@ -202,14 +204,15 @@ class VGGEngine:
         # split-K workspace.
         self.wstream = (torch.cuda.Stream(dev) if dev.type == "cuda" and os.environ.get("DPA_WGRAD_STREAM", "1") == "1"
                         else None)
-        self._wev = [torch.cuda.Event() for _ in L] if self.wstream is not None else None
+        self._wev = [DevEvent() for _ in L] if self.wstream is not None else None
+        self._join = StreamJoin() if self.wstream is not None else None
         self.slab = torch.empty(1, **f32)
         self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
         for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
             for kind in ("fprop", "dgrad", "wgrad"):
                 if kind == "dgrad" and i == 0:
                     continue
-                self._ensure_slab(self._slab_need(i, kind, N), wgrad=kind == "wgrad")
+                self._ensure_slab(self._slab_need(i, kind, N), wgrad=kind == "wgrad" and self._wgrad_on_side(i))
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -397,10 +400,12 @@ class VGGEngine:
             out += [(t, s, False) for t in ok for s in splits]
         return out
 
-    def autotune(self, n: Optional[int] = None, iters: int = 3, verbose: bool = False) -> Dict[str, list]:
+    def autotune(self, n: Optional[int] = None, iters: int = 3, verbose: bool = False,
+                 only: Optional[List[str]] = None) -> Dict[str, list]:
         """Time every candidate (tile, splits, posmajor) of every conv call of the step at batch n on
         this GPU and adopt the fastest.  Returns {conv_key: [tile, splits, posmajor, ms]} (the
-        format of tuning/mi355x.json).  Buffers must hold one step's data (run a step first)."""
+        format of tuning/mi355x.json).  Buffers must hold one step's data (run a step first).
+        ``only``: tune just the calls whose conv_key contains one of these substrings."""
         n = n or self.max_batch
         res: Dict[str, list] = {}
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -411,6 +416,8 @@ class VGGEngine:
                     continue
                 impl = self._layer_impl(i)
                 key = (impl, kind, n, i)
+                if only and not any(o in conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout) for o in only):
+                    continue
                 best = None
                 for cand in self.conv_candidates(i, kind):
                     tile, s, pm = cand
@@ -478,11 +485,16 @@ class VGGEngine:
                               False, pm)
         return s
 
+    def _wgrad_on_side(self, i: int) -> bool:
+        """Whether layer i's weight gradient runs on the wgrad stream (every layer but the first)."""
+        return self.wstream is not None and i > 0
+
     def _conv_wgrad(self, i: int, x: torch.Tensor, n: int):
         l = self.spec.convs[i]
         tile, s, pm = self.conv_config(i, "wgrad", n)
-        self._ensure_slab(self._slab_need(i, "wgrad", n), wgrad=True)
-        slab = (self.wslab if self.wslab is not None else self.slab) if s > 1 else None
+        side = self._wgrad_on_side(i)
+        self._ensure_slab(self._slab_need(i, "wgrad", n), wgrad=side)
+        slab = (self.wslab if side else self.slab) if s > 1 else None
         dw = self.grads[f"{l.conv_key}.weight"]
         if self.planes[i]:
             self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
@@ -497,10 +509,18 @@ class VGGEngine:
     # ------------------------------------------------------------------ training step
     def forward_backward(self, x: torch.Tensor, target: torch.Tensor,
                          grad_ready: Optional[Callable[[List[str]], None]] = None,
-                         pre_forward: Optional[Callable[[], None]] = None) -> torch.Tensor:
+                         pre_forward: Optional[Callable[[], None]] = None,
+                         params_free: Optional[Callable[[List[str]], None]] = None) -> torch.Tensor:
         """One training forward+backward on x [n,H,W,4] (NHWC fp32, 4th channel zero).
         Gradients land in ``self.grads``; the batch-mean loss in ``self.loss`` (device) and is
-        also accumulated into ``self.loss_accum``.  Returns ``self.loss``."""
+        also accumulated into ``self.loss_accum``.  Returns ``self.loss``.
+
+        Callbacks (the gradient-sync strategy's hooks):
+          ``grad_ready(names)``  every kernel writing those gradients has been enqueued; called with
+                                 the stream that ran the last of them current (wgrad stream or main);
+          ``params_free(names)`` every kernel of this step READING those parameters (or their bf16
+                                 planes) has been enqueued; called with the main stream current.
+        Once both have fired for a tensor its optimizer step may run while backward continues."""
         K, P, G = self.K, self.params, self.grads
         n = x.shape[0]
         L = self.spec.convs
@@ -524,6 +544,8 @@ class VGGEngine:
                       self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
         if grad_ready is not None:
             grad_ready(["fc1.weight", "fc1.bias"])
+        if params_free is not None:
+            params_free(["fc1.weight", "fc1.bias"])
         gsplit = 1  # split-K slabs of g[i] left unreduced by the previous dgrad (summed inside bn_bwd)
         ws = self.wstream
         main = torch.cuda.current_stream(self.device) if ws is not None else None
@@ -537,13 +559,17 @@ class VGGEngine:
                      st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
                      G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool)
             names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
-            if ws is None:
-                # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early
+            if not self._wgrad_on_side(i):
+                # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
+                # Layer 0's wgrad has nothing left to overlap with, so it stays on the main stream (a
+                # stream hop costs ~15 us on MI355X, tools/event_overhead.py)
                 self._conv_wgrad(i, x, n)
                 if grad_ready is not None:
                     grad_ready(names)
                 if i > 0:
                     gsplit = self._conv_dgrad(i, n)
+                if params_free is not None:  # dgrad(i) was the last reader of layer i's weights
+                    params_free(names)
                 continue
             # two streams: the critical path (dgrad -> BN backward of layer i-1) is issued first on
             # the main stream; wgrad(i) follows bn_bwd(i) on the wgrad stream, and the bucket's
@@ -552,13 +578,15 @@ class VGGEngine:
             ev.record(main)
             if i > 0:
                 gsplit = self._conv_dgrad(i, n)
-            ws.wait_event(ev)
+            if params_free is not None:
+                params_free(names)
+            ev.wait(ws)
             with torch.cuda.stream(ws):
                 self._conv_wgrad(i, x, n)
                 if grad_ready is not None:
                     grad_ready(names)
         if ws is not None:
-            main.wait_stream(ws)
+            self._join(main, ws)
         self._eval_dirty = True
         return self.loss
 

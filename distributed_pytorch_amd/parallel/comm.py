@@ -25,6 +25,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..utils.streams import StreamJoin
+
 
 class Comm:
     rank: int = 0
@@ -105,13 +107,15 @@ class TorchComm(Comm):
         self.world = dist.get_world_size(group)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._join_in = StreamJoin() if self.side is not None else None
+        self._join_out = StreamJoin() if self.side is not None else None
 
     @contextlib.contextmanager
     def region(self):
         if self.side is None:
             yield
             return
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        self._join_in(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             yield
 
@@ -151,7 +155,7 @@ class TorchComm(Comm):
 
     def wait(self):
         if self.side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self._join_out(torch.cuda.current_stream(self.device), self.side)
 
     def synchronize(self):
         if self.side is not None:
@@ -204,11 +208,12 @@ class RcclComm(Comm):
                                  exit_on_error=os.environ.get("DPA_WATCHDOG_EXIT", "1") == "1",
                                  debug_sync=os.environ.get("DPA_DEBUG_SYNC", "0") == "1")
         self.stream = torch.cuda.ExternalStream(self._c.stream_ptr(), device=self.device)
+        self._join_in, self._join_out = StreamJoin(), StreamJoin()
         self._store = store
 
     @contextlib.contextmanager
     def region(self):
-        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self._join_in(self.stream, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             yield
 
@@ -228,7 +233,7 @@ class RcclComm(Comm):
         self._c.all_gather(send, recv)
 
     def wait(self):
-        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        self._join_out(torch.cuda.current_stream(self.device), self.stream)
 
     def synchronize(self):
         self._c.synchronize()

@@ -20,25 +20,37 @@ Differences from the reference, all by design:
   three 9 MiB [512,512,3,3] weights each get a bucket; the last-ready bucket is kept small so the
   exposed tail after backward is short) instead of DDP's 25 MiB/1 MiB;
 * all modes broadcast rank 0's parameters and buffers once at start, so replicas
-  cannot silently fork.
+  cannot silently fork;
+* the optimizer step is fused per bucket into backward (``overlap=True``): once a bucket's
+  collective is issued AND the engine reports its parameters no longer read this step
+  (``params_free``: dgrad of that layer enqueued), the fused SGD of that slice is queued behind the
+  collective on the comm stream.  The big late-layer
+  weights are updated while the early layers' backward still runs, so what is left after backward
+  is only the small tail bucket's collective and update.  Per-element SGD math is unchanged, so
+  results are bitwise identical to one SGD launch after ``finish()``.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
 
+from ..utils.streams import DevEvent, StreamJoin
 from .comm import Comm
 
 
 class Bucket:
-    __slots__ = ("names", "lo", "hi", "pending", "issued")
+    __slots__ = ("names", "lo", "hi", "pending", "issued", "busy", "stepped", "free_ev")
 
     def __init__(self, names: List[str], lo: int, hi: int):
         self.names = list(names)
         self.lo, self.hi = lo, hi
-        self.pending = set(names)
-        self.issued = False
+        self.pending = set(names)   # gradients not yet produced this step
+        self.busy = set(names)      # parameters still read by kernels not yet enqueued this step
+        self.issued = False         # collective enqueued
+        self.stepped = False        # optimizer step of this slice enqueued
+        self.free_ev = None         # main-stream event after the last reader of the parameters
 
     @property
     def numel(self):
@@ -92,17 +104,30 @@ def plan_buckets(arena, ready_order: List[List[str]], bucket_mb: float, tail_mb:
 class GradSync:
     mode = "none"
 
+    # whether this mode's optimizer step can run per bucket inside backward (see module doc)
+    fusable_step = True
+
     def __init__(self, engine, comm: Comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
         self.engine = engine
         self.comm = comm
         self.world = comm.world
         self.active = comm.name != "null"  # a real communicator (also a forced 1-rank one)
         self.overlap = overlap
+        # DPA_FUSED_STEP: auto (default: with a real communicator, where the update hides behind the
+        # collectives of later buckets; for a lone rank the extra stream hops cost more than the
+        # ~40 us update they would hide, measured on MI355X) | 1 (always) | 0 (never)
+        fused = os.environ.get("DPA_FUSED_STEP", "auto")
+        self.fuse_step = overlap and self.fusable_step and (fused == "1" or (fused == "auto" and self.active))
+        self._cuda = engine.device.type == "cuda"
         order = [["fc1.weight", "fc1.bias"]] + [
             [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
             for l in reversed(engine.spec.convs)]
         self.buckets = plan_buckets(engine.grads, order, bucket_mb)
         self._by_name: Dict[str, Bucket] = {n: b for b in self.buckets for n in b.names}
+        self._join = StreamJoin() if self._cuda else None
+        if self._cuda:
+            for b in self.buckets:
+                b.free_ev = DevEvent()
         self.issued_bytes = 0
         if broadcast_init and self.active:
             self.broadcast_state()
@@ -128,18 +153,60 @@ class GradSync:
     def begin_step(self):
         for b in self.buckets:
             b.pending = set(b.names)
+            b.busy = set(b.names)
             b.issued = False
+            b.stepped = False
 
     def grad_ready(self, names: List[str]):
-        if not self.active:
-            return
         for n in names:
             b = self._by_name.get(n)
             if b is None:
                 continue
             b.pending.discard(n)
-            if not b.pending and self.overlap and not b.issued:
+            if b.pending:
+                continue
+            if self.active and self.overlap and not b.issued:
                 self._issue(b)
+            self._maybe_step(b)
+
+    def params_free(self, names: List[str]):
+        """Engine hook (main stream current): no kernel of this step still to be enqueued reads
+        these parameters."""
+        if not self.fuse_step:
+            return
+        for n in names:
+            b = self._by_name.get(n)
+            if b is None or n not in b.busy:
+                continue
+            b.busy.discard(n)
+            if b.busy:
+                continue
+            if b.free_ev is not None:
+                b.free_ev.record(torch.cuda.current_stream(self.engine.device))
+            self._maybe_step(b)
+
+    def _maybe_step(self, b: Bucket):
+        """Enqueue the fused SGD of bucket b once its gradients are final (collective issued) and
+        its parameters are free.  Runs on the comm stream behind the collective; for a single rank
+        on the engine's wgrad stream (else inline on the current stream)."""
+        if not self.fuse_step or b.stepped or b.pending or b.busy or (self.active and not b.issued):
+            return
+        b.stepped = True
+        scale = self.grad_scale()
+        if self.active:
+            with self.comm.region():  # comm stream: behind the collective, after the triggering stream
+                if b.free_ev is not None:
+                    b.free_ev.wait(torch.cuda.current_stream(self.engine.device))
+                self.engine.sgd_step(scale, b.lo, b.numel)
+            return
+        s = self.engine.wstream if self._cuda else None
+        if s is None:
+            self.engine.sgd_step(scale, b.lo, b.numel)
+            return
+        self._join(s, torch.cuda.current_stream(self.engine.device))
+        b.free_ev.wait(s)
+        with torch.cuda.stream(s):
+            self.engine.sgd_step(scale, b.lo, b.numel)
 
     def _issue(self, b: Bucket):
         b.issued = True
@@ -154,10 +221,13 @@ class GradSync:
         """Issue whatever is left, make the compute stream wait for the comm stream, and return
         the scale the optimizer must apply to the synced grads."""
         if not self.active:
+            if self.fuse_step and self._cuda and self.engine.wstream is not None:
+                self._join(torch.cuda.current_stream(self.engine.device), self.engine.wstream)
             return 1.0
         for b in self.buckets:
             if not b.issued:
                 self._issue(b)
+            self._maybe_step(b)
         self.comm.wait()
         return self.grad_scale()
 
@@ -165,8 +235,15 @@ class GradSync:
         return 1.0
 
     def update(self, grad_scale: float):
-        """Apply the optimizer step to the synchronised gradients (the whole arena by default)."""
-        self.engine.sgd_step(grad_scale)
+        """Apply the optimizer step to the synchronised gradients (the whole arena by default;
+        with the fused step only slices whose update was not already queued during backward)."""
+        if not self.fuse_step:
+            self.engine.sgd_step(grad_scale)
+            return
+        for b in self.buckets:
+            if not b.stepped:
+                b.stepped = True
+                self.engine.sgd_step(grad_scale, b.lo, b.numel)
 
 
 class GatherScatterSync(GradSync):
@@ -237,6 +314,7 @@ class ZeroSync(DDPSync):
     spans are multiples of 64 elements, so W | 16 keeps every shard float4-aligned."""
 
     mode = "zero1"
+    fusable_step = False  # the update is sharded (owned slices after reduce-scatter, then all-gather)
 
     def __init__(self, engine, comm, bucket_mb: float = 10.0, overlap: bool = True, broadcast_init: bool = True,
                  broadcast_buffers: bool = True):

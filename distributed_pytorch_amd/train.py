@@ -50,7 +50,8 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
         with trace_range("step"):
             sync.begin_step()
             with trace_range("fwd_bwd"):
-                engine.forward_backward(x, target, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+                engine.forward_backward(x, target, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                                        params_free=sync.params_free)
             with trace_range("sync"):
                 gscale = sync.finish()
             with trace_range("sgd"):

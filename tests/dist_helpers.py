@@ -50,7 +50,8 @@ def run_engine_mode(rank, world, port, mode, steps, outdir, bucket_mb=None, over
     losses = []
     for x, t in _batches(rank, steps):
         sync.begin_step()
-        e.forward_backward(_x4(x), t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+        e.forward_backward(_x4(x), t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                           params_free=sync.params_free)
         sync.update(sync.finish())
         e.finish_step()
         losses.append(float(e.loss.item()))

@@ -240,3 +240,33 @@ def test_cifar10_binary_reader(tmp_path):
     assert np.array_equal(tr.images[0].numpy(), chw.transpose(1, 2, 0))
     a, b = cifar.get_datasets(str(tmp_path / "nope"), False, 64, 32)
     assert len(a) == 64 and len(b) == 32
+
+
+@pytest.mark.parametrize("mode", ["ddp", "allreduce", "gather"])
+def test_fused_step_matches_single_update(mode, monkeypatch):
+    """Per-bucket SGD queued inside backward (params_free + grad_ready) gives the same parameters
+    and momentum, bit for bit, as one SGD over the arena after backward."""
+    from distributed_pytorch_amd.parallel import NullComm, make_sync
+
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(4, 3, 32, 32, generator=g) for _ in range(2)]
+    ts = [torch.randint(0, 10, (4,), generator=g) for _ in range(2)]
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DPA_FUSED_STEP", fused)
+        e = VGGEngine("VGG11", "cpu", max_batch=4, lr=0.05)
+        e.init_parameters(seed=2)
+        sync = make_sync(mode, e, NullComm(), bucket_mb=1.0 if mode == "ddp" else None)
+        assert sync.fuse_step == (fused == "1")
+        stepped = []
+        for x, t in zip(xs, ts):
+            sync.begin_step()
+            e.forward_backward(_x4(x), t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                               params_free=sync.params_free)
+            stepped.append(all(b.stepped for b in sync.buckets))  # all queued inside backward
+            sync.update(sync.finish())
+            e.finish_step()
+        if fused == "1":
+            assert all(stepped)
+        out.append((e.params.flat.clone(), e.mom.flat.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

@@ -302,6 +302,8 @@ HALO_SHAPES = [
     (1, 32, 32, 32, 48),    # blocks are bands of rows; 48 output channels (partial column tile)
     (2, 7, 7, 32, 16),      # ResNet-style odd maps: blocks straddle image boundaries
     (1, 56, 56, 16, 16),    # rows of 56 pixels (fits the 256-pixel tiles only)
+    (3, 16, 16, 128, 64),   # VGG layer-1-like data gradient into 64 channels (tiles 20/21)
+    (2, 8, 8, 64, 96),      # 96 output channels: one full and one partial 64-column tile
 ]
 
 
@@ -313,12 +315,13 @@ def _halo_ok(kind, tile, w, cred, cout):
 
 @pytest.mark.parametrize("shape", HALO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", [16, 17, 18, 19])
+@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21])
 @pytest.mark.parametrize("np_", [3, 1])
 @pytest.mark.parametrize("dgrad", [False, True])
 def test_conv_halo(shape, splits, tile, np_, dgrad):
-    """Halo-staged 3x3 fprop / data gradient (tiles 16-19) against fp64: partial blocks, blocks
-    across image boundaries, bands of rows, partial column tiles and split-K."""
+    """Halo-staged 3x3 fprop / data gradient (tiles 16-21) against fp64: partial blocks, blocks
+    across image boundaries, bands of rows, partial column tiles (128- and 64-column tiles) and
+    split-K."""
     C = _C()
     N, H, W, Cin, K = shape
     cred, cout = (K, Cin) if dgrad else (Cin, K)

@@ -315,7 +315,11 @@ def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatc
     xs = [torch.randn(32, 32, 32, 4, generator=g) for _ in range(3)]
     ts = [torch.randint(0, 10, (32,), generator=g) for _ in range(3)]
     outs = []
-    for comm in (NullComm(), RcclComm(0, 1, dev, uid=C.rccl_unique_id())):
+    # null comm with the update after backward, null comm with the per-bucket update fused into
+    # backward (wgrad stream), 1-rank RCCL with the fused update on the comm stream
+    runs = [(NullComm(), "0"), (NullComm(), "1"), (RcclComm(0, 1, dev, uid=C.rccl_unique_id()), "1")]
+    for comm, fused in runs:
+        monkeypatch.setenv("DPA_FUSED_STEP", fused)
         e = VGGEngine("VGG11", dev, max_batch=32, impl="x3", lr=0.01)
         e.init_parameters(seed=3)
         sync = make_sync(mode, e, comm, bucket_mb=1.0 if mode == "ddp" else None)
@@ -323,14 +327,15 @@ def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatc
             x = x.cuda()
             x[..., 3] = 0
             sync.begin_step()
-            e.forward_backward(x, t.cuda(), grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+            e.forward_backward(x, t.cuda(), grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                               params_free=sync.params_free)
             sync.update(sync.finish())
             e.finish_step()
         torch.cuda.synchronize()
         comm.check()
         outs.append(e.params.flat.clone())
         comm.close()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 def test_bn_reductions_bitwise_reproducible():

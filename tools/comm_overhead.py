@@ -72,7 +72,8 @@ def run(comm, mode, steps, warmup, batch):
 
     def step():
         sync.begin_step()
-        e.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward)
+        e.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                           params_free=sync.params_free)
         sync.update(sync.finish())
         e.finish_step()
 

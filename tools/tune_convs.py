@@ -1,7 +1,7 @@
 """Measure the best (tile, split-K, position-major) for every conv call of the VGG training step
 on this GPU and write distributed_pytorch_amd/tuning/mi355x.json (merged with existing entries).
 
-    python tools/tune_convs.py [--impls fp32,x3,bf16] [--batch 256]
+    python tools/tune_convs.py [--impls fp32,x3,bf16] [--batch 256] [--only x3|dgrad|256|16|,...]
 """
 import argparse
 import json
@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--model", default="VGG11")
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--only", default="", help="comma-separated conv_key substrings to re-tune (default: all)")
     ap.add_argument("--out", default=os.path.join(ROOT, "distributed_pytorch_amd", "tuning", "mi355x.json"))
     a = ap.parse_args()
     table = {}
@@ -36,7 +37,7 @@ def main():
         t = torch.randint(0, 10, (a.batch,), device="cuda")
         e.forward_backward(e.x0, t)
         torch.cuda.synchronize()
-        res = e.autotune(a.batch, iters=a.iters, verbose=True)
+        res = e.autotune(a.batch, iters=a.iters, verbose=True, only=[o for o in a.only.split(",") if o] or None)
         table.update(res)
         tot = sum(v[3] for v in res.values())
         print(json.dumps({"impl": impl, "sum_best_conv_ms": round(tot, 4)}), flush=True)
