@@ -648,6 +648,20 @@ PYBIND11_MODULE(_C, m) {
   m.def("fc_ce_train", &fc_ce_train);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);
+  // A HIP stream with an explicit priority (lower number = higher priority; HIP's range is reported
+  // by stream_priority_range()).  Owned by the caller; lives until stream_destroy.
+  m.def("stream_create", [](int64_t priority) {
+    hipStream_t s = nullptr;
+    TORCH_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, (int)priority) == hipSuccess,
+                "hipStreamCreateWithPriority failed");
+    return reinterpret_cast<int64_t>(s);
+  });
+  m.def("stream_destroy", [](int64_t s) { (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(s)); });
+  m.def("stream_priority_range", []() {
+    int least = 0, greatest = 0;
+    TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "hipDeviceGetStreamPriorityRange");
+    return std::make_pair(least, greatest);
+  });
   py::class_<DevEvent>(m, "DevEvent")
       .def(py::init<int64_t>(), py::arg("flags"))
       .def("record", &DevEvent::record, py::arg("stream"))

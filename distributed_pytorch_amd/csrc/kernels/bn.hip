@@ -23,12 +23,30 @@
 // Reductions: a RT-thread (1024) block covers RPB rows x all channels (threads per row = C/4
 // float4 lanes, RT/(C/4) rows in flight, 4 rows' loads issued together), keeps per-thread partials
 // in registers, combines them with an LDS tree, and writes ONE partial per (block, channel) —
-// deterministic, no atomics.  ~256 blocks: one wave of full CUs, few partials to merge.
+// deterministic, no atomics.  ~256 blocks: one wave of full CUs, few partials to merge.  The
+// backward reduce uses RTB (256) -thread blocks, ~1024 of them (see RTB).
 #include "common.h"
+
+#include <cstdlib>
 
 namespace {
 
-constexpr int RT = 1024;  // reduction block size
+constexpr int RT = 1024;  // forward-statistics block size
+// Backward reduce: 256-thread blocks with a 4 KB LDS tree, ~1024 of them.  The backward reduce runs
+// beside the weight-gradient convs of the other stream; a 1024-thread / 48 KB block could not be
+// placed on a CU holding conv blocks and waited for whole CUs to drain (3-6x slower in the step).
+// DPA_BN_BWD_BLOCK=1024 selects the old single-stream geometry (1024 threads, ~256 blocks) for A/B.
+constexpr int RTB = 256;
+constexpr int BWD_BLOCKS = 1024;
+inline bool bwd_wide() {
+  static const bool w = [] {
+    const char* e = std::getenv("DPA_BN_BWD_BLOCK");
+    return e && std::atoi(e) == 1024;
+  }();
+  return w;
+}
+inline int bwd_rt() { return bwd_wide() ? RT : RTB; }
+inline int bwd_blocks() { return bwd_wide() ? 256 : BWD_BLOCKS; }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -50,27 +68,27 @@ struct RedGeom {
   int C4, TPR, RPI, CG;  // float4 lanes per row, threads per row, rows per iteration, channel groups/thread
 };
 
-__host__ __device__ inline RedGeom red_geom(int C) {
+__host__ __device__ inline RedGeom red_geom(int C, int rt = RT) {
   RedGeom g;
   g.C4 = C >> 2;
-  g.TPR = g.C4 < RT ? g.C4 : RT;
-  g.RPI = RT / g.TPR;
+  g.TPR = g.C4 < rt ? g.C4 : rt;
+  g.RPI = rt / g.TPR;
   g.CG = (g.C4 + g.TPR - 1) / g.TPR;
   return g;
 }
 
-// rows per block so that the grid has ~256 blocks (at least one full iteration per block)
-__host__ inline int red_rows_per_block(int M, int C) {
-  const RedGeom g = red_geom(C);
-  int rpb = (M + 255) / 256;
+// rows per block so that the grid has ~`blocks` blocks (at least one full iteration per block)
+__host__ inline int red_rows_per_block(int M, int C, int rt = RT, int blocks = 256) {
+  const RedGeom g = red_geom(C, rt);
+  int rpb = (M + blocks - 1) / blocks;
   rpb = ((rpb + g.RPI - 1) / g.RPI) * g.RPI;
   return rpb < g.RPI ? g.RPI : rpb;
 }
 
 // In-block tree over the RPI row lanes of each channel lane (fixed order): on return sh[t] for
 // lane_r == 0 holds the block sum.  Caller has stored sh[t] and synchronised.
-template <int NARR>
-__device__ __forceinline__ void tree_rows(float4 (*sh)[RT], int t, int lane_r, int TPR, int RPI) {
+template <int NARR, int T = RT>
+__device__ __forceinline__ void tree_rows(float4 (*sh)[T], int t, int lane_r, int TPR, int RPI) {
   int p2 = 1;
   while (p2 < RPI) p2 <<= 1;
   for (int o = p2 >> 1; o >= 1; o >>= 1) {
@@ -346,8 +364,8 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat.  Rows are OUTPUT rows of
 // the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
 // the summed g is written to gout (consumed by the apply pass).  part layout: [block][3][C]
-template <bool POOL, int ACT, typename TZ>
-__global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
+template <bool POOL, int ACT, typename TZ, int RTB>
+__global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
                                                             int nsplit, const TZ* __restrict__ z,
                                                             const TZ* __restrict__ res,
                                                             const float* __restrict__ scale,
@@ -356,7 +374,7 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const TZ* __restrict_
                                                             const float* __restrict__ invstd,
                                                             float* __restrict__ part, int N, int H, int W, int C,
                                                             int rpb) {
-  const RedGeom gg = red_geom(C);
+  const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
   const int lane_c = t % gg.TPR, lane_r = t / gg.TPR;
   const bool active = lane_r < gg.RPI;
@@ -365,7 +383,7 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const TZ* __restrict_
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(Mo, r0 + rpb);
   const long slab4 = (long)Mo * gg.C4;
-  __shared__ float4 sh[3][RT];
+  __shared__ float4 sh[1][RTB];  // one tree buffer, used for the three sums in turn
   for (int cg = 0; cg < gg.CG; ++cg) {
     const int c4 = lane_c + cg * gg.TPR;
     const bool cval = active && c4 < gg.C4;
@@ -415,19 +433,17 @@ __global__ __launch_bounds__(RT) void bn_bwd_reduce_kernel(const TZ* __restrict_
         }
       }
     }
-    sh[0][t] = make_float4(sdy[0], sdy[1], sdy[2], sdy[3]);
-    sh[1][t] = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
-    sh[2][t] = make_float4(sx[0], sx[1], sx[2], sx[3]);
-    __syncthreads();
-    tree_rows<3>(sh, t, lane_r, gg.TPR, gg.RPI);
-    if (cval && lane_r == 0) {
-      const float4 a = sh[0][t], b = sh[1][t], x = sh[2][t];
-      float* o = part + (long)blockIdx.x * 3 * C + c4 * 4;
-      *reinterpret_cast<float4*>(o) = a;
-      *reinterpret_cast<float4*>(o + C) = b;
-      *reinterpret_cast<float4*>(o + 2 * C) = x;
+    const float4 vals[3] = {make_float4(sdy[0], sdy[1], sdy[2], sdy[3]), make_float4(sdx[0], sdx[1], sdx[2], sdx[3]),
+                            make_float4(sx[0], sx[1], sx[2], sx[3])};
+    float* o = part + (long)blockIdx.x * 3 * C + c4 * 4;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      sh[0][t] = vals[q];
+      __syncthreads();
+      tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
+      if (cval && lane_r == 0) *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -636,15 +652,24 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
   if (nsplit < 1) nsplit = 1;
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
-  const int rpb = red_rows_per_block(Mo, C);
+  const int rpb = red_rows_per_block(Mo, C, bwd_rt(), bwd_blocks());
   const int nblk = (Mo + rpb - 1) / rpb;
-#define RED(P, A) \
-  bn_bwd_reduce_kernel<P, A, TZ><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, N, H, \
-                                                      W, C, rpb)
-  if (pool) RED(true, 0);
-  else if (act == 0) RED(false, 0);
-  else if (act == 1) RED(false, 1);
-  else RED(false, 2);
+#define RED(P, A)                                                                                                 \
+  if (bwd_wide())                                                                                                 \
+    bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
+                                                            N, H, W, C, rpb);                                     \
+  else                                                                                                            \
+    bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
+                                                              part, N, H, W, C, rpb)
+  if (pool) {
+    RED(true, 0);
+  } else if (act == 0) {
+    RED(false, 0);
+  } else if (act == 1) {
+    RED(false, 1);
+  } else {
+    RED(false, 2);
+  }
 #undef RED
   bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
                                                       dbeta, dbias, coef);
@@ -671,7 +696,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
 extern "C" {
 // floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (3 per ...)
 long dpa_bn_part_floats(int M, int C, int bwd) {
-  const int rpb = red_rows_per_block(M, C);
+  const int rpb = bwd ? red_rows_per_block(M, C, bwd_rt(), bwd_blocks()) : red_rows_per_block(M, C);
   const long nblk = (M + rpb - 1) / rpb;
   return nblk * C * (bwd ? 3 : 2);
 }

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import json
 import os
+import weakref
 from collections import OrderedDict
 from typing import Callable, Dict, List, Optional
 
@@ -202,7 +203,7 @@ class VGGEngine:
         # only dz(i) and the stored forward activation, so it runs beside dgrad(i) and the BN
         # backward of layer i-1, whose reduce/finalize kernels leave most CUs idle.  It has its own
         # split-K workspace.
-        self.wstream = (torch.cuda.Stream(dev) if dev.type == "cuda" and os.environ.get("DPA_WGRAD_STREAM", "1") == "1"
+        self.wstream = (self._make_wgrad_stream(dev) if dev.type == "cuda" and os.environ.get("DPA_WGRAD_STREAM", "1") == "1"
                         else None)
         self._wev = [DevEvent() for _ in L] if self.wstream is not None else None
         self._join = StreamJoin() if self.wstream is not None else None
@@ -224,6 +225,19 @@ class VGGEngine:
         self.eval_acc = torch.zeros(2, **f32)
         self._eval_dirty = True
         self.init_parameters(seed=None)
+
+    def _make_wgrad_stream(self, dev: torch.device):
+        """The weight-gradient stream.  ``DPA_WGRAD_PRIO=low`` (default) creates it at HIP's lowest
+        stream priority, so when both streams have work queued the dispatcher serves the main
+        stream (the dgrad -> BN-backward critical path) first; ``normal`` uses a default-priority
+        torch stream."""
+        if os.environ.get("DPA_WGRAD_PRIO", "low") != "low":
+            return torch.cuda.Stream(dev)
+        least, _greatest = self.K.stream_priority_range()
+        with torch.cuda.device(dev):
+            ptr = self.K.stream_create(least)
+        weakref.finalize(self, self.K.stream_destroy, ptr)
+        return torch.cuda.ExternalStream(ptr, device=dev)
 
     # ------------------------------------------------------------------ parameters / state
     @torch.no_grad()
