@@ -25,6 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_cifar  # noqa: E402
 from distributed_pytorch_amd.engine import VGGEngine  # noqa: E402
+from distributed_pytorch_amd.graph_step import GraphedStep  # noqa: E402
 from distributed_pytorch_amd.parallel import init_env, make_sync  # noqa: E402
 
 BASELINE_METRIC = "images/sec whole-node VGG-11 CIFAR-10 at 1/2/4/8 MI355X; scaling efficiency"  # BASELINE.json
@@ -46,6 +47,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--graph", default="auto", choices=["auto", "off", "on"],
+                    help="replay the captured step as a HIP graph (graph_step.py); auto = on for a single GPU")
     ap.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
                     help="conv kernels: x3 = fp32-grade results from bf16 matrix cores (3 bf16 planes per "
                          "operand, 6 plane products; default) | fp32 = fp32 MFMA | bf16 = mixed precision")
@@ -73,9 +76,14 @@ def main():
             ep += 1
 
     it = batches()
+    graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
+               if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
 
     def step():
         x, t = next(it)
+        if graphed is not None:
+            graphed.run(x, t)
+            return
         sync.begin_step()
         engine.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
                                 params_free=sync.params_free)
@@ -117,6 +125,7 @@ def main():
             "vs_baseline": round(img_s / base, 2) if base else None,
             "dtype": "bf16" if a.impl == "bf16" else "fp32",
             "conv_impl": a.impl,
+            "hip_graph": graphed is not None and graphed.graph is not None,
             "data": "synthetic (CIFAR-10-shaped uint8 on device, random-crop/flip/normalize each step)",
             "config": {"model": a.model, "global_batch": a.batch * ctx.world, "seq_len": None, "image_size": 32,
                        "parallelism": f"dp{ctx.world}", "sync_mode": a.mode, "comm": ctx.comm.name,

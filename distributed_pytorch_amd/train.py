@@ -25,6 +25,7 @@ import torch
 
 from .data import DeviceLoader, ShardSampler, get_datasets
 from .engine import VGGEngine
+from .graph_step import GraphedStep
 from .parallel import DistContext, env_dict, init_cli, init_env, init_single, make_sync
 from .utils import checkpoint
 from .utils.profiling import enable_tracing, trace_range
@@ -37,6 +38,19 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+def _eager_step(engine: VGGEngine, sync, x: torch.Tensor, target: torch.Tensor):
+    with trace_range("step"):
+        sync.begin_step()
+        with trace_range("fwd_bwd"):
+            engine.forward_backward(x, target, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                                    params_free=sync.params_free)
+        with trace_range("sync"):
+            gscale = sync.finish()
+        with trace_range("sgd"):
+            sync.update(gscale)
+        engine.finish_step()
+
+
 def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: DistContext, args,
                 start_batch: int = 0, stats: Optional[dict] = None):
     dev = engine.device
@@ -46,17 +60,14 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
     t_epoch0 = None
     max_iters = getattr(args, "max_iters", None)
     ck_every = getattr(args, "checkpoint_every", 0) or 0
+    graphed = GraphedStep(engine, sync) if getattr(args, "graph", False) and not sync.active and dev.type == "cuda" \
+        else None
     for batch_idx, (x, target) in enumerate(loader.iterate(start_batch), start=start_batch):
-        with trace_range("step"):
-            sync.begin_step()
-            with trace_range("fwd_bwd"):
-                engine.forward_backward(x, target, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
-                                        params_free=sync.params_free)
-            with trace_range("sync"):
-                gscale = sync.finish()
-            with trace_range("sgd"):
-                sync.update(gscale)
-            engine.finish_step()
+        if graphed is not None:
+            with trace_range("step_graph"):
+                graphed.run(x, target)
+        else:
+            _eager_step(engine, sync, x, target)
         n_iters += 1
         if batch_idx == start_batch:
             _sync(dev)
@@ -139,6 +150,8 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--max-iters", type=int, default=None, help="stop each epoch after this many iterations")
     g.add_argument("--no-eval", action="store_true")
     g.add_argument("--trace", action="store_true", help="emit roctx ranges (rocprofv3 --marker-trace)")
+    g.add_argument("--graph", action="store_true",
+                   help="single rank: replay the training step as a captured HIP graph (graph_step.py)")
     g.add_argument("--json-metrics", default=None, help="append a JSON metrics line per epoch to this file")
     g.add_argument("--port", type=int, default=6585)
     return ap

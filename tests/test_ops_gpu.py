@@ -474,3 +474,43 @@ def test_wgrad_stream_matches_single_stream(monkeypatch):
         torch.cuda.synchronize()
         outs.append(e.params.flat.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("impl", ["x3", "bf16"])
+def test_graphed_step_matches_eager(impl):
+    """The captured HIP-graph step (both streams, fused SGD) replays to bit-identical parameters,
+    momentum and loss as the eager step, across several replays."""
+    from distributed_pytorch_amd.engine import VGGEngine
+    from distributed_pytorch_amd.graph_step import GraphedStep
+    from distributed_pytorch_amd.parallel import NullComm, make_sync
+
+    g = torch.Generator().manual_seed(21)
+    batches = [(torch.randn(32, 32, 32, 4, generator=g), torch.randint(0, 10, (32,), generator=g)) for _ in range(5)]
+    outs = []
+    for graph in (False, True):
+        e = VGGEngine("VGG11", "cuda", max_batch=32, impl=impl, lr=0.02)
+        e.init_parameters(seed=4)
+        sync = make_sync("ddp", e, NullComm())
+        gs = GraphedStep(e, sync, warmup=2) if graph else None
+        xb = torch.empty(32, 32, 32, 4, device="cuda")
+        tb = torch.empty(32, dtype=torch.int64, device="cuda")
+        losses = []
+        for x, t in batches:
+            xb.copy_(x)
+            xb[..., 3] = 0
+            tb.copy_(t)
+            if gs is not None:
+                gs.run(xb, tb)
+            else:
+                sync.begin_step()
+                e.forward_backward(xb, tb, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
+                                   params_free=sync.params_free)
+                sync.update(sync.finish())
+                e.finish_step()
+            losses.append(e.loss.clone())
+        torch.cuda.synchronize()
+        if gs is not None:
+            assert gs.replays == 3 and gs.graph is not None
+        outs.append((e.params.flat.clone(), e.mom.flat.clone(), torch.stack(losses)))
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert torch.equal(a_, b_)
