@@ -69,6 +69,34 @@ def split_planes(x: torch.Tensor, np_: int) -> torch.Tensor:
     return out
 
 
+def weight_planes(w: torch.Tensor, np_: int) -> torch.Tensor:
+    """Operand planes of a conv weight: the cached copy the optimizer keeps current
+    (``w._dpa_planes``, refreshed inside the fused SGD kernel, see parallel/ddp.py) when it is
+    still valid for this tensor version, else a fresh split."""
+    pl = getattr(w, "_dpa_planes", None)
+    if pl is not None and pl.shape[0] == np_ and getattr(w, "_dpa_planes_ver", -1) == w._version:
+        return pl
+    return split_planes(w, np_)
+
+
+def grad_slot(p: torch.Tensor, uses: int) -> Optional[torch.Tensor]:
+    """Where a parameter gradient may be written directly: the optimizer arena view
+    (``p._dpa_grad_slot()``), when the parameter has no gradient yet this step and was used once
+    in this forward.  The view is handed back to autograd, whose AccumulateGrad adopts it as
+    ``p.grad`` instead of running a copy / add kernel per parameter."""
+    slot = getattr(p, "_dpa_grad_slot", None)
+    if slot is None or p.grad is not None or uses != 1:
+        return None
+    return slot()
+
+
+def note_use(p: torch.Tensor) -> int:
+    """Count uses of a parameter in the current forward (the DDP wrapper resets the count)."""
+    n = getattr(p, "_dpa_uses", 0) + 1
+    p._dpa_uses = n
+    return n
+
+
 # ------------------------------------------------------------------ conv launch configuration
 # Per-call (tile, splits, posmajor): measured table (tuning/generic_mi355x.json, written by the
 # autotuner: ``set_autotune(True)``, e.g. ``bench_resnet.py --autotune``), else a heuristic.
@@ -188,13 +216,14 @@ class Conv2dNHWC(torch.autograd.Function):
         P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
         ctx.geom = (N, H, W, C, K, R, S, stride, pad, P, Q)
         ctx.impl = impl
+        ctx.w_param, ctx.w_use = w, note_use(w)
         if not _native(x):
             z = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
             ctx.save_for_backward(x, w)
             return z.permute(0, 2, 3, 1).contiguous()
         Kx = _ext.require()
         np_ = NPLANES[impl]
-        xp, wp = split_planes(x, np_), split_planes(w, np_)
+        xp, wp = split_planes(x, np_), weight_planes(w, np_)
         act_dtype = torch.bfloat16 if np_ == 1 else torch.float32
         ctx.x_dtype = x.dtype if np_ == 3 else torch.bfloat16
         z = torch.empty(N, P, Q, K, device=x.device, dtype=act_dtype)
@@ -225,6 +254,9 @@ class Conv2dNHWC(torch.autograd.Function):
                 dx = torch.nn.grad.conv2d_input(xn.shape, wn, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
             if ctx.needs_input_grad[1]:
                 dw = torch.nn.grad.conv2d_weight(xn, wn.shape, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
+                slot = grad_slot(ctx.w_param, ctx.w_use)
+                if slot is not None:
+                    dw = slot.copy_(dw)
             return dx, dw, None, None, None
         Kx = _ext.require()
         xp, wp = a, b
@@ -243,7 +275,9 @@ class Conv2dNHWC(torch.autograd.Function):
                                 lambda s: 4 * s * N * H * W * C)
             run_d(cfg[0], Kx.x3_splits(R * S * K, cfg[1]), cfg[2])
         if ctx.needs_input_grad[1]:
-            dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
+            dw = grad_slot(ctx.w_param, ctx.w_use)
+            if dw is None:
+                dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
 
             def run_w(tile, s, pm):
                 slab = WS.get("slab", s * K * R * S * C, dz.device) if s > 1 else None
@@ -279,6 +313,8 @@ class BnActNHWC(torch.autograd.Function):
         a = torch.empty_like(z)
         K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None)
         ctx.act, ctx.training = act, training
+        ctx.params = (gamma, beta)
+        ctx.uses = (note_use(gamma), note_use(beta)) if training else (0, 0)
         ctx.save_for_backward(z, res if act == 2 else None, gamma, mean, invstd, scale, shift)
         return a
 
@@ -293,7 +329,11 @@ class BnActNHWC(torch.autograd.Function):
         K = _ext.require() if native else cpu_ref
         f32 = dict(device=z.device, dtype=torch.float32 if native else z.dtype)
         dz = torch.empty_like(z)
-        dgamma, dbeta = torch.empty(C, **f32), torch.empty(C, **f32)
+        dgamma, dbeta = (grad_slot(p, u) for p, u in zip(ctx.params, ctx.uses))
+        if dgamma is None or dgamma.dtype != f32["dtype"]:
+            dgamma = torch.empty(C, **f32)
+        if dbeta is None or dbeta.dtype != f32["dtype"]:
+            dbeta = torch.empty(C, **f32)
         dres = torch.empty_like(z) if ctx.act == 2 else None
         part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), z.device, zero=True) if native else None
         coef = torch.empty(3 * C, **f32)

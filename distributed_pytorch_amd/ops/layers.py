@@ -24,6 +24,7 @@ class Conv2d(nn.Module):
         self.cin, self.cout, self.k, self.stride, self.padding, self.impl = cin, cout, k, stride, padding, impl
         self.cin_pad = _pad8(cin)
         self.weight = nn.Parameter(Fn.kaiming_uniform_krsc(cout, k, k, self.cin_pad, cin))
+        self.weight._dpa_direct = True  # the conv backward can write its gradient into an optimizer slot
         self._register_state_dict_hook(Conv2d._to_oihw)
         self._register_load_state_dict_pre_hook(self._from_oihw)
 
@@ -60,6 +61,7 @@ class BatchNorm2d(nn.Module):
         self.c, self.act, self.momentum, self.eps = c, act, momentum, eps
         self.weight = nn.Parameter(torch.ones(c))
         self.bias = nn.Parameter(torch.zeros(c))
+        self.weight._dpa_direct = self.bias._dpa_direct = True  # BN backward writes into optimizer slots
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))

@@ -23,6 +23,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn as nn
 
+from ..ops.functional import NPLANES
 from .comm import Comm, NullComm
 
 ALIGN = 64
@@ -62,12 +63,20 @@ class DistributedDataParallel(nn.Module):
         self._params = order
         self._pflat = _Flat(order, dt, dev)
         self._gflat = _Flat(order, dt, dev)
+        # parameters whose producing kernel writes its gradient straight into the arena slot (conv
+        # weights, BN affine: ops/functional.grad_slot) keep p.grad = None until backward hands
+        # autograd the arena view; the rest accumulate into a pre-assigned arena view
+        self._direct = [bool(getattr(p, "_dpa_direct", False)) for p in order]
         with torch.no_grad():
             for i, p in enumerate(order):
                 v = self._pflat.view(i, p)
                 v.copy_(p.data)
                 p.data = v
-                p.grad = self._gflat.view(i, p)
+                if self._direct[i]:
+                    p._dpa_grad_slot = (lambda i=i, p=p: self._gflat.view(i, p))
+                    p.grad = None
+                else:
+                    p.grad = self._gflat.view(i, p)
         # buckets: contiguous arena slices of ~bucket_mb, cut at tensor boundaries
         cap = max(1, int(bucket_mb * (1 << 20) / self._gflat.flat.element_size()))
         self._buckets: List[List[int]] = []
@@ -102,6 +111,32 @@ class DistributedDataParallel(nn.Module):
         self._reset()
         if self.active:
             self._broadcast_state()
+        self._init_planes(order, dev)
+
+    def _init_planes(self, order, dev):
+        """bf16 operand planes of the conv weights, kept current by the fused SGD kernel (one
+        split per update instead of one per conv call): [NP, arena] bf16, each conv weight reads
+        its slice (ops/functional.weight_planes)."""
+        self._planes = None
+        convs = [m for m in self.module.modules() if hasattr(m, "impl") and hasattr(m, "cin_pad")]
+        nps = {NPLANES.get(m.impl) for m in convs}
+        if dev.type != "cuda" or len(nps) != 1 or None in nps or self._pflat.flat.dtype != torch.float32:
+            return
+        np_ = nps.pop()
+        from .. import _ext
+
+        self._planes = torch.empty(np_, self._pflat.flat.numel(), dtype=torch.bfloat16, device=dev)
+        _ext.require().split_planes(self._pflat.flat, self._planes)
+        conv_w = {id(m.weight) for m in convs}
+        for i, p in enumerate(order):
+            if id(p) in conv_w:
+                o = self._pflat.offsets[i]
+                p._dpa_planes = self._planes[:, o:o + p.numel()].view((np_,) + tuple(p.shape))
+                p._dpa_planes_ver = p._version
+
+    @property
+    def weight_planes(self) -> Optional[torch.Tensor]:
+        return self._planes
 
     # ---------------------------------------------------------------- state sync
     def _broadcast_state(self):
@@ -117,6 +152,8 @@ class DistributedDataParallel(nn.Module):
 
     def forward(self, *args, **kwargs):
         self._reset()
+        for p in self._params:
+            p._dpa_uses = 0
         if self.active and self.broadcast_buffers and self._bufs and self.module.training:
             with self.comm.region():
                 for fl in self._bufs:
@@ -161,6 +198,9 @@ class DistributedDataParallel(nn.Module):
 
     def zero_grad(self, set_to_none: bool = False):
         self._gflat.flat.zero_()
+        for p, d in zip(self._params, self._direct):
+            if d:
+                p.grad = None  # backward hands autograd the arena view again
 
     @property
     def flat_params(self) -> torch.Tensor:
@@ -194,7 +234,7 @@ class FlatSGD:
             from .. import _ext
 
             _ext.require().sgd_flat(p, g, self.buf, self.lr, self.momentum, self.weight_decay, grad_scale,
-                                    self.steps == 0)
+                                    self.steps == 0, 0, -1, self.ddp.weight_planes)
         else:
             from ..ops import cpu_ref
 
