@@ -48,6 +48,10 @@ int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
                       int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
                       int tile, int reduce, int posmajor, int np, int obf, hipStream_t st);
+int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
+                    int bf, hipStream_t st);
+int dpa_maxpool_bwd(const void* dy, const unsigned char* arg, void* dx, int N, int H, int W, int C, int k, int s,
+                    int p, int bf, hipStream_t st);
 int dpa_augment(const unsigned char* img, const long long* idx, const long long* labels, float* out,
                 long long* target, int B, int Hs, int Ws, int pad, int train, unsigned long long seed,
                 unsigned long long salt, const float* mean, const float* std, hipStream_t st);
@@ -512,6 +516,38 @@ void augment(Tensor images, Tensor idx, Tensor labels, Tensor out, OptT target, 
       "augment");
 }
 
+// ---------------- NHWC max-pool (generic path) ----------------
+void maxpool_check(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, name, " must be a contiguous 4-D GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, name, " must be fp32 or bf16");
+}
+
+void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t k, int64_t s, int64_t p) {
+  maxpool_check(x, "x");
+  maxpool_check(y, "y");
+  TORCH_CHECK(y.scalar_type() == x.scalar_type() && arg.scalar_type() == at::kByte && arg.sizes() == y.sizes() &&
+                  arg.is_contiguous(), "maxpool_fwd: y/arg shape or dtype");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(y.size(0) == N && y.size(1) == (H + 2 * p - k) / s + 1 && y.size(2) == (W + 2 * p - k) / s + 1 &&
+                  y.size(3) == C, "maxpool_fwd: output shape");
+  chk(dpa_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)s, (int)p,
+                      x.scalar_type() == at::kBFloat16 ? 1 : 0, cur_stream()),
+      "maxpool_fwd");
+}
+
+void maxpool_bwd(Tensor dy, Tensor arg, Tensor dx, int64_t k, int64_t s, int64_t p) {
+  maxpool_check(dy, "dy");
+  maxpool_check(dx, "dx");
+  TORCH_CHECK(dx.scalar_type() == dy.scalar_type() && arg.scalar_type() == at::kByte && arg.sizes() == dy.sizes() &&
+                  arg.is_contiguous(), "maxpool_bwd: dy/arg shape or dtype");
+  const int N = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3);
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == (H + 2 * p - k) / s + 1 && dy.size(2) == (W + 2 * p - k) / s + 1 &&
+                  dy.size(3) == C, "maxpool_bwd: gradient shape");
+  chk(dpa_maxpool_bwd(dy.data_ptr(), arg.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, (int)k, (int)s, (int)p,
+                      dx.scalar_type() == at::kBFloat16 ? 1 : 0, cur_stream()),
+      "maxpool_bwd");
+}
+
 // ---------------- RCCL communicator ----------------
 ncclDataType_t nccl_dtype(const Tensor& t) {
   switch (t.scalar_type()) {
@@ -648,6 +684,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fc_ce_train", &fc_ce_train);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
   // A HIP stream with an explicit priority (lower number = higher priority; HIP's range is reported
   // by stream_priority_range()).  Owned by the caller; lives until stream_destroy.
   m.def("stream_create", [](int64_t priority) {

@@ -352,8 +352,34 @@ def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, 
                            bool(training), float(momentum), float(eps), a)
 
 
+class MaxPoolNHWC(torch.autograd.Function):
+    """k x k / stride / pad max-pool on NHWC (fp32 or bf16) over csrc/kernels/pool.hip: the
+    forward keeps a one-byte window position per output element, the backward gathers."""
+
+    @staticmethod
+    def forward(ctx, x, k: int, stride: int, pad: int):
+        N, H, W, C = x.shape
+        P, Q = conv_out(H, k, stride, pad), conv_out(W, k, stride, pad)
+        y = torch.empty(N, P, Q, C, device=x.device, dtype=x.dtype)
+        arg = torch.empty(N, P, Q, C, device=x.device, dtype=torch.uint8)
+        _ext.require().maxpool_fwd(x, y, arg, k, stride, pad)
+        ctx.save_for_backward(arg)
+        ctx.geom = (N, H, W, C, k, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, H, W, C, k, stride, pad = ctx.geom
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=dy.dtype)
+        _ext.require().maxpool_bwd(dy.contiguous(), arg, dx, k, stride, pad)
+        return dx, None, None, None
+
+
 def max_pool_nhwc(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -> torch.Tensor:
-    """Max-pool on an NHWC tensor (channels_last view; stem pooling is a minor op)."""
+    """Max-pool on an NHWC tensor: the native kernels on GPU (C % 8 == 0), torch on CPU."""
+    if _native(x) and x.shape[-1] % 8 == 0 and x.dtype in (torch.float32, torch.bfloat16):
+        return MaxPoolNHWC.apply(x.contiguous(), int(k), int(stride), int(pad))
     y = F.max_pool2d(x.permute(0, 3, 1, 2), k, stride, pad)
     return y.permute(0, 2, 3, 1).contiguous()
 

@@ -161,3 +161,25 @@ def test_bf16_activation_path_dtypes_and_accuracy():
     assert rel(nchw(xd.grad), torch.nn.grad.conv2d_input(list(nchw(x).shape), wb, dzr, padding=1)) < 1e-2
     assert rel(nchw(wd.grad), torch.nn.grad.conv2d_weight(nchw(x), list(wb.shape), dzr, padding=1)) < 1e-2
     assert rel(rmd, torch.zeros(K).double() * 0.9 + 0.1 * zr.detach().mean((0, 2, 3))) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,k,s,p", [((2, 112, 112, 64), 3, 2, 1), ((3, 9, 7, 16), 3, 2, 1),
+                                         ((2, 8, 8, 8), 2, 2, 0), ((1, 10, 10, 24), 3, 1, 1)])
+def test_maxpool_nhwc_matches_torch(shape, k, s, p, dtype):
+    """Native NHWC max-pool (pool.hip) == torch max_pool2d forward and backward, including ties
+    (first max in window scan order) and windows cut by the padding."""
+    from distributed_pytorch_amd.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(shape, generator=g).round(decimals=1).to(dtype)  # rounding makes ties common
+    xg = x.cuda().requires_grad_(True)
+    y = Fn.max_pool_nhwc(xg, k, s, p)
+    dy = torch.randn(y.shape, generator=g).to(dtype)
+    (dx,) = torch.autograd.grad(y, xg, dy.cuda())
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    (dxr,) = torch.autograd.grad(yr, xr, dy.double().permute(0, 3, 1, 2))
+    assert torch.equal(y.cpu().double(), yr.detach().permute(0, 2, 3, 1))
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert (dx.cpu().double() - dxr.permute(0, 2, 3, 1)).abs().max() <= tol * dxr.abs().max()
