@@ -137,14 +137,28 @@ def save_tuning_table(path: Optional[str] = None):
     _AUTOTUNE["dirty"] = False
 
 
+def halo_candidates(kind: str, geom: tuple) -> Tuple[int, ...]:
+    """Halo-staged tiles (conv_x3.hip, ids >= 16) that can run this conv call: 3x3, stride 1,
+    pad 1 only, channel / row-width limits as in engine.halo_ok."""
+    from ..engine import HALO_TILES, HALO_WGRAD_TILES, halo_ok
+
+    N, H, W, C, K, R, S, stride, pad = geom
+    if (R, S, stride, pad) != (3, 3, 1, 1):
+        return ()
+    if kind == "wgrad":
+        return tuple(t for t in HALO_WGRAD_TILES if halo_ok("wgrad", t, W, C, K))
+    cred, cout = (C, K) if kind == "fprop" else (K, C)
+    return tuple(t for t in HALO_TILES if halo_ok(kind, t, W, cred, cout))
+
+
 def _autotune(key: str, kind: str, red: int, run: Callable[[int, int, bool], None],
-              slab_bytes: Callable[[int], int]) -> Tuple[int, int, bool]:
+              slab_bytes: Callable[[int], int], extra_tiles: Tuple[int, ...] = ()) -> Tuple[int, int, bool]:
     Kx = _ext.require()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best = None
     splits = (1, 2, 4, 8, 16, 32, 64, 128, 256) if kind == "wgrad" else (1, 2, 4, 8, 16)
     seen = set()
-    for tile in range(N_TILES):
+    for tile in tuple(range(N_TILES)) + tuple(extra_tiles):
         for s0 in splits:
             s = Kx.x3_splits(red, s0)
             for pm in (False, True):
@@ -176,7 +190,7 @@ def choose_config(impl: str, kind: str, geom: tuple, M: int, Ngemm: int, Kred: i
     if t is not None:
         c = (int(t[0]), int(t[1]), bool(t[2]))
     elif _AUTOTUNE["on"] and run is not None:
-        c = _autotune(key, kind, M if kind == "wgrad" else Kred, run, slab_bytes)
+        c = _autotune(key, kind, M if kind == "wgrad" else Kred, run, slab_bytes, halo_candidates(kind, geom))
     else:
         c = conv_config(kind, M, Ngemm, Kred, hw_small)
     _chosen[key] = c
