@@ -108,6 +108,23 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, long elem_off, 
 
 enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
 
+// The plane products of one k-slice over a TM x TN register tile, product-major: the TM*TN
+// accumulators are independent, so back-to-back MFMAs never wait on each other's result (an
+// accumulator-major order gives chains of six dependent MFMAs).  Each accumulator still sees its
+// products smallest-first, so results are unchanged bit for bit.
+template <int TM, int TN, int NP>
+__device__ __forceinline__ void mfma_tile(f32x16 (&acc)[TM][TN], const bf16x8 (&fa)[TM][NP],
+                                          const bf16x8 (&fb)[TN][NP]) {
+  constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};  // (A plane, B plane)
+#pragma unroll
+  for (int q = NP == 3 ? 0 : 5; q < 6; ++q)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][PA[q]], fb[j][PB[q]], acc[i][j], 0, 0, 0);
+}
+
 // BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  LDS image layouts: see the
 // APITCH/BPITCH comment in the kernel (XOR swizzles, conflict-free fragment reads).
 // NSTAGE: 2 = double-buffered LDS (one barrier per k step); 1 = single LDS stage + register
@@ -410,20 +427,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         else
           fb[j][p] = frag_k(Bs + p * B_PLANE, BPITCH, wc * WTN + j * 32, ks);
       }
-    // smallest products first
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (NP == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-        }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-      }
+    mfma_tile<TM, TN, NP>(acc, fa, fb);  // smallest products first
     }
   };
 
@@ -739,19 +743,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
           else
             fb[j][p] = frag_k(Bst + p * B_PLANE, wc * WTN + j * 32 + li, ks);
         }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (NP == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-        }
+      mfma_tile<TM, TN, NP>(acc, fa, fb);
     }
   };
 
