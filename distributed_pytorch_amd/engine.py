@@ -227,11 +227,11 @@ class VGGEngine:
         self.init_parameters(seed=None)
 
     def _make_wgrad_stream(self, dev: torch.device):
-        """The weight-gradient stream.  ``DPA_WGRAD_PRIO=low`` (default) creates it at HIP's lowest
-        stream priority, so when both streams have work queued the dispatcher serves the main
-        stream (the dgrad -> BN-backward critical path) first; ``normal`` uses a default-priority
-        torch stream."""
-        if os.environ.get("DPA_WGRAD_PRIO", "low") != "low":
+        """The weight-gradient stream: a default-priority torch stream.  ``DPA_WGRAD_PRIO=low``
+        creates it at HIP's lowest priority instead (A/B only: no gain without a communicator,
+        and with the RCCL comm stream present the mixed queue priorities cost 28 % of the step,
+        docs/PERF_NOTES.md)."""
+        if os.environ.get("DPA_WGRAD_PRIO", "normal") != "low":
             return torch.cuda.Stream(dev)
         least, _greatest = self.K.stream_priority_range()
         with torch.cuda.device(dev):
