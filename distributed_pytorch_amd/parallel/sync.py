@@ -294,10 +294,12 @@ class DDPSync(GradSync):
         # each training forward (torch nn/parallel/distributed.py:2178).
         if not self.active or not self.broadcast_buffers:
             return
+        # The num_batches_tracked counters are not re-broadcast per step: every replica advances
+        # them once per training forward, so after the start-up broadcast (broadcast_state) they
+        # agree by construction -- one collective per step instead of two.
         e = self.engine
         with self.comm.region():
             self.comm.broadcast(e.buffers.flat, 0)
-            self.comm.broadcast(e.nbt, 0)
         return self.comm.wait
 
     def reduce_bucket(self, b: Bucket):
