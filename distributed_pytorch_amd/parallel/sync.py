@@ -40,6 +40,10 @@ from ..utils.streams import DevEvent, StreamJoin
 from .comm import Comm
 
 
+# DPA_BUF_BCAST=pre restores the per-forward buffer broadcast of torch DDP (A/B); default post
+_POST_FORWARD_BUFFERS = os.environ.get("DPA_BUF_BCAST", "post") != "pre"
+
+
 class Bucket:
     __slots__ = ("names", "lo", "hi", "pending", "issued", "busy", "stepped", "free_ev")
 
@@ -288,18 +292,37 @@ class DDPSync(GradSync):
                  broadcast_buffers: bool = True):
         super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
         self.broadcast_buffers = broadcast_buffers
+        self._bufs_fresh = False  # replicas hold rank 0's running stats (sent after the last forward)
+        self._bufs_sent = False   # ... sent during the current step
+
+    # DDP._sync_buffers (torch nn/parallel/distributed.py:2178): rank 0's BN running stats
+    # overwrite every replica's before each training forward.  Nothing touches the running stats
+    # between the end of one training forward and the start of the next, so the broadcast is
+    # issued as soon as this step's forward is done (first grad_ready), where it runs on the comm
+    # stream under the backward; the next forward then finds the replicas already in sync and
+    # needs no stream hop.  The num_batches_tracked counters advance identically on every replica
+    # after the start-up broadcast, so they are not re-sent.
+    def _send_buffers(self):
+        with self.comm.region():
+            self.comm.broadcast(self.engine.buffers.flat, 0)
+
+    def begin_step(self):
+        super().begin_step()
+        self._bufs_sent = False
+
+    def grad_ready(self, names: List[str]):
+        if self.active and self.broadcast_buffers and not self._bufs_sent and _POST_FORWARD_BUFFERS:
+            self._send_buffers()  # the engine reports gradients only once the forward is done
+            self._bufs_sent = self._bufs_fresh = True
+        super().grad_ready(names)
 
     def pre_forward(self):
-        # DDP._sync_buffers: rank 0's BN running stats/counters overwrite every replica's before
-        # each training forward (torch nn/parallel/distributed.py:2178).
         if not self.active or not self.broadcast_buffers:
-            return
-        # The num_batches_tracked counters are not re-broadcast per step: every replica advances
-        # them once per training forward, so after the start-up broadcast (broadcast_state) they
-        # agree by construction -- one collective per step instead of two.
-        e = self.engine
-        with self.comm.region():
-            self.comm.broadcast(e.buffers.flat, 0)
+            return None
+        if self._bufs_fresh:  # already broadcast after the previous training forward
+            self._bufs_fresh = False
+            return None
+        self._send_buffers()  # first forward, or a caller that bypasses grad_ready
         return self.comm.wait
 
     def reduce_bucket(self, b: Bucket):
