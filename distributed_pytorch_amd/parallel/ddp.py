@@ -109,6 +109,8 @@ class DistributedDataParallel(nn.Module):
                     b.data = v
             self._bufs.append(fl)
         self._reset()
+        self._bufs_sent = False   # buffers broadcast during the current step (first gradient hook)
+        self._bufs_fresh = False  # replicas already hold rank 0's buffers for the next forward
         if self.active:
             self._broadcast_state()
         self._init_planes(order, dev)
@@ -150,20 +152,35 @@ class DistributedDataParallel(nn.Module):
         self._pending = [len(b) for b in self._buckets]
         self._issued = [False] * len(self._buckets)
 
+    def _send_buffers(self):
+        with self.comm.region():
+            for fl in self._bufs:
+                self.comm.broadcast(fl.flat, 0)
+
     def forward(self, *args, **kwargs):
         self._reset()
         for p in self._params:
             p._dpa_uses = 0
         if self.active and self.broadcast_buffers and self._bufs and self.module.training:
-            with self.comm.region():
-                for fl in self._bufs:
-                    self.comm.broadcast(fl.flat, 0)
-            self.comm.wait()
+            if self._bufs_fresh:  # broadcast right after the previous training forward
+                self._bufs_fresh = False
+            else:
+                self._send_buffers()
+                self.comm.wait()
+        self._bufs_sent = False
         return self.module(*args, **kwargs)
 
     # ---------------------------------------------------------------- gradient buckets
     def _make_hook(self, i: int):
         def hook(_p):
+            # first gradient of the step: the forward is over, so rank 0's buffers (BN running
+            # stats) are final for this step -- broadcast them now, under the backward, instead of
+            # before the next forward (nothing changes them in between; finish() orders the
+            # compute stream after the comm stream)
+            if not self._bufs_sent and self.active and self.broadcast_buffers and self._bufs \
+                    and self.module.training:
+                self._send_buffers()
+                self._bufs_sent = self._bufs_fresh = True
             b = self._bucket_of[i]
             self._pending[b] -= 1
             if self._pending[b] == 0 and self.overlap:
