@@ -193,16 +193,14 @@ class GradSync:
         """Enqueue the fused SGD of bucket b once its gradients are final (collective issued) and
         its parameters are free.  Runs on the comm stream behind the collective; for a single rank
         on the engine's wgrad stream (else inline on the current stream)."""
-        if not self.fuse_step or b.stepped or b.pending or b.busy or (self.active and not b.issued):
+        if not self._step_ready(b) or (self.active and not b.issued):
+            return
+        if self.active:
+            with self.comm.region():  # comm stream: behind the collective, after the triggering stream
+                self._step_here(b)
             return
         b.stepped = True
         scale = self.grad_scale()
-        if self.active:
-            with self.comm.region():  # comm stream: behind the collective, after the triggering stream
-                if b.free_ev is not None:
-                    b.free_ev.wait(torch.cuda.current_stream(self.engine.device))
-                self.engine.sgd_step(scale, b.lo, b.numel)
-            return
         s = self.engine.wstream if self._cuda else None
         if s is None:
             self.engine.sgd_step(scale, b.lo, b.numel)
@@ -212,11 +210,24 @@ class GradSync:
         with torch.cuda.stream(s):
             self.engine.sgd_step(scale, b.lo, b.numel)
 
+    def _step_ready(self, b: Bucket) -> bool:
+        return self.fuse_step and not b.stepped and not b.pending and not b.busy
+
+    def _step_here(self, b: Bucket):
+        """The bucket's SGD on the current stream (the comm stream, inside a region), after the
+        main-stream event that follows the last reader of its parameters."""
+        b.stepped = True
+        if b.free_ev is not None:
+            b.free_ev.wait(torch.cuda.current_stream(self.engine.device))
+        self.engine.sgd_step(self.grad_scale(), b.lo, b.numel)
+
     def _issue(self, b: Bucket):
         b.issued = True
         self.issued_bytes += 4 * b.numel
         with self.comm.region():
             self.reduce_bucket(b)
+            if self._step_ready(b):  # parameters already free: update in the same region (one join)
+                self._step_here(b)
 
     def reduce_bucket(self, b: Bucket):
         raise NotImplementedError
