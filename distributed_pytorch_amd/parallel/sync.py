@@ -19,8 +19,8 @@ Differences from the reference, all by design:
 * buckets are cut at layer boundaries with an xGMI-sized cap (``bucket_mb``, default 10 MiB: the
   three 9 MiB [512,512,3,3] weights each get a bucket; the last-ready bucket is kept small so the
   exposed tail after backward is short) instead of DDP's 25 MiB/1 MiB;
-* all modes broadcast rank 0's parameters and buffers once at start, so replicas
-  cannot silently fork;
+* all modes broadcast rank 0's parameters (and momenta, when resuming) once at start (SURVEY
+  §5.4), so replicas cannot silently fork; BN buffers only in the modes that share them (ddp/zero1);
 * the optimizer step is fused per bucket into backward (``overlap=True``): once a bucket's
   collective is issued AND the engine reports its parameters no longer read this step
   (``params_free``: dgrad of that layer enqueued), the fused SGD of that slice is queued behind the
@@ -110,6 +110,10 @@ class GradSync:
 
     # whether this mode's optimizer step can run per bucket inside backward (see module doc)
     fusable_step = True
+    # whether BN buffers are kept equal across ranks (DDP broadcast_buffers).  Modes A/B keep per-rank
+    # statistics: the start-up broadcast then sends only parameters/momenta, so a resumed run keeps
+    # each rank's own running stats (identical at a fresh start anyway: same seed, same init).
+    shared_buffers = False
 
     def __init__(self, engine, comm: Comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
         self.engine = engine
@@ -141,8 +145,9 @@ class GradSync:
         e = self.engine
         with self.comm.region():
             self.comm.broadcast(e.params.flat, 0)
-            self.comm.broadcast(e.buffers.flat, 0)
-            self.comm.broadcast(e.nbt, 0)
+            if self.shared_buffers:
+                self.comm.broadcast(e.buffers.flat, 0)
+                self.comm.broadcast(e.nbt, 0)
             if e.steps_taken > 0:
                 self.comm.broadcast(e.mom.flat, 0)
         self.comm.wait()
@@ -301,6 +306,7 @@ class DDPSync(GradSync):
 
     def __init__(self, engine, comm, bucket_mb: float = 10.0, overlap: bool = True, broadcast_init: bool = True,
                  broadcast_buffers: bool = True):
+        self.shared_buffers = broadcast_buffers
         super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
         self.broadcast_buffers = broadcast_buffers
         self._bufs_fresh = False  # replicas hold rank 0's running stats (sent after the last forward)

@@ -52,12 +52,15 @@ def _eager_step(engine: VGGEngine, sync, x: torch.Tensor, target: torch.Tensor):
 
 
 def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: DistContext, args,
-                start_batch: int = 0, stats: Optional[dict] = None):
+                start_batch: int = 0, stats: Optional[dict] = None, budget: Optional[int] = None) -> Optional[int]:
+    """One epoch (main.py:19-49).  ``budget`` caps the iterations run in this call (the remainder of
+    ``--stop-after-iters``); returns the next batch index when the budget ran out mid-epoch, else None."""
     dev = engine.device
     engine.loss_accum.zero_()
     t_win, win_start = None, None
     n_iters = 0
     t_epoch0 = None
+    stopped_at = None
     max_iters = getattr(args, "max_iters", None)
     ck_every = getattr(args, "checkpoint_every", 0) or 0
     graphed = GraphedStep(engine, sync) if getattr(args, "graph", False) and not sync.active and dev.type == "cuda" \
@@ -95,6 +98,9 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
                             sync.mode, ddp_prefix=sync.mode == "ddp")
         if max_iters and n_iters >= max_iters:
             break
+        if budget is not None and n_iters >= budget and batch_idx + 1 < len(loader):
+            stopped_at = batch_idx + 1
+            break
     _sync(dev)
     if stats is not None and t_epoch0 is not None and n_iters > 1:
         el = time.perf_counter() - t_epoch0
@@ -102,7 +108,9 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
         stats["sec_per_iter"] = el / (n_iters - 1)
         stats["images_per_sec_rank"] = loader.batch_size / stats["sec_per_iter"]
         stats["images_per_sec_total"] = stats["images_per_sec_rank"] * ctx.world
-    return None
+    if stats is not None:
+        stats["iters_run"] = n_iters
+    return stopped_at
 
 
 def test_model(engine: VGGEngine, loader: DeviceLoader, sync=None):
@@ -148,6 +156,9 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--checkpoint-every", type=int, default=0)
     g.add_argument("--resume", action="store_true")
     g.add_argument("--max-iters", type=int, default=None, help="stop each epoch after this many iterations")
+    g.add_argument("--stop-after-iters", type=int, default=None,
+                   help="end the whole run after this many training iterations, mid-epoch if need be, writing a "
+                        "resumable checkpoint (preemption drill for --resume)")
     g.add_argument("--no-eval", action="store_true")
     g.add_argument("--trace", action="store_true", help="emit roctx ranges (rocprofv3 --marker-trace)")
     g.add_argument("--graph", action="store_true",
@@ -178,11 +189,20 @@ def run(ctx: DistContext, mode: str, args):
             if start_batch >= len(train_loader):
                 start_epoch, start_batch = start_epoch + 1, 0
     sync = make_sync(mode, engine, ctx.comm, bucket_mb=args.bucket_mb, overlap=not args.no_overlap)
+    budget = getattr(args, "stop_after_iters", None)
     for epoch in range(start_epoch, args.epochs):
         train_loader.set_epoch(epoch)
         stats = {}
-        train_model(engine, train_loader, sync, epoch, ctx, args, start_batch=start_batch, stats=stats)
+        stopped = train_model(engine, train_loader, sync, epoch, ctx, args, start_batch=start_batch, stats=stats,
+                              budget=budget)
         start_batch = 0
+        if budget is not None:
+            budget -= stats.get("iters_run", 0)
+        if stopped is not None:  # preempted mid-epoch: checkpoint the position, no eval
+            if args.checkpoint_dir:
+                checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch, stopped, args.sampler_seed, ctx.world,
+                                mode, ddp_prefix=mode == "ddp")
+            break
         if args.checkpoint_dir:
             checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch + 1, 0, args.sampler_seed, ctx.world, mode,
                             ddp_prefix=mode == "ddp")
@@ -196,6 +216,8 @@ def run(ctx: DistContext, mode: str, args):
                 rec["test_loss"], rec["test_correct"] = res
             with open(args.json_metrics, "a") as f:
                 f.write(json.dumps(rec) + "\n")
+        if budget is not None and budget <= 0:
+            break
     ctx.shutdown()
 
 

@@ -144,3 +144,38 @@ def test_native_tcp_store(tmp_path):
         assert r["uid"] == list(range(128))
         assert r["max"] == 1.5 * (WORLD - 1) + 0.25
     assert sorted(r["cnt"] for r in res) == list(range(1, WORLD + 1))
+
+
+def _run_ranks(script, args, outdir, world):
+    port = H.free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=H.run_cli_main, args=(r, world, port, script, args, os.path.join(outdir, f"log{r}.txt")))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(600)
+        assert p.exitcode == 0
+
+
+@pytest.mark.parametrize("script,world", [("main_part3.py", WORLD), ("main_all_reduce.py", WORLD)])
+def test_preempt_and_resume_is_bitwise_identical(tmp_path, script, world):
+    """a run stopped mid-epoch (--stop-after-iters, per-rank checkpoint) and resumed
+    (--resume) ends with exactly the parameters, SGD momenta and position of an uninterrupted run."""
+    base = ["--device", "cpu", "--synthetic", "--batch-size", "8", "--train-size", "96", "--test-size", "16",
+            "--epochs", "2", "--no-eval"]  # 6 iterations per epoch per rank at W=2
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    _run_ranks(script, base + ["--checkpoint-dir", a], str(tmp_path), world)
+    _run_ranks(script, base + ["--checkpoint-dir", b, "--stop-after-iters", "8"], str(tmp_path), world)
+    mid = torch.load(os.path.join(b, "rank0.pt"), weights_only=True)
+    assert (mid["epoch"], mid["batch_idx"]) == (1, 2)  # stopped inside the second epoch
+    _run_ranks(script, base + ["--checkpoint-dir", b, "--resume"], str(tmp_path), world)
+    for r in range(world):
+        ca = torch.load(os.path.join(a, f"rank{r}.pt"), weights_only=True)
+        cb = torch.load(os.path.join(b, f"rank{r}.pt"), weights_only=True)
+        assert (ca["epoch"], ca["batch_idx"]) == (cb["epoch"], cb["batch_idx"]) == (2, 0)
+        assert ca["model"].keys() == cb["model"].keys()
+        for k in ca["model"]:
+            assert torch.equal(ca["model"][k], cb["model"][k]), (r, k)
+        for (ia, sa), (ib, sb) in zip(sorted(ca["optimizer"]["state"].items()), sorted(cb["optimizer"]["state"].items())):
+            assert ia == ib and torch.equal(sa["momentum_buffer"], sb["momentum_buffer"]), (r, ia)
