@@ -51,6 +51,25 @@ def _eager_step(engine: VGGEngine, sync, x: torch.Tensor, target: torch.Tensor):
         engine.finish_step()
 
 
+def _fault_point(rank: int, it: int):
+    """Fault injection: ``DPA_FAULT=rank:iter[:kind]`` makes that rank fail at that
+    training iteration — ``exit`` (default: the process dies without cleanup, like a lost node),
+    ``raise`` (a Python error) or ``hang`` (stops issuing collectives; peers must time out)."""
+    spec = os.environ.get("DPA_FAULT")
+    if not spec:
+        return
+    parts = spec.split(":")
+    if int(parts[0]) != rank or int(parts[1]) != it:
+        return
+    kind = parts[2] if len(parts) > 2 else "exit"
+    print(f"[rank {rank}] injected fault '{kind}' at iteration {it}", flush=True)
+    if kind == "raise":
+        raise RuntimeError(f"injected fault at iteration {it}")
+    if kind == "hang":
+        time.sleep(10 ** 6)
+    os._exit(13)
+
+
 def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: DistContext, args,
                 start_batch: int = 0, stats: Optional[dict] = None, budget: Optional[int] = None) -> Optional[int]:
     """One epoch (main.py:19-49).  ``budget`` caps the iterations run in this call (the remainder of
@@ -72,6 +91,7 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
         else:
             _eager_step(engine, sync, x, target)
         n_iters += 1
+        _fault_point(ctx.rank, batch_idx)
         if batch_idx == start_batch:
             _sync(dev)
             t_win = time.perf_counter()

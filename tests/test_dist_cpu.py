@@ -179,3 +179,34 @@ def test_preempt_and_resume_is_bitwise_identical(tmp_path, script, world):
             assert torch.equal(ca["model"][k], cb["model"][k]), (r, k)
         for (ia, sa), (ib, sb) in zip(sorted(ca["optimizer"]["state"].items()), sorted(cb["optimizer"]["state"].items())):
             assert ia == ib and torch.equal(sa["momentum_buffer"], sb["momentum_buffer"]), (r, ia)
+
+
+@pytest.mark.parametrize("kind", ["exit", "hang"])
+def test_lost_rank_fails_peers_instead_of_hanging(tmp_path, monkeypatch, kind):
+    """SURVEY §5.3 fault injection: rank 1 dies (or stops issuing collectives) at iteration 3; the
+    surviving rank must fail with an error within the process-group timeout, never hang."""
+    import time as _time
+
+    monkeypatch.setenv("DPA_FAULT", f"1:3:{kind}")
+    monkeypatch.setenv("DPA_PG_TIMEOUT", "20")
+    args = ["--device", "cpu", "--synthetic", "--batch-size", "8", "--train-size", "160", "--test-size", "16",
+            "--no-eval"]
+    port = H.free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=H.run_cli_main, args=(r, WORLD, port, "main_part3.py", args,
+                                                   str(tmp_path / f"log{r}.txt"))) for r in range(WORLD)]
+    t0 = _time.monotonic()
+    for p in ps:
+        p.start()
+    ps[0].join(240)
+    took = _time.monotonic() - t0
+    alive = ps[0].is_alive()
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    assert not alive, "surviving rank hung after its peer was lost"
+    assert ps[0].exitcode != 0, "surviving rank finished as if nothing happened"
+    if kind == "exit":
+        assert ps[1].exitcode == 13
+    assert took < 200, took
