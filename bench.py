@@ -1,19 +1,28 @@
 """Headline benchmark: VGG-11 / CIFAR-10-shaped training throughput (images/sec, whole job).
 
-BASELINE.json metric: "images/sec whole-node VGG-11 CIFAR-10 at 1/2/4/8 MI355X".  Config is the
-reference's: VGG-11 (BN), batch 256 per rank (weak scaling), SGD(0.1, 0.9, wd 1e-4), fp32 compute
-(the reference trains in fp32), synthetic CIFAR-shaped data on device, random init (seed 1).
-Every timed step is a full training step: on-device augmentation of the batch, forward, loss,
-backward, gradient synchronisation (DDP mode by default: bucketed RCCL all-reduce overlapped with
-backward + BN-buffer broadcast), fused SGD update.
+BASELINE.json metric: "images/sec whole-node VGG-11 CIFAR-10 at 1/2/4/8 MI355X; scaling efficiency".
+Config is the reference's: VGG-11 (BN), batch 256 per rank (weak scaling), SGD(0.1, 0.9, wd 1e-4),
+fp32-grade compute (the reference trains in fp32), synthetic CIFAR-shaped data on device, random
+init (seed 1).  Every timed step is a full training step: on-device augmentation of the batch,
+forward, loss, backward, gradient synchronisation (DDP mode by default: bucketed RCCL all-reduce
+overlapped with backward + BN-buffer broadcast), fused SGD update.
 
-    python bench.py [--gpus 1] [--steps 50] [--warmup 10] [--mode ddp|allreduce|gather]
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+    python bench.py [--gpus N] [--steps 50] [--warmup 10] [--mode ddp|allreduce|gather|zero1]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
+    python bench.py --profile            # the same run under rocprofv3 --kernel-trace --stats
+
+``--gpus N`` without torchrun starts N local ranks itself (parallel/spawn.py: fresh child
+processes, the parent never touches the GPU).  For N > 1, rank 0 first times the same step alone
+(``--solo-steps``, no communicator; the other ranks wait) so the JSON line carries a same-run
+scaling efficiency; after the timed steps a short diagnostic phase records the communication left
+exposed after backward and each bucket's collective time with timing events (kept out of the
+timed region), and the parameter arenas are compared across ranks.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -26,7 +35,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_cifar  # noqa: E402
 from distributed_pytorch_amd.engine import VGGEngine  # noqa: E402
 from distributed_pytorch_amd.graph_step import GraphedStep  # noqa: E402
-from distributed_pytorch_amd.parallel import init_env, make_sync  # noqa: E402
+from distributed_pytorch_amd.parallel import NullComm, init_env, make_sync  # noqa: E402
+from distributed_pytorch_amd.parallel.spawn import is_spawned_child  # noqa: E402
+from distributed_pytorch_amd.utils import benchlib  # noqa: E402
+from distributed_pytorch_amd.utils.profiling import EventProbe, step_comm_report  # noqa: E402
 
 BASELINE_METRIC = "images/sec whole-node VGG-11 CIFAR-10 at 1/2/4/8 MI355X; scaling efficiency"  # BASELINE.json
 # BASELINE.md (reference harness measured on CPU — the only numbers the reference has)
@@ -35,9 +47,9 @@ BASELINE_IMG_S = {1: 397.8, 2: 601.8}
 TORCH_EAGER_IMG_S_PER_GPU = 68699.5
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (reference: 256 per node)")
@@ -55,21 +67,25 @@ def main():
     ap.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
                     help="conv kernels: x3 = fp32-grade results from bf16 matrix cores (3 bf16 planes per "
                          "operand, 6 plane products; default) | fp32 = fp32 MFMA | bf16 = mixed precision")
-    a = ap.parse_args()
+    ap.add_argument("--solo-steps", type=int, default=None,
+                    help="N>1: steps rank 0 times alone first (same-run 1-GPU figure; 0 = skip; default "
+                         "min(steps, 30))")
+    ap.add_argument("--diag-steps", type=int, default=5,
+                    help="diagnostic steps after the timed region (exposed comm / per-bucket times; 0 = off)")
+    ap.add_argument("--profile", action="store_true",
+                    help="re-run this command under rocprofv3 --kernel-trace --stats (prints the command)")
+    ap.add_argument("--profile-dir", default="gpurun_out/prof")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0, help="wall-clock limit of a self-launched job")
+    return ap.parse_args(argv)
 
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws != a.gpus:
-        if a.gpus > 1 and ws == 1:
-            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
-    ctx = init_env(device=a.device, comm=a.comm)
-    dev = ctx.device
-    torch.manual_seed(1)
+
+def build(a, dev, rank, world, comm):
     train = synthetic_cifar(50000, 0)
-    sampler = ShardSampler(len(train), ctx.world, ctx.rank, shuffle=True, seed=0)
-    loader = DeviceLoader(train, a.batch, dev, sampler=sampler, train=True, seed=7919 + ctx.rank, drop_last=True)
+    sampler = ShardSampler(len(train), world, rank, shuffle=True, seed=0)
+    loader = DeviceLoader(train, a.batch, dev, sampler=sampler, train=True, seed=7919 + rank, drop_last=True)
     engine = VGGEngine(a.model, dev, max_batch=a.batch, impl=a.impl)
     engine.init_parameters(seed=1)
-    sync = make_sync(a.mode, engine, ctx.comm, bucket_mb=a.bucket_mb, overlap=not a.no_overlap)
+    sync = make_sync(a.mode, engine, comm, bucket_mb=a.bucket_mb, overlap=not a.no_overlap)
 
     def batches():
         ep = 0
@@ -78,10 +94,10 @@ def main():
             yield from loader  # drop_last: every step has the full per-GPU batch
             ep += 1
 
-    it = batches()
-    graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
-               if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
+    return engine, sync, batches()
 
+
+def make_step(engine, sync, it, graphed=None, probe=None):
     def step():
         x, t = next(it)
         if graphed is not None:
@@ -90,31 +106,103 @@ def main():
         sync.begin_step()
         engine.forward_backward(x, t, grad_ready=sync.grad_ready, pre_forward=sync.pre_forward,
                                 params_free=sync.params_free)
+        if probe is not None:
+            probe.mark("bwd_end")
         sync.update(sync.finish())
+        if probe is not None:
+            probe.mark("step_end")
         engine.finish_step()
 
-    for _ in range(a.warmup):
+    if probe is None:
+        return step
+
+    orig_finish = sync.finish
+
+    def finish():  # mark when the compute stream has caught up with the comm stream
+        s = orig_finish()
+        probe.mark("synced")
+        return s
+
+    sync.finish = finish
+    return step
+
+
+def solo_phase(a, dev, steps, warmup):
+    """1-GPU figure of the same step (rank 0, no communicator) in this run."""
+    engine, sync, it = build(a, dev, 0, 1, NullComm())
+    step = make_step(engine, sync, it)
+    for _ in range(warmup):
         step()
-
-    def barrier():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        ctx.barrier()
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-
-    barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         step()
-    barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    el = ctx.all_max(el)  # slowest rank
+    del engine, sync, it
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return a.batch * steps / el
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    gpus = a.gpus if a.gpus is not None else env_world
+    rc = benchlib.relaunch(os.path.abspath(__file__), argv, gpus, a.profile, a.profile_dir, a.launch_timeout)
+    if rc is not None:
+        return rc
+    if "WORLD_SIZE" in os.environ and a.gpus is not None and a.gpus != env_world:
+        raise SystemExit(f"--gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+    launcher = "spawn" if is_spawned_child() else ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or
+                                                   "WORLD_SIZE" in os.environ else "single")
+    ctx = init_env(device=a.device, comm=a.comm)
+    dev = ctx.device
+    torch.manual_seed(1)
+
+    solo_img_s = None
+    solo_steps = min(a.steps, 30) if a.solo_steps is None else a.solo_steps
+    if ctx.world > 1 and solo_steps > 0:
+        if ctx.rank == 0:
+            solo_img_s = solo_phase(a, dev, solo_steps, min(a.warmup, 5))
+        ctx.barrier()
+
+    engine, sync, it = build(a, dev, ctx.rank, ctx.world, ctx.comm)
+    graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
+               if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
+    el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev)
     loss = float(engine.loss.item())
     ms = el / a.steps * 1e3
     img_s = a.batch * ctx.world * a.steps / el
+
+    diag = None
+    if a.diag_steps > 0 and dev.type == "cuda":
+        probe = EventProbe(dev)
+        sync.probe = probe
+        step = make_step(engine, sync, it, probe=probe)
+        samples = []
+        for _ in range(a.diag_steps):
+            probe.reset()
+            probe.mark("start")
+            step()
+            samples.append(probe.times())
+        sync.probe = None
+        sync.__dict__.pop("finish", None)  # drop make_step's probe wrapper
+        diag = step_comm_report(samples, len(sync.buckets))
+        diag["exposed_comm_ms"] = ctx.all_max(diag["exposed_comm_ms"] or 0.0)
+    benchlib.device_barrier(ctx, dev)
+    pdiff = benchlib.replicas_max_diff(ctx.comm, engine.params.flat)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    cw = benchlib.comm_world(ctx.comm)
+
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(ctx.world)
+        per_gpu = img_s / ctx.world
         rec = {
             "metric": BASELINE_METRIC,
             "value": round(img_s, 1),
@@ -132,13 +220,23 @@ def main():
             "data": "synthetic (CIFAR-10-shaped uint8 on device, random-crop/flip/normalize each step)",
             "config": {"model": a.model, "global_batch": a.batch * ctx.world, "seq_len": None, "image_size": 32,
                        "parallelism": f"dp{ctx.world}", "sync_mode": a.mode, "comm": ctx.comm.name,
+                       "bucket_mb": [round(4 * b.numel / 2 ** 20, 3) for b in sync.buckets] if sync.active else None,
+                       "overlap": not a.no_overlap, "launcher": launcher,
                        "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
+            "per_gpu_img_s": round(per_gpu, 1),
+            "solo_img_s": round(solo_img_s, 1) if solo_img_s else None,
+            "scaling_efficiency": round(per_gpu / solo_img_s, 4) if solo_img_s else None,
+            "rccl_world": cw,
+            "replicas_identical": pdiff == 0.0,
+            "replica_param_max_diff": pdiff,
+            "comm_diag": diag,
             "vs_torch_eager_fp32": round(img_s / (TORCH_EAGER_IMG_S_PER_GPU * ctx.world), 3),
             "final_loss": round(loss, 4),
         }
         print(json.dumps(rec), flush=True)
     ctx.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

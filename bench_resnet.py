@@ -5,7 +5,7 @@ ImageNet-shaped data (224x224x3 NHWC, 1000 classes) resident on the device; rand
 Every timed step: forward, loss, backward with bucketed RCCL all-reduce issued from gradient
 hooks (parallel/ddp.py), fused SGD(0.1, 0.9, wd 1e-4).
 
-    python bench_resnet.py [--batch 128] [--steps 20] [--warmup 5] [--impl bf16|x3]
+    python bench_resnet.py [--gpus N] [--batch 128] [--steps 20] [--warmup 5] [--impl bf16|x3] [--profile]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench_resnet.py --gpus N
 """
@@ -15,7 +15,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 import torch
 import torch.nn.functional as F
@@ -25,11 +24,14 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_pytorch_amd.models.resnet import resnet50  # noqa: E402
 from distributed_pytorch_amd.parallel import init_env  # noqa: E402
 from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel, FlatSGD  # noqa: E402
+from distributed_pytorch_amd.utils import benchlib  # noqa: E402
 
 
-def main():
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1); without a "
+                    "launcher environment N>1 starts N local ranks (parallel/spawn.py)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="per-GPU batch")
@@ -39,7 +41,15 @@ def main():
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
     ap.add_argument("--autotune", action="store_true",
                     help="time every conv kernel config during warmup and save tuning/generic_mi355x.json")
-    a = ap.parse_args()
+    ap.add_argument("--profile", action="store_true", help="re-run under rocprofv3 --kernel-trace --stats")
+    ap.add_argument("--profile-dir", default="gpurun_out/prof_resnet")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0)
+    a = ap.parse_args(argv)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    rc = benchlib.relaunch(os.path.abspath(__file__), argv, a.gpus if a.gpus is not None else env_world, a.profile,
+                           a.profile_dir, a.launch_timeout)
+    if rc is not None:
+        return rc
     ctx = init_env(comm=a.comm)
     dev = ctx.device
     torch.manual_seed(1)
@@ -65,23 +75,14 @@ def main():
         Fn.set_autotune(False)
         if ctx.rank == 0:
             Fn.save_tuning_table()
-    for _ in range(a.warmup):
-        step()
+    last = {}
 
-    def barrier():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        ctx.barrier()
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
+    def timed_step():
+        last["loss"] = step()
 
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss = step()
-    barrier()
-    el = time.perf_counter() - t0
-    el = ctx.all_max(el)  # slowest rank
+    el = benchlib.timed_steps(timed_step, a.steps, a.warmup, ctx, dev)  # max over ranks
+    loss = last["loss"]
+    pdiff = benchlib.replicas_max_diff(ctx.comm, ddp.flat_params)
     img_s = a.batch * ctx.world * a.steps / el
     if ctx.rank == 0:
         print(json.dumps({
@@ -93,10 +94,12 @@ def main():
             "config": {"model": "resnet50", "global_batch": a.batch * ctx.world, "seq_len": None,
                        "image_size": a.image, "parallelism": f"dp{ctx.world}", "buckets": ddp.num_buckets(),
                        "comm": ctx.comm.name, "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
+            "rccl_world": benchlib.comm_world(ctx.comm), "replicas_identical": pdiff == 0.0,
             "final_loss": round(float(loss.item()), 4),
         }), flush=True)
     ctx.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

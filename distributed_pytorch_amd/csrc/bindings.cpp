@@ -10,7 +10,7 @@
 extern "C" {
 int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd, float gscale,
                  int first, unsigned short* planes, long ps, int np, hipStream_t s);
-int dpa_scale(float* x, long n, float sc, hipStream_t s);
+int dpa_spin(long long usec, int* done, hipStream_t s);
 int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
                    int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, int posmajor,
@@ -133,9 +133,12 @@ void sgd_flat(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double
       "sgd_flat");
 }
 
-void scale_(Tensor x, double s) {
-  need(x, "x");
-  chk(dpa_scale(fp(x), x.numel(), (float)s, cur_stream()), "scale_");
+// Diagnostics: occupy the current stream for ~usec microseconds (one wave, bounded loop) and then
+// write 1 to done[0].  Used to hold a collective behind a long kernel (watchdog timeout test).
+void spin(int64_t usec, Tensor done) {
+  need(done, "done", at::kInt);
+  TORCH_CHECK(usec >= 0 && usec <= 10000000, "spin: usec out of range");
+  chk(dpa_spin(usec, done.data_ptr<int>(), cur_stream()), "spin");
 }
 
 void mean_of_w(Tensor in, Tensor out, int64_t W) {
@@ -637,6 +640,7 @@ class PyRcclComm {
   int64_t stream_ptr() { return reinterpret_cast<int64_t>(stream_.stream()); }
   int64_t outstanding() { return (int64_t)comm_.outstanding(); }
   int64_t ops_issued() { return (int64_t)comm_.ops_issued(); }
+  int comm_count() { return comm_.comm_count(); }
   int rank() const { return comm_.rank(); }
   int world() const { return comm_.world(); }
 
@@ -652,7 +656,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_flat", &sgd_flat, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
         py::arg("wd"), py::arg("gscale"), py::arg("first"), py::arg("offset") = 0, py::arg("count") = -1,
         py::arg("planes") = py::none());
-  m.def("scale_", &scale_);
+  m.def("spin", &spin, py::arg("usec"), py::arg("done"));
   m.def("mean_of_w", &mean_of_w);
   m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("dgrad") = false, py::arg("reduce") = true,
@@ -741,6 +745,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("exit_on_error") = true, py::arg("debug_sync") = false)
       .def("outstanding", &PyRcclComm::outstanding)
       .def("ops_issued", &PyRcclComm::ops_issued)
+      .def("comm_count", &PyRcclComm::comm_count)
       .def("all_reduce", &PyRcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
       .def("broadcast", &PyRcclComm::broadcast)
       .def("gather", &PyRcclComm::gather)

@@ -52,13 +52,6 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, co
   }
 }
 
-// Elementwise y = x * s over a flat fp32 range (K12: grad /= W for the all-reduce mode when the
-// scale is not fused into the optimizer).
-__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, long n, float s) {
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
-}
-
 // K11 — mean over W stacked copies: out[i] = (sum_w in[w*n + i]) / W   (gather mode, rank 0).
 __global__ __launch_bounds__(256) void mean_of_w_kernel(const float* __restrict__ in, float* __restrict__ out, long n,
                                                         int W) {
@@ -90,11 +83,6 @@ extern "C" int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float 
     sgd_flat_kernel<1><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, planes, ps);
   else
     sgd_flat_kernel<0><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, nullptr, 0);
-  return (int)hipGetLastError();
-}
-
-extern "C" int dpa_scale(float* x, long n, float sc, hipStream_t s) {
-  scale_kernel<<<grid_for(n, 256), 256, 0, s>>>(x, n, sc);
   return (int)hipGetLastError();
 }
 

@@ -7,6 +7,8 @@
 
 namespace dpa {
 
+using Lock = std::unique_lock<std::timed_mutex>;
+
 static void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
 }
@@ -59,11 +61,11 @@ RcclComm::~RcclComm() {
   stop_ = true;
   cv_.notify_all();
   if (watchdog_.joinable()) watchdog_.join();
-  if (comm_) {
-    if (aborted_)
-      ncclCommAbort(comm_);
-    else
-      ncclCommDestroy(comm_);
+  {
+    Lock g(comm_mu_);
+    // a healthy communicator is destroyed in order; one whose peer failed is aborted (destroy
+    // could wait forever on collectives that will never complete)
+    release_locked(state_.load() != kHealthy);
   }
   for (auto& op : ops_) hipEventDestroy(op.ev);
   for (auto ev : free_events_) hipEventDestroy(ev);
@@ -71,11 +73,30 @@ RcclComm::~RcclComm() {
   hipEventDestroy(ev_out_);
 }
 
-void RcclComm::begin_op() {
-  if (aborted_) {
+void RcclComm::release_locked(bool abort) {
+  if (comm_) {
+    if (abort)
+      ncclCommAbort(comm_);
+    else
+      ncclCommDestroy(comm_);
+    comm_ = nullptr;
+  }
+  state_ = kAborted;
+}
+
+void RcclComm::require_healthy_locked() {
+  if (state_.load() != kHealthy || !comm_) {
     std::lock_guard<std::mutex> g(mu_);
     throw std::runtime_error("RCCL communicator is aborted: " + (error_.empty() ? std::string("abort()") : error_));
   }
+}
+
+int RcclComm::comm_count() {
+  Lock g(comm_mu_);
+  if (!comm_ || state_.load() != kHealthy) return -1;
+  int n = -1;
+  if (ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+  return n;
 }
 
 void RcclComm::end_op(const char* what) {
@@ -112,28 +133,38 @@ void RcclComm::fail(const std::string& msg) {
     std::lock_guard<std::mutex> g(mu_);
     if (error_.empty()) error_ = msg;
   }
+  int expect = kHealthy;
+  state_.compare_exchange_strong(expect, kFailed);  // from now on every issue throws
   std::fprintf(stderr, "[dpa rank %d] RCCL watchdog: %s\n", rank_, msg.c_str());
   std::fflush(stderr);
-  if (!aborted_.exchange(true) && comm_) ncclCommAbort(comm_);
-  comm_ = nullptr;
   if (wd_.exit_on_error) {
+    // the process is about to end: the driver reclaims the context (and with it the RCCL kernels
+    // spinning on the dead peer); no abort call that could itself block on the fabric
     std::fprintf(stderr, "[dpa rank %d] terminating the process (exit 70) so the launcher can tear the job down\n",
                  rank_);
     std::fflush(stderr);
     std::_Exit(70);
+  }
+  // Abort under comm_mu_: an issue that is in flight finishes first (enqueue calls return without
+  // waiting on peers), and no issuer can ever see the handle after it is released.
+  while (!stop_) {
+    Lock g(comm_mu_, std::defer_lock);
+    if (g.try_lock_for(std::chrono::milliseconds(500))) {
+      release_locked(true);
+      return;
+    }
   }
 }
 
 void RcclComm::watchdog_loop() {
   hipSetDevice(device_);
   const auto poll = std::chrono::duration<double>(wd_.poll_s);
-  std::mutex m;
   while (!stop_) {
     {
-      std::unique_lock<std::mutex> lk(m);
+      std::unique_lock<std::mutex> lk(wake_mu_);
       cv_.wait_for(lk, poll, [this] { return stop_.load(); });
     }
-    if (stop_ || aborted_) break;
+    if (stop_ || state_.load() != kHealthy) break;
     // retire completed ops in issue order; time out the oldest pending one
     std::string timeout_msg;
     {
@@ -161,12 +192,18 @@ void RcclComm::watchdog_loop() {
       fail(timeout_msg);
       break;
     }
-    if (comm_) {
-      ncclResult_t e = ncclSuccess;
-      if (ncclCommGetAsyncError(comm_, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress) {
-        fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(e));
-        break;
+    std::string async_msg;
+    {
+      Lock g(comm_mu_, std::try_to_lock);  // the issuer holds it only for an enqueue: skip this poll
+      if (g.owns_lock() && comm_) {
+        ncclResult_t e = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress)
+          async_msg = std::string("asynchronous RCCL error: ") + ncclGetErrorString(e);
       }
+    }
+    if (!async_msg.empty()) {
+      fail(async_msg);
+      break;
     }
   }
 }
@@ -178,16 +215,22 @@ void RcclComm::fence_after(hipStream_t after) {
 }
 
 void RcclComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
+  }
   end_op("all_reduce");
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  check(ncclBroadcast(buf, buf, count, dt, root, comm_, stream_), "ncclBroadcast");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    check(ncclBroadcast(buf, buf, count, dt, root, comm_, stream_), "ncclBroadcast");
+  }
   end_op("broadcast");
 }
 
@@ -209,52 +252,67 @@ static size_t dt_size(ncclDataType_t dt) {
 }
 
 void RcclComm::gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  const size_t bytes = count * dt_size(dt);
-  check(ncclGroupStart(), "ncclGroupStart");
-  if (rank_ == root) {
-    for (int p = 0; p < world_; ++p) {
-      char* dst = static_cast<char*>(recv) + (size_t)p * bytes;
-      if (p == root) {
-        if (dst != send) hip_check(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, stream_), "memcpy");
-      } else {
-        check(ncclRecv(dst, count, dt, p, comm_, stream_), "ncclRecv");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    const size_t bytes = count * dt_size(dt);
+    check(ncclGroupStart(), "ncclGroupStart");
+    if (rank_ == root) {
+      for (int p = 0; p < world_; ++p) {
+        char* dst = static_cast<char*>(recv) + (size_t)p * bytes;
+        if (p == root) {
+          if (dst != send) hip_check(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, stream_), "memcpy");
+        } else {
+          check(ncclRecv(dst, count, dt, p, comm_, stream_), "ncclRecv");
+        }
       }
+    } else {
+      check(ncclSend(send, count, dt, root, comm_, stream_), "ncclSend");
     }
-  } else {
-    check(ncclSend(send, count, dt, root, comm_, stream_), "ncclSend");
+    check(ncclGroupEnd(), "ncclGroupEnd");
   }
-  check(ncclGroupEnd(), "ncclGroupEnd");
   end_op("gather");
 }
 
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t recvcount, ncclDataType_t dt, ncclRedOp_t op,
                               hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  check(ncclReduceScatter(send, recv, recvcount, dt, op, comm_, stream_), "ncclReduceScatter");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    check(ncclReduceScatter(send, recv, recvcount, dt, op, comm_, stream_), "ncclReduceScatter");
+  }
   end_op("reduce_scatter");
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t sendcount, ncclDataType_t dt, hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  check(ncclAllGather(send, recv, sendcount, dt, comm_, stream_), "ncclAllGather");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    check(ncclAllGather(send, recv, sendcount, dt, comm_, stream_), "ncclAllGather");
+  }
   end_op("all_gather");
 }
 
 void RcclComm::send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  check(ncclSend(buf, count, dt, peer, comm_, stream_), "ncclSend");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    check(ncclSend(buf, count, dt, peer, comm_, stream_), "ncclSend");
+  }
   end_op("send");
 }
 
 void RcclComm::recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t after) {
-  begin_op();
-  fence_after(after);
-  check(ncclRecv(buf, count, dt, peer, comm_, stream_), "ncclRecv");
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    fence_after(after);
+    check(ncclRecv(buf, count, dt, peer, comm_, stream_), "ncclRecv");
+  }
   end_op("recv");
 }
 
@@ -271,7 +329,8 @@ std::string RcclComm::async_error() {
     std::lock_guard<std::mutex> g(mu_);
     if (!error_.empty()) return error_;
   }
-  if (aborted_) return "communicator aborted";
+  Lock g(comm_mu_);
+  if (state_.load() != kHealthy) return "communicator aborted";
   if (!comm_) return "no communicator";
   ncclResult_t e = ncclSuccess;
   ncclResult_t r = ncclCommGetAsyncError(comm_, &e);
@@ -284,10 +343,12 @@ void RcclComm::abort() {
   stop_ = true;
   cv_.notify_all();
   if (watchdog_.joinable() && watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();
-  if (comm_ && !aborted_.exchange(true)) {
-    ncclCommAbort(comm_);
-    comm_ = nullptr;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (error_.empty()) error_ = "abort()";
   }
+  Lock g(comm_mu_);
+  release_locked(true);
 }
 
 }  // namespace dpa

@@ -34,6 +34,12 @@ struct WatchdogConfig {
   bool debug_sync = false;
 };
 
+// Thread-safety contract.  Two threads touch the communicator: the issuing (Python) thread and the
+// watchdog.  `comm_` is only read or changed with `comm_mu_` held: every enqueue holds it for the
+// duration of the RCCL call(s), and the communicator is aborted / destroyed (and `comm_` cleared)
+// under it, so no thread can use a handle another thread is tearing down.  `state_` moves
+// kHealthy -> kFailed (watchdog recorded an error) -> kAborted (communicator released) and never
+// back; an op issued in any state but kHealthy throws.
 class RcclComm {
  public:
   // uid: NCCL_UNIQUE_ID_BYTES bytes created by rank 0 (unique_id()) and shared out of band.
@@ -47,6 +53,8 @@ class RcclComm {
   int rank() const { return rank_; }
   int world() const { return world_; }
   hipStream_t stream() const { return stream_; }
+  // ranks RCCL itself reports for this communicator (ncclCommCount); -1 once aborted
+  int comm_count();
 
   // All ops: comm stream waits for everything already queued on `after` (the compute stream),
   // then runs the collective.  Returns immediately.
@@ -72,18 +80,22 @@ class RcclComm {
   uint64_t ops_issued() const { return ops_issued_.load(); }
 
  private:
+  enum State : int { kHealthy = 0, kFailed = 1, kAborted = 2 };
   void fence_after(hipStream_t after);
   void check(ncclResult_t r, const char* what);
-  void begin_op();                // throws if the communicator is dead
-  void end_op(const char* what);  // track completion (or sync in debug mode)
+  // throws if the communicator is not healthy; caller holds comm_mu_
+  void require_healthy_locked();
+  void end_op(const char* what);  // track completion (or sync in debug mode); caller does NOT hold comm_mu_
   void watchdog_loop();
-  void fail(const std::string& msg);
+  void fail(const std::string& msg);  // watchdog thread only
+  void release_locked(bool abort);    // caller holds comm_mu_
 
   int rank_, world_, device_;
-  ncclComm_t comm_ = nullptr;
+  ncclComm_t comm_ = nullptr;  // guarded by comm_mu_
+  std::timed_mutex comm_mu_;
   hipStream_t stream_;
   hipEvent_t ev_in_, ev_out_;
-  std::atomic<bool> aborted_{false};
+  std::atomic<int> state_{kHealthy};
   WatchdogConfig wd_;
   struct Op {
     hipEvent_t ev;
@@ -96,6 +108,7 @@ class RcclComm {
   std::string error_;
   std::atomic<uint64_t> ops_issued_{0};
   std::atomic<bool> stop_{false};
+  std::mutex wake_mu_;
   std::condition_variable cv_;
   std::thread watchdog_;
 };

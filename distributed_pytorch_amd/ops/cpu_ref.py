@@ -50,10 +50,6 @@ def split_bf16(x, np_):
     return torch.stack(out)
 
 
-def scale_(x, s):
-    x.mul_(s)
-
-
 def mean_of_w(inp, out, W):
     out.copy_(inp.view(W, -1).mean(0))
 

@@ -265,3 +265,7 @@ class RcclComm(Comm):
 
     def ops_issued(self) -> int:
         return self._c.ops_issued()
+
+    def comm_count(self) -> int:
+        """Ranks in the communicator as RCCL reports them (ncclCommCount); -1 once aborted."""
+        return self._c.comm_count()

@@ -5,13 +5,17 @@
 * torchrun style (main_ddp.py:93-104, start_ddp.sh): MASTER_ADDR/MASTER_PORT/WORLD_SIZE/RANK/
   LOCAL_RANK from the environment (``env://``).
 
-One process per GPU: LOCAL_RANK (or rank mod #GPUs) selects the device.  Rendezvous:
-* ``DPA_RENDEZVOUS=torch`` (default): a torch.distributed gloo group carries the rendezvous store
-  and CPU-side barriers; the native RCCL communicator is bootstrapped from that store;
-* ``DPA_RENDEZVOUS=native``: no torch.distributed at all — the native C++ TCP store
-  (parallel/store.py) on MASTER_ADDR:DPA_STORE_PORT bootstraps RCCL and provides barriers.
+One process per GPU: LOCAL_RANK (or rank mod #GPUs) selects the device.  Rendezvous
+(``DPA_RENDEZVOUS``):
+* ``native`` (default on GPU): no torch.distributed at all — the native C++ TCP store
+  (parallel/store.py, csrc/runtime/tcp_store.cpp) on MASTER_ADDR:DPA_STORE_PORT bootstraps RCCL
+  (ncclUniqueId exchange) and provides the CPU-side barriers;
+* ``torch`` (default on CPU, and for ``--comm torch``): a torch.distributed gloo group carries the
+  rendezvous store and barriers — on CPU it is also the communicator (the multi-process test oracle).
 On GPU the gradient collectives go through the native RCCL communicator (``comm="rccl"``), or
 through torch's own nccl group (``comm="torch"``, torch rendezvous only) for A/B comparison.
+There is no silent fallback: if the native communicator cannot be created the job fails
+(``DPA_COMM_FALLBACK=1`` opts into torch's nccl group instead, which the bench reports).
 """
 from __future__ import annotations
 
@@ -83,10 +87,12 @@ def pick_device(local_rank: int, want: str = "auto") -> torch.device:
     return d
 
 
-def _rendezvous() -> str:
-    r = os.environ.get("DPA_RENDEZVOUS", "torch")
-    if r not in ("torch", "native"):
-        raise ValueError("DPA_RENDEZVOUS must be 'torch' or 'native'")
+def _rendezvous(device: torch.device, comm: str = "rccl") -> str:
+    r = os.environ.get("DPA_RENDEZVOUS", "auto")
+    if r not in ("auto", "torch", "native"):
+        raise ValueError("DPA_RENDEZVOUS must be 'auto', 'torch' or 'native'")
+    if r == "auto":
+        return "native" if device.type == "cuda" and comm == "rccl" else "torch"
     return r
 
 
@@ -118,7 +124,7 @@ def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=Non
     try:
         comm = RcclComm(rank, world, device, store=store)
     except Exception as e:  # noqa: BLE001 — keep the job alive on torch's own RCCL group
-        if not torch_store or os.environ.get("DPA_COMM_FALLBACK", "1") != "1":
+        if not torch_store or os.environ.get("DPA_COMM_FALLBACK", "0") != "1":
             raise
         print(f"[rank {rank}] native RCCL communicator failed ({e}); falling back to torch's nccl (RCCL) group",
               flush=True)
@@ -140,7 +146,7 @@ def init_cli(master_ip: str, num_nodes: int, rank: int, port: int = DEFAULT_PORT
     dev = pick_device(local_rank, device)
     init, store = False, None
     if num_nodes > 1:
-        if _rendezvous() == "native":
+        if _rendezvous(dev, comm) == "native":
             store = _native_store(master_ip, port, rank, num_nodes)
         else:
             dist.init_process_group(backend="gloo", init_method=f"tcp://{master_ip}:{port}", world_size=num_nodes,
@@ -161,7 +167,7 @@ def init_env(device: str = "auto", comm: str = "rccl") -> DistContext:
     dev = pick_device(local_rank, device)
     init, store = False, None
     if world > 1:
-        if _rendezvous() == "native":
+        if _rendezvous(dev, comm) == "native":
             port = int(os.environ.get("DPA_STORE_PORT", int(os.environ["MASTER_PORT"]) + 1))
             store = _native_store(os.environ["MASTER_ADDR"], port, rank, world)
         else:

@@ -137,6 +137,10 @@ class GradSync:
             for b in self.buckets:
                 b.free_ev = DevEvent()
         self.issued_bytes = 0
+        # optional utils.profiling.EventProbe: marks b{i}_start / b{i}_end around each bucket's
+        # collective on the comm stream (bench diagnostic phase only)
+        self.probe = None
+        self._index = {id(b): i for i, b in enumerate(self.buckets)}
         if broadcast_init and self.active:
             self.broadcast_state()
 
@@ -230,7 +234,11 @@ class GradSync:
         b.issued = True
         self.issued_bytes += 4 * b.numel
         with self.comm.region():
+            if self.probe is not None:
+                self.probe.mark(f"b{self._index[id(b)]}_start")
             self.reduce_bucket(b)
+            if self.probe is not None:
+                self.probe.mark(f"b{self._index[id(b)]}_end")
             if self._step_ready(b):  # parameters already free: update in the same region (one join)
                 self._step_here(b)
 

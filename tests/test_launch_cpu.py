@@ -1,0 +1,100 @@
+"""The single-node N-rank launcher (parallel/spawn.py) and the self-launching bench: what the
+round-end driver runs as ``python bench.py --gpus N`` must start N ranks, report one JSON line,
+and turn a failed or hung rank into a non-zero exit instead of a hang."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from distributed_pytorch_amd.parallel import spawn
+from distributed_pytorch_amd.utils.benchlib import strip_flag
+from distributed_pytorch_amd.utils.profiling import rocprof_command
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _script(tmp_path, body):
+    p = tmp_path / "child.py"
+    p.write_text(textwrap.dedent(body))
+    return str(p)
+
+
+def test_launch_sets_rank_env(tmp_path):
+    out = tmp_path / "out"
+    out.mkdir()
+    s = _script(tmp_path, f"""
+        import os, json
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                "DPA_STORE_PORT", "{spawn.SPAWNED_ENV}")
+        with open(os.path.join({str(out)!r}, os.environ["RANK"] + ".json"), "w") as f:
+            json.dump({{k: os.environ[k] for k in keys}}, f)
+        """)
+    assert spawn.launch(s, [], 3, timeout_s=60) == 0
+    envs = [json.loads((out / f"{r}.json").read_text()) for r in range(3)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"]
+    assert all(e["WORLD_SIZE"] == "3" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
+    assert len({e["MASTER_PORT"] for e in envs}) == 1 and envs[0]["MASTER_PORT"] != envs[0]["DPA_STORE_PORT"]
+    assert all(e[spawn.SPAWNED_ENV] == "1" for e in envs)
+
+
+def test_launch_failing_rank_stops_the_others(tmp_path):
+    s = _script(tmp_path, """
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(120)
+        """)
+    t0 = time.monotonic()
+    rc = spawn.launch(s, [], 3, timeout_s=100, grace_s=5)
+    assert rc == 3
+    assert time.monotonic() - t0 < 30
+
+
+def test_launch_timeout(tmp_path):
+    s = _script(tmp_path, "import time\ntime.sleep(120)\n")
+    t0 = time.monotonic()
+    assert spawn.launch(s, [], 2, timeout_s=2, grace_s=2) == 124
+    assert time.monotonic() - t0 < 30
+
+
+def test_needs_spawn(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv(spawn.SPAWNED_ENV, raising=False)
+    assert spawn.needs_spawn(2) and not spawn.needs_spawn(1)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert not spawn.needs_spawn(2)  # torchrun already started the ranks
+
+
+def test_profile_command_puts_python_right_after_dashes():
+    cmd = rocprof_command(["bench.py", "--steps", "5"], outdir="gpurun_out/p")
+    i = cmd.index("--")
+    assert cmd[0] == "rocprofv3" and "--kernel-trace" in cmd and "--stats" in cmd
+    assert cmd[i + 1] == sys.executable and cmd[i + 2:] == ["bench.py", "--steps", "5"]
+    assert strip_flag(["--profile", "--steps", "5"], "--profile") == ["--steps", "5"]
+
+
+@pytest.mark.slow
+def test_bench_self_launch_two_ranks_cpu():
+    """``bench.py --gpus 2`` with no launcher environment: 2 gloo ranks on CPU through the same
+    spawn path the driver's 8-GPU run takes; one JSON line with the scaling fields."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", spawn.SPAWNED_ENV)}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--batch", "4", "--steps", "2", "--warmup", "1", "--solo-steps", "1"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "per_gpu_img_s", "scaling_efficiency", "rccl_world",
+              "replicas_identical"):
+        assert k in rec, k
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["parallelism"] == "dp2" and rec["config"]["launcher"] == "spawn"
+    assert rec["config"]["global_batch"] == 8
+    assert rec["replicas_identical"] is True and rec["rccl_world"] == 2
+    assert rec["scaling_efficiency"] is not None and rec["value"] > 0

@@ -1,0 +1,236 @@
+"""The benchmark's exact kernel configurations, checked against fp64 autograd.
+
+bench.py trains VGG-11 at batch 256 with the measured per-layer conv configurations of
+tuning/mi355x.json (halo tiles, split-K counts up to 512, ...).  Smaller-batch parity tests run the
+heuristic configurations instead, so here ONE full training step at batch 256 — forward, softmax-CE,
+backward, fused SGD — is compared tensor by tensor with ``VGG11().double()`` autograd + torch SGD on
+the same weights and data (reference: main.py:32-36, model.py:11-46):
+
+* every conv call of the step (8 fprop, 7 dgrad, 8 wgrad) at its tuned configuration, fed with
+  random operands, vs fp64 conv: rel ≤ 1e-5 (a wrong tile, split or reduction shows up as O(1));
+* the loss, all 34 parameter gradients and the 34 parameter updates of the whole step.  A
+  random-init VGG-11 with BN at batch 256 is ill-conditioned (stock torch fp32 on CPU is off from
+  fp64 by up to ~3e-2 on single gradient tensors, measured), so the yardstick is torch's own fp32
+  error on the same step: x3 and the fp32 MFMA path must stay within a small factor of it on
+  every tensor, and on the median tensor be no worse than it;
+* the layer-0 weight gradient, whose reduction runs over all 256·32·32 = 262,144 output pixels
+  (the longest sum in the step), at the tuned x3 config vs fp32 MFMA vs fp64.
+"""
+import json
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+N = 256
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def reference():
+    from distributed_pytorch_amd.models import VGG11
+
+    torch.manual_seed(1)
+    m = VGG11().double()
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(256)
+    x = torch.randn(N, 3, 32, 32, generator=g, dtype=torch.float64)
+    t = torch.randint(0, 10, (N,), generator=g)
+    loss = F.cross_entropy(m(x), t)
+    loss.backward()
+    grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt.step()
+    new = {n: p.detach().clone() for n, p in m.named_parameters()}
+    return dict(sd0=sd0, x=x, t=t, loss=float(loss), grads=grads, new=new)
+
+
+def _torch_fp32_errors(ref):
+    from distributed_pytorch_amd.models import VGG11
+
+    m = VGG11()
+    m.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref["sd0"].items()})
+    F.cross_entropy(m(ref["x"].float()), ref["t"]).backward()
+    return {n: (_rel(p.grad, ref["grads"][n]) if ref["grads"][n].abs().max() >= 1e-7 else None)
+            for n, p in m.named_parameters()}
+
+
+def _engine_step(ref, impl):
+    from distributed_pytorch_amd.engine import VGGEngine, conv_key, tuning_table
+
+    e = VGGEngine("VGG11", "cuda", max_batch=N, impl=impl)
+    # the tuned table must cover every conv call of the step at this batch (no heuristic fallback)
+    tab = tuning_table()
+    for i, l in enumerate(e.spec.convs):
+        for kind in ("fprop", "dgrad", "wgrad"):
+            if kind == "dgrad" and i == 0:
+                continue
+            k = conv_key(e._layer_impl(i), kind, N, l.hw, l.cin_pad, l.cout)
+            assert k in tab, f"no tuned entry for {k}"
+    e.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref["sd0"].items()})
+    old = {n: e._to_torch_layout(n, e.params[n]).cpu().double() for n in ref["grads"]}
+    x4 = torch.zeros(N, 32, 32, 4)
+    x4[..., :3] = ref["x"].float().permute(0, 2, 3, 1)
+    loss = float(e.forward_backward(x4.cuda(), ref["t"].cuda()).item())
+    grads = {n: e._to_torch_layout(n, e.grads[n]).cpu() for n in ref["grads"]}
+    e.sgd_step()
+    e.finish_step()
+    torch.cuda.synchronize()
+    new = {n: e._to_torch_layout(n, e.params[n]).cpu().double() for n in ref["grads"]}
+    return loss, grads, old, new
+
+
+@pytest.fixture(scope="module")
+def errors(reference):
+    out = {}
+    for impl in ("fp32", "x3"):
+        loss, grads, old, new = _engine_step(reference, impl)
+        ge, ue = {}, {}
+        for n, gref in reference["grads"].items():
+            if gref.abs().max() < 1e-7:  # conv biases: analytically zero gradient (BN follows)
+                ge[n] = None
+                assert grads[n].abs().max().item() < 1e-5, (impl, n)
+            else:
+                ge[n] = _rel(grads[n], gref)
+            # update error, absolute, and what fp32 arithmetic allows for it: the gradient's error
+            # times lr, plus one rounding of the parameter itself (p - lr*buf is formed in fp32)
+            dref = reference["new"][n] - reference["sd0"][n]
+            err = ((new[n] - old[n]) - dref).abs().max().item()
+            gabs = 0.0 if ge[n] is None else ge[n] * gref.abs().max().item()
+            allow = 0.1 * max(gabs, 1e-6) + 2.0 ** -23 * reference["new"][n].abs().max().item()
+            ue[n] = [err, allow]
+        out[impl] = dict(loss=abs(loss - reference["loss"]) / abs(reference["loss"]), grads=ge, updates=ue)
+    out["torch_fp32"] = dict(grads=_torch_fp32_errors(reference))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/parity256_errors.json", "w") as f:
+        json.dump(out, f, indent=1)
+    return out
+
+
+@pytest.mark.parametrize("impl", ["fp32", "x3"])
+def test_loss_matches_fp64(errors, impl):
+    assert errors[impl]["loss"] < 1e-5, errors[impl]["loss"]
+
+
+@pytest.mark.parametrize("impl", ["fp32", "x3"])
+def test_all_gradients_fp32_grade(errors, impl):
+    ref = errors["torch_fp32"]["grads"]
+    ratios = []
+    for n, e in errors[impl]["grads"].items():
+        if e is None:
+            continue
+        assert e <= 16.0 * ref[n] + 1e-5, (n, e, ref[n])
+        ratios.append(e / max(ref[n], 1e-12))
+    ratios.sort()
+    assert ratios[len(ratios) // 2] <= 1.5, ratios
+
+
+@pytest.mark.parametrize("impl", ["fp32", "x3"])
+def test_all_updates_match_fp64(errors, impl):
+    # an update is -lr * (g + wd * p) on the first step (conv biases: g analytically 0)
+    for n, (err, allow) in errors[impl]["updates"].items():
+        assert err <= 2.0 * allow, (n, err, allow)
+
+
+CALLS = [(i, k) for i in range(8) for k in ("fprop", "dgrad", "wgrad") if not (i == 0 and k == "dgrad")]
+
+
+@pytest.fixture(scope="module")
+def x3_engine():
+    from distributed_pytorch_amd.engine import VGGEngine
+
+    e = VGGEngine("VGG11", "cuda", max_batch=N, impl="x3")
+    e.init_parameters(seed=1)
+    return e
+
+
+@pytest.mark.parametrize("layer,kind", CALLS)
+def test_conv_call_at_bench_config(x3_engine, layer, kind):
+    """One conv call of the step exactly as the engine issues it (tuned tile/splits, its own
+    workspaces and plane buffers) on random operands vs fp64."""
+    from distributed_pytorch_amd import _ext
+
+    C = _ext.require()
+    e = x3_engine
+    l = e.spec.convs[layer]
+    g = torch.Generator().manual_seed(100 * layer + len(kind))
+    cin = l.cin
+    act = torch.randn(N, l.hw, l.hw, cin, generator=g)
+    w = e._to_torch_layout(f"{l.conv_key}.weight", e.params[f"{l.conv_key}.weight"]).cpu().double()  # OIHW
+    if layer == 0:
+        x4 = torch.zeros(N, 32, 32, 4)
+        x4[..., :3] = act
+        C.pad_split8(x4.cuda(), e.x0p)
+    else:
+        C.split_planes(act.cuda().contiguous().view(-1), e.a3[layer - 1].view(3, -1))
+    xd = act.permute(0, 3, 1, 2).double()
+    torch.cuda.synchronize()
+    if kind == "fprop":
+        e._conv_fwd(layer, None, N, reduce=True)
+        out = e.z[layer].cpu().permute(0, 3, 1, 2).double()
+        ref = F.conv2d(xd, w, padding=1)
+    else:
+        dz = torch.randn(N, l.hw, l.hw, l.cout, generator=g)
+        C.split_planes(dz.cuda().view(-1), e.dz3[layer].view(3, -1))
+        dzd = dz.permute(0, 3, 1, 2).double()
+        if kind == "dgrad":
+            s = e._conv_dgrad(layer, N)
+            shp = e.g[layer - 1].shape
+            if s > 1:
+                out = e.slab[: s * e.g[layer - 1].numel()].view(s, *shp).double().sum(0).cpu()
+            else:
+                out = e.g[layer - 1].cpu().double()
+            out = out.permute(0, 3, 1, 2)
+            ref = torch.nn.grad.conv2d_input(xd.shape, w, dzd, padding=1)
+        else:
+            e._conv_wgrad(layer, None, N)
+            out = e._to_torch_layout(f"{l.conv_key}.weight", e.grads[f"{l.conv_key}.weight"]).cpu().double()
+            ref = torch.nn.grad.conv2d_weight(xd, w.shape, dzd, padding=1)
+    torch.cuda.synchronize()
+    err = _rel(out, ref)
+    assert err < 1e-5, (layer, kind, e.conv_config(layer, kind, N), err)
+
+
+def test_layer0_wgrad_full_reduction_accuracy():
+    """wgrad of layer 0 at the bench's tuned x3 config (262,144-long reduction) vs fp32 MFMA vs fp64."""
+    from distributed_pytorch_amd import _ext
+    from distributed_pytorch_amd.engine import VGGEngine
+
+    C = _ext.require()
+    e = VGGEngine("VGG11", "cuda", max_batch=N, impl="x3")
+    tile, splits, pm = e.conv_config(0, "wgrad", N)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, 3, 32, 32, generator=g)
+    dz = torch.randn(N, 64, 32, 32, generator=g) * 1e-3
+    ref = torch.nn.grad.conv2d_weight(x.double(), (64, 3, 3, 3), dz.double(), padding=1)  # [64,3,3,3]
+    # x3 path: input padded to 8 channels and split into planes exactly as the engine does it
+    x4 = torch.zeros(N, 32, 32, 4)
+    x4[..., :3] = x.permute(0, 2, 3, 1)
+    x4 = x4.cuda()
+    xp = torch.zeros(3, N, 32, 32, 8, dtype=torch.bfloat16, device="cuda")
+    C.pad_split8(x4, xp)
+    dzd = dz.permute(0, 2, 3, 1).contiguous().cuda()
+    dzp = torch.zeros(3, N, 32, 32, 64, dtype=torch.bfloat16, device="cuda")
+    C.split_planes(dzd.view(-1), dzp.view(3, -1))
+    dw3 = torch.zeros(64, 3, 3, 8, device="cuda")
+    slab = torch.empty(max(1, splits) * dw3.numel(), device="cuda") if splits > 1 else None
+    C.conv_x3_wgrad(xp, dzp, dw3, slab, 1, 1, splits, tile, pm)
+    # exact fp32 MFMA path (4-channel padded input, as the fp32 engine runs layer 0)
+    dw32 = torch.zeros(64, 3, 3, 4, device="cuda")
+    s32 = 64
+    slab32 = torch.empty(s32 * dw32.numel(), device="cuda")
+    C.conv_wgrad(x4, dzd, dw32, slab32, 1, 1, s32, 0, False)
+    torch.cuda.synchronize()
+    r = ref.permute(0, 2, 3, 1)
+    e3 = ((dw3[..., :3].double().cpu() - r).abs().max() / r.abs().max()).item()
+    e32 = ((dw32[..., :3].double().cpu() - r).abs().max() / r.abs().max()).item()
+    assert splits > 1  # the tuned plan really splits the reduction
+    assert e3 < 1e-5, e3
+    assert e3 <= 4.0 * e32 + 1e-7, (e3, e32)
