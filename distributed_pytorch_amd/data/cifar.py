@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import math
 import os
+import pickle
 from typing import Iterator, List, Optional, Tuple
 
 import numpy as np
@@ -70,14 +71,37 @@ def _read_bin_batches(files: List[str]) -> ImageSet:
     return ImageSet(imgs, labels, "cifar10")
 
 
-def _read_py_batches(files: List[str]) -> ImageSet:
-    # The user's own torchvision-format CIFAR-10 download (pickled dicts, as torchvision reads it).
-    import pickle
+class _CifarUnpickler(pickle.Unpickler):
+    """The python release of CIFAR-10 is pickled dicts of numpy arrays, lists and bytes.  A plain
+    ``pickle.load`` would run whatever callable a tampered file names, so only the numpy array
+    reconstruction hooks are admitted; any other global in the stream is refused."""
 
+    _ALLOWED = {
+        ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+        ("numpy", "ndarray"), ("numpy", "dtype"),
+        ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+    }
+
+    def find_class(self, module, name):
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a CIFAR-10 batch file")
+
+
+def safe_load_batch(path: str) -> dict:
+    with open(path, "rb") as fh:
+        d = _CifarUnpickler(fh, encoding="bytes").load()
+    if not isinstance(d, dict):
+        raise pickle.UnpicklingError(f"{path}: expected a dict, got {type(d).__name__}")
+    return d
+
+
+def _read_py_batches(files: List[str]) -> ImageSet:
+    # The user's own torchvision-format CIFAR-10 download (pickled dicts, as torchvision reads it),
+    # read with a restricted unpickler.
     xs, ys = [], []
     for f in files:
-        with open(f, "rb") as fh:
-            d = pickle.load(fh, encoding="bytes")
+        d = safe_load_batch(f)
         xs.append(np.asarray(d[b"data"], dtype=np.uint8))
         ys += list(d[b"labels"])
     x = np.concatenate(xs, 0).reshape(-1, 3, 32, 32).transpose(0, 2, 3, 1).copy()

@@ -79,13 +79,15 @@ def weight_planes(w: torch.Tensor, np_: int) -> torch.Tensor:
     return split_planes(w, np_)
 
 
-def grad_slot(p: torch.Tensor, uses: int) -> Optional[torch.Tensor]:
+def grad_slot(p: torch.Tensor) -> Optional[torch.Tensor]:
     """Where a parameter gradient may be written directly: the optimizer arena view
-    (``p._dpa_grad_slot()``), when the parameter has no gradient yet this step and was used once
-    in this forward.  The view is handed back to autograd, whose AccumulateGrad adopts it as
-    ``p.grad`` instead of running a copy / add kernel per parameter."""
+    (``p._dpa_grad_slot()``), when the parameter has no gradient yet this step and was used exactly
+    once in this forward (``p._dpa_uses`` holds the forward's TOTAL use count by the time backward
+    runs).  The view is handed back to autograd, whose AccumulateGrad adopts it as ``p.grad``
+    instead of running a copy / add kernel per parameter.  A parameter used more than once gets a
+    fresh tensor per use; autograd sums them and the DDP hook moves the sum into the arena."""
     slot = getattr(p, "_dpa_grad_slot", None)
-    if slot is None or p.grad is not None or uses != 1:
+    if slot is None or p.grad is not None or getattr(p, "_dpa_uses", 0) != 1:
         return None
     return slot()
 
@@ -230,7 +232,8 @@ class Conv2dNHWC(torch.autograd.Function):
         P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
         ctx.geom = (N, H, W, C, K, R, S, stride, pad, P, Q)
         ctx.impl = impl
-        ctx.w_param, ctx.w_use = w, note_use(w)
+        ctx.w_param = w
+        note_use(w)
         if not _native(x):
             z = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
             ctx.save_for_backward(x, w)
@@ -268,7 +271,7 @@ class Conv2dNHWC(torch.autograd.Function):
                 dx = torch.nn.grad.conv2d_input(xn.shape, wn, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
             if ctx.needs_input_grad[1]:
                 dw = torch.nn.grad.conv2d_weight(xn, wn.shape, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
-                slot = grad_slot(ctx.w_param, ctx.w_use)
+                slot = grad_slot(ctx.w_param)
                 if slot is not None:
                     dw = slot.copy_(dw)
             return dx, dw, None, None, None
@@ -289,7 +292,7 @@ class Conv2dNHWC(torch.autograd.Function):
                                 lambda s: 4 * s * N * H * W * C)
             run_d(cfg[0], Kx.x3_splits(R * S * K, cfg[1]), cfg[2])
         if ctx.needs_input_grad[1]:
-            dw = grad_slot(ctx.w_param, ctx.w_use)
+            dw = grad_slot(ctx.w_param)
             if dw is None:
                 dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
 
@@ -328,7 +331,9 @@ class BnActNHWC(torch.autograd.Function):
         K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None)
         ctx.act, ctx.training = act, training
         ctx.params = (gamma, beta)
-        ctx.uses = (note_use(gamma), note_use(beta)) if training else (0, 0)
+        if training:
+            note_use(gamma)
+            note_use(beta)
         ctx.save_for_backward(z, res if act == 2 else None, gamma, mean, invstd, scale, shift)
         return a
 
@@ -343,7 +348,7 @@ class BnActNHWC(torch.autograd.Function):
         K = _ext.require() if native else cpu_ref
         f32 = dict(device=z.device, dtype=torch.float32 if native else z.dtype)
         dz = torch.empty_like(z)
-        dgamma, dbeta = (grad_slot(p, u) for p, u in zip(ctx.params, ctx.uses))
+        dgamma, dbeta = (grad_slot(p) for p in ctx.params)
         if dgamma is None or dgamma.dtype != f32["dtype"]:
             dgamma = torch.empty(C, **f32)
         if dbeta is None or dbeta.dtype != f32["dtype"]:

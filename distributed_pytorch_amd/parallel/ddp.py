@@ -172,7 +172,16 @@ class DistributedDataParallel(nn.Module):
 
     # ---------------------------------------------------------------- gradient buckets
     def _make_hook(self, i: int):
-        def hook(_p):
+        def hook(p):
+            if self._direct[i]:
+                # a parameter used more than once in the forward gets its gradient summed by
+                # autograd into a fresh tensor: move it into the arena slot the collectives and the
+                # fused optimizer read
+                v = self._gflat.view(i, p)
+                if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                    with torch.no_grad():
+                        v.copy_(p.grad)
+                    p.grad = v
             # first gradient of the step: the forward is over, so rank 0's buffers (BN running
             # stats) are final for this step -- broadcast them now, under the backward, instead of
             # before the next forward (nothing changes them in between; finish() orders the

@@ -157,6 +157,10 @@ class GradSync:
         self.comm.wait()
         e.refresh_weight_planes()
 
+    def prepare_checkpoint(self):
+        """Collective hook before every rank writes its checkpoint: make the local optimizer state
+        complete (a no-op except for sharded optimizer state)."""
+
     def pre_forward(self):
         """Called before the training forward.  May return a callable that the engine invokes
         right before the first read of the BN buffers (so a buffer broadcast overlaps the first
@@ -308,7 +312,14 @@ class AllReduceSync(GradSync):
 
 
 class DDPSync(GradSync):
-    """Mode C: DistributedDataParallel semantics on RCCL."""
+    """Mode C: DistributedDataParallel semantics on RCCL.
+
+    One intentional difference from torch DDP: rank 0's BN running statistics are broadcast right
+    after each training forward (under the backward) instead of before the next forward, so after
+    the last training step every replica already holds rank 0's statistics — which torch DDP only
+    establishes at the first eval forward.  Eval results are identical; a per-rank checkpoint taken
+    at that point holds rank 0's statistics on every rank (``DPA_BUF_BCAST=pre`` restores torch's
+    placement)."""
 
     mode = "ddp"
 
@@ -374,6 +385,32 @@ class ZeroSync(DDPSync):
                 if b.numel % (4 * self.world):
                     raise ValueError(f"zero1: bucket of {b.numel} elements does not split into 4-aligned shards "
                                      f"over {self.world} ranks")
+
+    def broadcast_state(self):
+        """Parameters (and BN buffers) from rank 0, but NOT momenta: under ZeRO-1 every rank updates
+        only its own shards' momentum, so rank 0's copy of the other shards is stale.  A resumed
+        rank holds the complete momentum arena already (``prepare_checkpoint`` all-gathers the
+        shards before each save)."""
+        e = self.engine
+        with self.comm.region():
+            self.comm.broadcast(e.params.flat, 0)
+            if self.shared_buffers:
+                self.comm.broadcast(e.buffers.flat, 0)
+                self.comm.broadcast(e.nbt, 0)
+        self.comm.wait()
+        e.refresh_weight_planes()
+
+    def prepare_checkpoint(self):
+        """All-gather every bucket's owned momentum shards so each rank's arena (and checkpoint)
+        holds the full, current SGD state."""
+        if not self.active:
+            return
+        e = self.engine
+        with self.comm.region():
+            for b in self.buckets:
+                lo, sb = self._shard(b)
+                self.comm.all_gather(e.mom.flat[lo:lo + sb], e.mom.flat[b.lo:b.hi])
+        self.comm.wait()
 
     def _shard(self, b: Bucket):
         sb = b.numel // self.world

@@ -114,6 +114,7 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
             t_win = now
             ctx.comm.check()
         if ck_every and args.checkpoint_dir and (batch_idx + 1) % ck_every == 0:
+            sync.prepare_checkpoint()
             checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch, batch_idx + 1, args.sampler_seed, ctx.world,
                             sync.mode, ddp_prefix=sync.mode == "ddp")
         if max_iters and n_iters >= max_iters:
@@ -175,6 +176,9 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--checkpoint-dir", default=None)
     g.add_argument("--checkpoint-every", type=int, default=0)
     g.add_argument("--resume", action="store_true")
+    g.add_argument("--resume-reshard", action="store_true",
+                   help="resume a checkpoint written with a different world size / sync mode: load weights and "
+                        "optimizer state, restart its epoch at batch 0")
     g.add_argument("--max-iters", type=int, default=None, help="stop each epoch after this many iterations")
     g.add_argument("--stop-after-iters", type=int, default=None,
                    help="end the whole run after this many training iterations, mid-epoch if need be, writing a "
@@ -184,8 +188,36 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--graph", action="store_true",
                    help="single rank: replay the training step as a captured HIP graph (graph_step.py)")
     g.add_argument("--json-metrics", default=None, help="append a JSON metrics line per epoch to this file")
+    g.add_argument("--single-gpu-img-s", type=float, default=None,
+                   help="1-GPU images/sec of the same config (e.g. bench.py --gpus 1): adds scaling_efficiency "
+                        "to --json-metrics")
     g.add_argument("--port", type=int, default=6585)
     return ap
+
+
+def resume(ctx: DistContext, engine: VGGEngine, mode: str, args, n_batches: int):
+    """Load this rank's checkpoint (``--resume``) and check that every rank resumes from the same
+    point; returns (start_epoch, start_batch).  Runs BEFORE the sync strategy's start-up broadcast,
+    whose momentum broadcast depends on the (now agreed) step count."""
+    if not (args.resume and args.checkpoint_dir):
+        return 0, 0
+    err, obj = None, None
+    try:
+        obj = checkpoint.load(args.checkpoint_dir, ctx.rank, engine, world=ctx.world, mode=mode,
+                              reshard=getattr(args, "resume_reshard", False))
+        point = checkpoint.resume_point(obj)
+    except checkpoint.ResumeMismatch as e:
+        err, point = e, (-1, -1, -1, -1)
+    # every rank must resume from the same point (a collective: fails on all ranks, not one)
+    checkpoint.agree(ctx.comm, point, ctx.device)
+    if err is not None:
+        raise err
+    if obj is None:
+        return 0, 0
+    start_epoch, start_batch = obj["epoch"], obj["batch_idx"]
+    if start_batch >= n_batches:
+        start_epoch, start_batch = start_epoch + 1, 0
+    return start_epoch, start_batch
 
 
 def run(ctx: DistContext, mode: str, args):
@@ -201,13 +233,7 @@ def run(ctx: DistContext, mode: str, args):
     engine = VGGEngine(args.model, ctx.device, max_batch=args.batch_size, lr=args.lr, momentum=args.momentum,
                        weight_decay=args.weight_decay, impl=args.impl)
     engine.init_parameters(seed=args.seed)
-    start_epoch, start_batch = 0, 0
-    if args.resume and args.checkpoint_dir:
-        obj = checkpoint.load(args.checkpoint_dir, ctx.rank, engine)
-        if obj is not None:
-            start_epoch, start_batch = obj["epoch"], obj["batch_idx"]
-            if start_batch >= len(train_loader):
-                start_epoch, start_batch = start_epoch + 1, 0
+    start_epoch, start_batch = resume(ctx, engine, mode, args, len(train_loader))
     sync = make_sync(mode, engine, ctx.comm, bucket_mb=args.bucket_mb, overlap=not args.no_overlap)
     budget = getattr(args, "stop_after_iters", None)
     for epoch in range(start_epoch, args.epochs):
@@ -220,10 +246,12 @@ def run(ctx: DistContext, mode: str, args):
             budget -= stats.get("iters_run", 0)
         if stopped is not None:  # preempted mid-epoch: checkpoint the position, no eval
             if args.checkpoint_dir:
+                sync.prepare_checkpoint()
                 checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch, stopped, args.sampler_seed, ctx.world,
                                 mode, ddp_prefix=mode == "ddp")
             break
         if args.checkpoint_dir:
+            sync.prepare_checkpoint()
             checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch + 1, 0, args.sampler_seed, ctx.world, mode,
                             ddp_prefix=mode == "ddp")
         res = None
@@ -231,7 +259,11 @@ def run(ctx: DistContext, mode: str, args):
             res = test_model(engine, test_loader, sync)
         if args.json_metrics and ctx.rank == 0:
             rec = dict(stats, epoch=epoch + 1, mode=mode, world=ctx.world, model=args.model,
-                       batch_per_rank=args.batch_size)
+                       batch_per_rank=args.batch_size, comm=ctx.comm.name)
+            base = getattr(args, "single_gpu_img_s", None)
+            if base and "images_per_sec_rank" in stats:
+                # weak scaling: per-rank throughput relative to one GPU running alone
+                rec["scaling_efficiency"] = stats["images_per_sec_rank"] / base
             if res:
                 rec["test_loss"], rec["test_correct"] = res
             with open(args.json_metrics, "a") as f:

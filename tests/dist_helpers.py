@@ -59,8 +59,9 @@ def run_engine_mode(rank, world, port, mode, steps, outdir, bucket_mb=None, over
         wait = sync.pre_forward()  # what the first eval forward does
         if wait is not None:
             wait()
+    sync.prepare_checkpoint()  # zero1: all-gather the momentum shards (no-op for the other modes)
     torch.save({"params": e.params.flat.clone(), "buffers": e.buffers.flat.clone(), "losses": losses,
-                "sd": e.state_dict()}, os.path.join(outdir, f"{mode}_{rank}.pt"))
+                "mom": e.mom.flat.clone(), "sd": e.state_dict()}, os.path.join(outdir, f"{mode}_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -180,3 +181,33 @@ def run_native_store(rank, world, port, outdir):
     with open(os.path.join(outdir, f"ns_{rank}.json"), "w") as f:
         json.dump({"uid": list(uid), "max": mx, "cnt": cnt}, f)
     st.close()  # rank 0 keeps serving until every client checked out
+
+
+def run_resume_agree(rank, world, port, ckdir, outdir, batch_idx_by_rank, world_saved=None):
+    """Each rank writes a checkpoint (its own batch index, or none if None), then resumes through
+    train.resume exactly like a training run; records what happened."""
+    import argparse
+    import json
+
+    from distributed_pytorch_amd.engine import VGGEngine
+    from distributed_pytorch_amd.parallel import DistContext, TorchComm
+    from distributed_pytorch_amd.train import resume
+    from distributed_pytorch_amd.utils import checkpoint
+
+    _init(rank, world, port)
+    comm = TorchComm(device=torch.device("cpu"))
+    ctx = DistContext(rank, world, rank, torch.device("cpu"), comm, True)
+    e = VGGEngine("VGG11", "cpu", max_batch=4)
+    bi = batch_idx_by_rank[rank]
+    if bi is not None:
+        checkpoint.save(ckdir, rank, e, 0, bi, 0, world_saved or world, "ddp", ddp_prefix=True)
+    dist.barrier()
+    args = argparse.Namespace(resume=True, checkpoint_dir=ckdir, resume_reshard=False)
+    try:
+        out = {"ok": list(resume(ctx, e, "ddp", args, 100))}
+    except checkpoint.ResumeMismatch as ex:
+        out = {"error": str(ex)}
+    with open(os.path.join(outdir, f"resume_{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -50,6 +50,15 @@ def test_modes_agree(mode_results):
             assert all(abs(x - y) < 1e-4 for x, y in zip(la, lb))
 
 
+def test_zero1_checkpoint_momentum_is_complete(mode_results):
+    """After prepare_checkpoint, every zero1 rank holds the full momentum arena (not just its
+    shards) and it equals DDP's (same math, sharded update)."""
+    ref = mode_results["ddp"][0]["mom"]
+    for r in range(WORLD):
+        m = mode_results["zero1"][r]["mom"]
+        assert (m - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item()), r
+
+
 def test_ddp_matches_torch_ddp(mode_results):
     ours = mode_results["ddp"][0]["sd"]
     ref = mode_results["torchddp"][0]["sd"]

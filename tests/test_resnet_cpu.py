@@ -63,3 +63,43 @@ def test_eval_mode_uses_running_stats():
     ref.eval()
     with torch.no_grad():
         assert torch.allclose(ours(x.permute(0, 2, 3, 1).contiguous()), ref(x), rtol=1e-9, atol=1e-9)
+
+
+def test_ddp_arena_holds_gradient_of_a_weight_used_twice():
+    """A conv weight / BN affine used twice in one forward: both uses' gradients must reach the
+    arena slot the collectives and FlatSGD read (not just p.grad)."""
+    import torch.nn as nn
+
+    from distributed_pytorch_amd.ops.layers import BatchNorm2d, Conv2d
+    from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel
+
+    class Twice(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = Conv2d(8, 8, 3, 1, 1, impl="x3")
+            self.bn = BatchNorm2d(8, act="relu")
+            self.once = Conv2d(8, 8, 3, 1, 1, impl="x3")
+
+        def forward(self, x):
+            y = self.bn(self.conv(x))
+            y = self.bn(self.conv(y))  # same weight, same BN affine, second use
+            return self.once(y)
+
+    torch.manual_seed(0)
+    ref = Twice().double()
+    m = Twice().double()
+    m.load_state_dict(ref.state_dict())
+    ddp = DistributedDataParallel(m, bucket_mb=0.01)
+    x = torch.randn(2, 6, 6, 8, dtype=torch.float64)
+    for it in range(2):  # the second iteration runs with the arena views already adopted
+        ddp.zero_grad()
+        ddp(x).square().sum().backward()
+        ddp.finish()
+        ref.zero_grad()
+        ref(x).square().sum().backward()
+        po = dict(m.named_parameters())
+        for n, p in ref.named_parameters():
+            i = next(j for j, q in enumerate(ddp._params) if q is po[n])
+            arena = ddp._gflat.view(i, po[n])
+            assert torch.allclose(arena, p.grad, rtol=1e-10, atol=1e-12), (it, n)
+            assert torch.allclose(po[n].grad, p.grad, rtol=1e-10, atol=1e-12), (it, n)
