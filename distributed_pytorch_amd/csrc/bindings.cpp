@@ -31,6 +31,11 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st);
+long dpa_wgrad0_part_floats(int N);
+int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
+                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
+                      float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
+                      float* dw, int CP, int N, hipStream_t st);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st);
@@ -425,6 +430,31 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t
 
 // gsrc: grad wrt the layer output (pooled shape if pool) or nsplit slabs of it (then the sum is
 // written to g).
+// First VGG layer's backward: BN backward (ReLU + 2x2 max-pool) fused with the 3x3 weight gradient
+// on the fp32 network input (bn.hip, bn_bwd_wgrad0_kernel).  z [N,32,32,64], g [N,16,16,64],
+// x [N,32,32,4], dw [64,3,3,CP], wpart >= wgrad0_part_floats(N).
+void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean,
+                   Tensor invstd, Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias,
+                   Tensor x, Tensor wpart, Tensor dw) {
+  for (auto* t : {&gsrc, &g, &z, &scale, &shift, &mean, &invstd, &gamma, &part, &coef, &dgamma, &dbeta, &x, &wpart, &dw})
+    need(*t, "bn_bwd_wgrad0 operand");
+  const int N = z.size(0);
+  TORCH_CHECK(z.dim() == 4 && z.size(1) == 32 && z.size(2) == 32 && z.size(3) == 64, "bn_bwd_wgrad0: z [N,32,32,64]");
+  TORCH_CHECK(g.numel() == (int64_t)N * 16 * 16 * 64, "bn_bwd_wgrad0: g [N,16,16,64]");
+  TORCH_CHECK(gsrc.numel() >= nsplit * g.numel(), "bn_bwd_wgrad0: gsrc too small");
+  TORCH_CHECK(x.dim() == 4 && x.size(0) == N && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4,
+              "bn_bwd_wgrad0: x [N,32,32,4]");
+  TORCH_CHECK(dw.dim() == 4 && dw.size(0) == 64 && dw.size(1) == 3 && dw.size(2) == 3 && dw.size(3) >= 3,
+              "bn_bwd_wgrad0: dw [64,3,3,CP]");
+  TORCH_CHECK(wpart.numel() >= dpa_wgrad0_part_floats(N), "bn_bwd_wgrad0: wpart too small");
+  TORCH_CHECK(part.numel() >= dpa_bn_part_floats(N * 256, 64, 1), "bn_bwd_wgrad0: part too small");
+  TORCH_CHECK(coef.numel() >= 3 * 64 && scale.numel() == 64 && gamma.numel() == 64, "bn_bwd_wgrad0: channel vectors");
+  chk(dpa_bn_bwd_wgrad0(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma),
+                        fp(part), fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), fp(x), fp(wpart), fp(dw),
+                        (int)dw.size(3), N, cur_stream()),
+      "bn_bwd_wgrad0");
+}
+
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
             int64_t act, OptT res, OptT dres) {
@@ -685,6 +715,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none());
+  m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0);
+  m.def("wgrad0_part_floats", [](int64_t N) { return dpa_wgrad0_part_floats((int)N); });
   m.def("fc_ce_train", &fc_ce_train);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);

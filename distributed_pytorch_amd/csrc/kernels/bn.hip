@@ -24,7 +24,7 @@
 // float4 lanes, RT/(C/4) rows in flight, 4 rows' loads issued together), keeps per-thread partials
 // in registers, combines them with an LDS tree, and writes ONE partial per (block, channel) —
 // deterministic, no atomics.  ~256 blocks: one wave of full CUs, few partials to merge.  The
-// backward reduce uses RTB (256) -thread blocks, ~1024 of them (see RTB).
+// backward reduce uses RTB (256) -thread blocks, ~512 of them (see RTB).
 #include "common.h"
 
 #include <cstdlib>
@@ -32,12 +32,13 @@
 namespace {
 
 constexpr int RT = 1024;  // forward-statistics block size
-// Backward reduce: 256-thread blocks with a 4 KB LDS tree, ~1024 of them.  The backward reduce runs
+// Backward reduce: 256-thread blocks with a 4 KB LDS tree, ~512 of them (512: +2.2 % step
+// throughput over 1024 and +0.7 % over 256, fewer partial rows for the finalize).  The backward reduce runs
 // beside the weight-gradient convs of the other stream; a 1024-thread / 48 KB block could not be
 // placed on a CU holding conv blocks and waited for whole CUs to drain (3-6x slower in the step).
 // DPA_BN_BWD_BLOCK=1024 selects the old single-stream geometry (1024 threads, ~256 blocks) for A/B.
 constexpr int RTB = 256;
-constexpr int BWD_BLOCKS = 1024;
+constexpr int BWD_BLOCKS = 512;
 inline bool bwd_wide() {
   static const bool w = [] {
     const char* e = std::getenv("DPA_BN_BWD_BLOCK");
@@ -45,8 +46,23 @@ inline bool bwd_wide() {
   }();
   return w;
 }
+// channels per backward-finalize block: 8 (32 partial rows of each in flight) or 4 (64 rows;
+// DPA_BN_FIN_CPB=4).  Equal within noise in the step (158.5k vs 158.2k img/s), 8 is kept.
+inline int fin_cpb() {
+  static const int v = [] {
+    const char* e = std::getenv("DPA_BN_FIN_CPB");
+    return e ? std::atoi(e) : 8;
+  }();
+  return v;
+}
 inline int bwd_rt() { return bwd_wide() ? RT : RTB; }
-inline int bwd_blocks() { return bwd_wide() ? 256 : BWD_BLOCKS; }
+inline int bwd_blocks() {
+  static const int nb = [] {
+    const char* e = std::getenv("DPA_BN_BWD_BLOCKS");  // A/B of the backward reduce grid size
+    return e ? std::atoi(e) : BWD_BLOCKS;
+  }();
+  return bwd_wide() ? 256 : nb;
+}
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -225,22 +241,25 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
                                                           float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float momentum, float eps) {
-  const int cl = threadIdx.x & 7, grp = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + cl;
+  // 4 channels per block, 64 partial rows of each in flight (one batch of loads per thread for the
+  // ~256 partial rows of the statistics pass), fixed-order Chan merges
+  constexpr int CPB = 4, G = 256 / CPB;
+  const int cl = threadIdx.x % CPB, grp = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + cl;
   Welford acc{0.f, 0.f, 0.f};
   if (c < C) {
     int k = grp;
-    for (; k + 96 < nblk; k += 128) {
+    for (; k + 3 * G < nblk; k += 4 * G) {
       float2 p[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) p[u] = part[(long)(k + 32 * u) * C + c];
+      for (int u = 0; u < 4; ++u) p[u] = part[(long)(k + G * u) * C + c];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int kk = k + 32 * u;
+        const int kk = k + G * u;
         acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
       }
     }
-    for (; k < nblk; k += 32) {
+    for (; k < nblk; k += G) {
       const float2 p = part[(long)k * C + c];
       acc = merge(acc, Welford{(float)min(rpb, M - k * rpb), p.x, p.y});
     }
@@ -248,7 +267,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
   __shared__ Welford sh[256];
   sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int o = 128; o >= 8; o >>= 1) {
+  for (int o = 128; o >= CPB; o >>= 1) {
     if ((int)threadIdx.x < o) sh[threadIdx.x] = merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
@@ -449,34 +468,38 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
 
 // Per channel: sum the block partials (fixed order -> deterministic), emit dgamma, dbeta, dbias and
 // the dz coefficients: dz = k1*dy + k2*z + k3.   8 channels x 32 groups per block.
+// Backward finalize: BF_CPB channels per 256-thread block, 256/BF_CPB partial rows of each in
+// flight (a thread's loads are issued 8 rows at a time), fixed-order LDS tree.
+template <int BF_CPB>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                               float Mfull, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ dbias, float* __restrict__ coef) {
-  const int cl = threadIdx.x & 7, grp = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + cl;
+  constexpr int G = 256 / BF_CPB;  // partial-row groups per channel
+  const int cl = threadIdx.x % BF_CPB, grp = threadIdx.x / BF_CPB;
+  const int c = blockIdx.x * BF_CPB + cl;
   float a = 0.f, b = 0.f, x = 0.f;
   if (c < C) {
     int k = grp;
-    for (; k + 96 < nblk; k += 128) {
-      float pa[4], pb[4], px[4];
+    for (; k + 7 * G < nblk; k += 8 * G) {
+      float pa[8], pb[8], px[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float* p = part + (long)(k + 32 * u) * 3 * C + c;
+      for (int u = 0; u < 8; ++u) {
+        const float* p = part + (long)(k + G * u) * 3 * C + c;
         pa[u] = p[0];
         pb[u] = p[C];
         px[u] = p[2 * C];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         a += pa[u];
         b += pb[u];
         x += px[u];
       }
     }
-    for (; k < nblk; k += 32) {
+    for (; k < nblk; k += G) {
       const float* p = part + (long)k * 3 * C + c;
       a += p[0];
       b += p[C];
@@ -488,7 +511,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   sh[1][threadIdx.x] = b;
   sh[2][threadIdx.x] = x;
   __syncthreads();
-  for (int o = 128; o >= 8; o >>= 1) {
+  for (int o = 128; o >= BF_CPB; o >>= 1) {
     if ((int)threadIdx.x < o) {
       sh[0][threadIdx.x] += sh[0][threadIdx.x + o];
       sh[1][threadIdx.x] += sh[1][threadIdx.x + o];
@@ -586,7 +609,7 @@ int bn_fwd_stats_host(const TZ* src, int nsplit, TZ* z, float* part, int M, int 
   const int nblk = (M + rpb - 1) / rpb;
   bn_stats_kernel<TZ><<<nblk, RT, 0, st>>>(src, z, nsplit < 1 ? 1 : nsplit, reinterpret_cast<float2*>(part), M, C,
                                            rpb);
-  bn_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
+  bn_finalize_kernel<<<cdiv(C, 4), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
                                                   bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
   return (int)hipGetLastError();
 }
@@ -644,12 +667,13 @@ void bn_bwd_apply_launch(int act, int grid, hipStream_t st, const TZ* g, const T
   }
 }
 
+// Backward statistics: reduce pass (summing split-K dgrad slabs of g into g when nsplit > 1) and
+// finalize (dgamma, dbeta, dbias, apply coefficients).
 template <typename TZ>
-int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
-                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
-                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-                const TZ* res, TZ* dres, hipStream_t st) {
-  if (nsplit < 1) nsplit = 1;
+void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
+                  const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
+                  float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
+                  hipStream_t st) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = red_rows_per_block(Mo, C, bwd_rt(), bwd_blocks());
@@ -671,8 +695,164 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
     RED(false, 2);
   }
 #undef RED
-  bn_bwd_finalize_kernel<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
-                                                      dbeta, dbias, coef);
+  if (fin_cpb() == 8)
+    bn_bwd_finalize_kernel<8><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
+                                                          dgamma, dbeta, dbias, coef);
+  else
+    bn_bwd_finalize_kernel<4><<<cdiv(C, 4), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
+                                                          dgamma, dbeta, dbias, coef);
+}
+
+
+// ---- first layer: BN backward apply fused with the 3x3/s1/p1 weight gradient on the network input.
+// Layer 0 of VGG (model.py:18-25 with in_channels 3) has no data gradient, so its dz is read only by
+// its weight gradient: dW[co][r][s][ci] = sum_{n,h,w} dz[n,h,w,co] * x[n,h+r-1,w+s-1,ci].  Here each
+// thread computes dz for a 2x2 pool window x 4 channels (the apply kernel's routing + coefficients,
+// never stored) and accumulates the 27 (tap, input channel) products of each in fp32 registers.
+// x (fp32 NHWC, 4 channels, the 4th zero) is staged once per block in LDS with its zero halo.
+// Geometry: H = W = 32, 2x2 pool, C = 64, <= 3 live input channels; block = one image band of WB0_RPB
+// pooled rows; 256 threads = 16 channel quads x 16 pooled columns, a quad's 16 column lanes form one
+// 16-lane row of a wave.  Block partials [blocks][C][27] are summed in a fixed order by
+// wgrad0_reduce_kernel (deterministic, no atomics).
+constexpr int WB0_RPB = 8;          // pooled rows per block
+constexpr int WB0_XR = 2 * WB0_RPB + 2;  // staged input rows (with halo)
+constexpr int WB0_XC = 34;          // staged input columns (32 + halo)
+
+__global__ __launch_bounds__(256) void bn_bwd_wgrad0_kernel(const float* __restrict__ g, const float* __restrict__ z,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            const float* __restrict__ coef,
+                                                            const float* __restrict__ x, float* __restrict__ wpart) {
+  constexpr int H = 32, W = 32, C = 64, C4 = 16, Ho = 16, Wo = 16;
+  constexpr int bands = Ho / WB0_RPB;
+  __shared__ float4 xs[WB0_XR][WB0_XC];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
+  const int ow = lane & 15;
+  const int c4 = wv * 4 + (lane >> 4);
+  const int n = blockIdx.x / bands, band = blockIdx.x % bands;
+  const int oh0 = band * WB0_RPB;
+  const int h_lo = 2 * oh0 - 1;  // first staged input row
+  // stage x rows h_lo .. h_lo + XR - 1, columns -1 .. 32 (zero outside the image)
+  for (int e = t; e < WB0_XR * WB0_XC; e += 256) {
+    const int rr = e / WB0_XC, cc = e % WB0_XC;
+    const int h = h_lo + rr, w = cc - 1;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (h >= 0 && h < H && w >= 0 && w < W) v = reinterpret_cast<const float4*>(x)[((long)n * H + h) * W + w];
+    xs[rr][cc] = v;
+  }
+  __syncthreads();
+  const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
+  const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
+  const float4 k1 = reinterpret_cast<const float4*>(coef)[c4];
+  const float4 k2 = reinterpret_cast<const float4*>(coef + C)[c4];
+  const float4 k3 = reinterpret_cast<const float4*>(coef + 2 * C)[c4];
+  float acc[4][27];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 27; ++j) acc[k][j] = 0.f;
+  for (int oh = oh0; oh < oh0 + WB0_RPB; ++oh) {
+    const float4 gv = reinterpret_cast<const float4*>(g)[(((long)n * Ho + oh) * Wo + ow) * C4 + c4];
+    const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * C4 + c4;
+    float4 zq[4];
+    zq[0] = reinterpret_cast<const float4*>(z)[base];
+    zq[1] = reinterpret_cast<const float4*>(z)[base + C4];
+    zq[2] = reinterpret_cast<const float4*>(z)[base + W * C4];
+    zq[3] = reinterpret_cast<const float4*>(z)[base + W * C4 + C4];
+    float d[4][4];  // [window position][channel]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float r[4];
+      route1(F4GET(zq[0], k), F4GET(zq[1], k), F4GET(zq[2], k), F4GET(zq[3], k), F4GET(sc, k), F4GET(sh, k),
+             F4GET(gv, k), r[0], r[1], r[2], r[3]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q][k] = F4GET(k1, k) * r[q] + F4GET(k2, k) * F4GET(zq[q], k) + F4GET(k3, k);
+    }
+    // the 4x4 input neighbourhood of the 2x2 window: rows 2oh-1 .. 2oh+2, columns 2ow-1 .. 2ow+2
+    const int xr = 2 * oh - 1 - h_lo;  // staged row of input row 2oh-1
+    float4 nb[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) nb[a][b] = xs[xr + a][2 * ow + b];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int dh = q >> 1, dw = q & 1;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2) {
+          const float4 xv = nb[dh + r][dw + s2];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            acc[k][(r * 3 + s2) * 3 + 0] = fmaf(d[q][k], xv.x, acc[k][(r * 3 + s2) * 3 + 0]);
+            acc[k][(r * 3 + s2) * 3 + 1] = fmaf(d[q][k], xv.y, acc[k][(r * 3 + s2) * 3 + 1]);
+            acc[k][(r * 3 + s2) * 3 + 2] = fmaf(d[q][k], xv.z, acc[k][(r * 3 + s2) * 3 + 2]);
+          }
+        }
+    }
+  }
+  // sum over the 16 column lanes of each channel quad (fixed xor order), lane ow == 0 writes
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 27; ++j) {
+      float v = acc[k][j];
+      v += __shfl_xor(v, 8, 16);
+      v += __shfl_xor(v, 4, 16);
+      v += __shfl_xor(v, 2, 16);
+      v += __shfl_xor(v, 1, 16);
+      acc[k][j] = v;
+    }
+  if (ow == 0) {
+    float* o = wpart + (long)blockIdx.x * C * 27 + (long)(4 * c4) * 27;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 27; ++j) o[k * 27 + j] = acc[k][j];
+  }
+}
+
+// dw[co][r][s][0..CP) (KRSC, CP = padded input channels; channels >= 3 get 0) = fixed-order sum of
+// the block partials [nblk][C][27].  One block per output channel: 32 groups x 32 lanes.
+__global__ __launch_bounds__(1024) void wgrad0_reduce_kernel(const float* __restrict__ wpart, int nblk, int C,
+                                                             float* __restrict__ dw, int CP) {
+  __shared__ float sh[32][32];
+  const int co = blockIdx.x, j = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  float a = 0.f;
+  if (j < 27) {
+    int b = grp;
+    for (; b + 3 * 32 < nblk; b += 4 * 32) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = wpart[((long)(b + 32 * u) * C + co) * 27 + j];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a += v[u];
+    }
+    for (; b < nblk; b += 32) a += wpart[((long)b * C + co) * 27 + j];
+  }
+  sh[grp][j] = a;
+  __syncthreads();
+  for (int o = 16; o >= 1; o >>= 1) {
+    if (grp < o) sh[grp][j] += sh[grp + o][j];
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < 9 * CP; e += 1024) {
+    const int rs = e / CP, ci = e % CP;
+    dw[(long)co * 9 * CP + e] = ci < 3 ? sh[0][rs * 3 + ci] : 0.f;
+  }
+}
+
+template <typename TZ>
+int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
+                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
+                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
+                const TZ* res, TZ* dres, hipStream_t st) {
+  if (nsplit < 1) nsplit = 1;
+  bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
+                   C, pool, act, res, st);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
   const long ps = (long)N * H * W * C;
@@ -748,4 +928,22 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                             (float*)dres, st);
 }
 
+// Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.
+// g [N,16,16,64] (or nsplit slabs of it in gsrc), z [N,32,32,64], x [N,32,32,4] fp32, dw [64,3,3,CP].
+long dpa_wgrad0_part_floats(int N) { return (long)N * (16 / WB0_RPB) * 64 * 27; }
+
+int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
+                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
+                      float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
+                      float* dw, int CP, int N, hipStream_t st) {
+  if (nsplit < 1) nsplit = 1;
+  if (CP < 3) return -2;
+  bn_bwd_stats<float>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, 32,
+                      32, 64, 1, 0, nullptr, st);
+  const float* gg = nsplit > 1 ? g : gsrc;
+  const int nblk = N * (16 / WB0_RPB);
+  bn_bwd_wgrad0_kernel<<<nblk, 256, 0, st>>>(gg, z, scale, shift, coef, x, wpart);
+  wgrad0_reduce_kernel<<<64, 1024, 0, st>>>(wpart, nblk, 64, dw, CP);
+  return (int)hipGetLastError();
+}
 }  // extern "C"

@@ -214,6 +214,14 @@ class VGGEngine:
                 if kind == "dgrad" and i == 0:
                     continue
                 self._ensure_slab(self._slab_need(i, kind, N), wgrad=kind == "wgrad" and self._wgrad_on_side(i))
+        # Layer 0 (3-channel input, 32x32, 2x2 pool) has no data gradient: its BN-backward apply and
+        # weight gradient run as one fused fp32 kernel (bn.hip bn_bwd_wgrad0_kernel) that never stores
+        # dz.  DPA_FUSED_WGRAD0=0 runs them separately (A/B).
+        l0 = L[0]
+        self.fused_wgrad0 = (dev.type == "cuda" and hasattr(self.K, "bn_bwd_wgrad0")
+                             and os.environ.get("DPA_FUSED_WGRAD0", "1") == "1"
+                             and l0.hw == 32 and l0.cout == 64 and l0.pool and l0.cin <= 3)
+        self.wpart = (torch.empty(self.K.wgrad0_part_floats(N), **f32) if self.fused_wgrad0 else None)
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -569,10 +577,20 @@ class VGGEngine:
             z = self.z[i][:n]
             g = self.g[i][:n]
             dzbuf = self.dz3[i][:, :n] if self.planes[i] else self.dz[i][:n]
+            names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
+            if i == 0 and self.fused_wgrad0:
+                K.bn_bwd_wgrad0(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
+                                st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
+                                G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], x, self.wpart,
+                                G[f"{l.conv_key}.weight"])
+                if grad_ready is not None:
+                    grad_ready(names)
+                if params_free is not None:
+                    params_free(names)
+                continue
             K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                      st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
                      G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool)
-            names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
                 # Layer 0's wgrad has nothing left to overlap with, so it stays on the main stream (a

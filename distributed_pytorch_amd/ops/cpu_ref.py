@@ -161,6 +161,22 @@ def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dg
         dbias.copy_(-k1 * sx * sdx / M)
 
 
+def wgrad0_part_floats(N):
+    return 1
+
+
+def bn_bwd_wgrad0(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, x, wpart,
+                  dw):
+    """Layer-0 backward (native: bn.hip bn_bwd_wgrad0_kernel): BN backward with ReLU + 2x2 max-pool
+    routing, then the 3x3/s1/p1 weight gradient on the input x [N,H,W,4] (channels >= 3 zero)."""
+    dz = torch.empty_like(z)
+    bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, True)
+    cin = 3
+    w = torch.nn.grad.conv2d_weight(_nchw(x[..., :cin]), (z.shape[-1], cin, 3, 3), _nchw(dz), padding=1)
+    dw.zero_()
+    dw[..., :cin].copy_(w.permute(0, 2, 3, 1))
+
+
 # ---------------------------------------------------------------- classifier head
 def fc_ce_train(x, w, b, target, loss_row, dlogits, dx, dw, db, loss_out, loss_accum):
     B = x.shape[0]

@@ -1,0 +1,80 @@
+"""Fused kernels of the VGG step vs the plain-PyTorch reference of the same ops (cpu_ref, fp64)."""
+import pytest
+import torch
+
+from distributed_pytorch_amd.ops import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("N,nsplit,cp", [(256, 1, 8), (8, 3, 8), (5, 1, 4), (2, 2, 4)])
+def test_bn_bwd_wgrad0_matches_reference(N, nsplit, cp):
+    """Layer 0: BN backward (ReLU + 2x2 max-pool routing) fused with the 3x3 weight gradient on the
+    network input (bn.hip bn_bwd_wgrad0_kernel) vs BN backward + conv2d_weight in fp64."""
+    from distributed_pytorch_amd import _ext
+
+    C = _ext.require()
+    gen = torch.Generator().manual_seed(N * 10 + nsplit)
+    C_, H = 64, 32
+    z = torch.randn(N, H, H, C_, generator=gen) * 2 + 0.3
+    gs = torch.randn(nsplit, N, H // 2, H // 2, C_, generator=gen)
+    x = torch.zeros(N, H, H, 4)
+    x[..., :3] = torch.randn(N, H, H, 3, generator=gen)
+    gamma = torch.rand(C_, generator=gen) + 0.5
+    mean = z.reshape(-1, C_).mean(0)
+    invstd = torch.rsqrt(z.reshape(-1, C_).var(0, unbiased=False) + 1e-5)
+    scale = gamma * invstd
+    shift = torch.randn(C_, generator=gen) - mean * scale
+    # fp64 reference
+    d = {k: v.double() for k, v in dict(z=z, x=x, gamma=gamma, mean=mean, invstd=invstd, scale=scale,
+                                        shift=shift).items()}
+    ref = {k: torch.zeros(C_, dtype=torch.float64) for k in ("dgamma", "dbeta", "dbias")}
+    dw_ref = torch.zeros(C_, 3, 3, cp, dtype=torch.float64)
+    cpu_ref.bn_bwd_wgrad0(gs.double().reshape(-1), nsplit, torch.empty(N, 16, 16, C_, dtype=torch.float64), d["z"],
+                          d["scale"], d["shift"], d["mean"], d["invstd"], d["gamma"], None, None, ref["dgamma"],
+                          ref["dbeta"], ref["dbias"], d["x"], None, dw_ref)
+    # GPU
+    cu = lambda t: t.contiguous().cuda()
+    out = {k: torch.zeros(C_, device="cuda") for k in ("dgamma", "dbeta", "dbias")}
+    part = torch.zeros(C.bn_part_floats(N * 256, C_, True), device="cuda")
+    coef = torch.zeros(3 * C_, device="cuda")
+    wpart = torch.empty(C.wgrad0_part_floats(N), device="cuda")
+    dw = torch.full((C_, 3, 3, cp), 7.0, device="cuda")  # padded channels must come back as 0
+    g = torch.empty(N, 16, 16, C_, device="cuda")
+    C.bn_bwd_wgrad0(cu(gs.reshape(-1)), nsplit, g, cu(z), cu(scale), cu(shift), cu(mean), cu(invstd), cu(gamma), part,
+                    coef, out["dgamma"], out["dbeta"], out["dbias"], cu(x), wpart, dw)
+    torch.cuda.synchronize()
+    assert _rel(dw, dw_ref) < 2e-6, _rel(dw, dw_ref)
+    assert torch.all(dw[..., 3:] == 0)
+    for k in ("dgamma", "dbeta"):
+        assert _rel(out[k], ref[k]) < 2e-6, k
+    assert (out["dbias"].double().cpu() - ref["dbias"]).abs().max() < 1e-3  # analytically 0: roundoff only
+    if nsplit > 1:  # the split-K slabs were summed into g
+        assert _rel(g, gs.double().sum(0)) < 1e-6
+
+
+def test_fused_wgrad0_step_matches_unfused(monkeypatch):
+    """One x3 training step with the fused layer-0 backward vs the separate apply + x3 wgrad kernels."""
+    from distributed_pytorch_amd.engine import VGGEngine
+
+    g = torch.Generator().manual_seed(4)
+    x = torch.zeros(64, 32, 32, 4)
+    x[..., :3] = torch.randn(64, 32, 32, 3, generator=g)
+    t = torch.randint(0, 10, (64,), generator=g)
+    grads = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DPA_FUSED_WGRAD0", fused)
+        e = VGGEngine("VGG11", "cuda", max_batch=64, impl="x3")
+        e.init_parameters(seed=2)
+        assert e.fused_wgrad0 == (fused == "1")
+        e.forward_backward(x.cuda(), t.cuda())
+        torch.cuda.synchronize()
+        grads.append(e.grads.flat.clone())
+    w0 = slice(0, 64 * 9 * 8)  # layers.0.weight is the arena's first entry
+    assert _rel(grads[0][w0], grads[1][w0]) < 1e-5
+    assert torch.equal(grads[0][64 * 9 * 8:], grads[1][64 * 9 * 8:])  # everything else bit-identical

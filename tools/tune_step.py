@@ -1,0 +1,146 @@
+"""Tune the conv configurations of the VGG training step IN the step, not in isolation.
+
+tools/tune_convs.py times every (tile, split-K, row order) of a conv call alone.  In the step the
+backward runs on two streams (data gradients + BN backward on one, weight gradients + their split-K
+reductions on the other) that share the CUs, HBM and L2, so the fastest isolated configuration is
+not always the fastest in context (e.g. a wgrad with many splits runs its conv quickly but streams
+hundreds of MB of split-K slabs through the memory system the critical path needs).
+
+For every conv call of the step (one table key may cover several layers of the same shape) this
+keeps the ``--top`` best isolated candidates and picks, by coordinate descent, the one that gives
+the lowest whole-step time (median of ``--reps`` runs of ``--steps`` steps).  A candidate must win
+by ``--min-gain`` (relative) to replace the current choice.  The result is merged into
+distributed_pytorch_amd/tuning/mi355x.json ([tile, splits, posmajor, isolated_ms]).
+
+    python tools/tune_step.py [--batch 256] [--impl x3] [--top 5] [--kinds wgrad,dgrad,fprop]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from distributed_pytorch_amd.engine import conv_key  # noqa: E402
+from distributed_pytorch_amd.parallel import NullComm  # noqa: E402
+
+
+def step_ms(step, steps, reps):
+    out = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        out.append((time.perf_counter() - t0) / steps * 1e3)
+    return statistics.median(out)
+
+
+def isolated(e, i, kind, n, iters=3):
+    """[(ms, (tile, eff_splits, pm))] for every candidate of conv call (i, kind), fastest first."""
+    l = e.spec.convs[i]
+    impl = e._layer_impl(i)
+    key = (impl, kind, n, i)
+    saved = e._cfg_cache.get(key)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = []
+    for tile, s, pm in e.conv_candidates(i, kind):
+        M = n * l.hw * l.hw
+        red = M if kind == "wgrad" else 9 * (l.cin_pad if kind == "fprop" else l.cout)
+        s = e.K.conv_splits(red, s) if impl == "fp32" else e.K.x3_splits(red, s)
+        cand = (tile, s, pm)
+        if any(c == cand for _, c in res):
+            continue
+        e._cfg_cache[key] = cand
+        if e._slab_need(i, kind, n) * 4 > (256 << 20):
+            continue
+        fn = {"fprop": lambda: e._conv_fwd(i, e.x0[:n], n, reduce=False),
+              "dgrad": lambda: e._conv_dgrad(i, n),
+              "wgrad": lambda: e._conv_wgrad(i, e.x0[:n], n)}[kind]
+        fn()
+        ev0.record()
+        for _ in range(iters):
+            fn()
+        ev1.record()
+        torch.cuda.synchronize()
+        res.append((ev0.elapsed_time(ev1) / iters, cand))
+    if saved is not None:
+        e._cfg_cache[key] = saved
+    return sorted(res)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--impl", default="x3")
+    ap.add_argument("--top", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=15)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--min-gain", type=float, default=0.004)
+    ap.add_argument("--kinds", default="wgrad,dgrad,fprop")
+    ap.add_argument("--out", default=os.path.join(ROOT, "distributed_pytorch_amd", "tuning", "mi355x.json"))
+    ap.add_argument("--dry-run", action="store_true", help="report, do not write the table")
+    a = ap.parse_args()
+    args = bench.parse(["--batch", str(a.batch), "--impl", a.impl])
+    dev = torch.device("cuda", 0)
+    engine, sync, it = bench.build(args, dev, 0, 1, NullComm())
+    step = bench.make_step(engine, sync, it)
+    for _ in range(10):
+        step()
+    n = a.batch
+    base = step_ms(step, a.steps, a.reps)
+    print(json.dumps({"start_step_ms": round(base, 4)}), flush=True)
+    # group layers by table key (layers of identical shape share one entry)
+    groups = {}
+    for kind in a.kinds.split(","):
+        for i, l in enumerate(engine.spec.convs):
+            if kind == "dgrad" and i == 0:
+                continue
+            k = conv_key(engine._layer_impl(i), kind, n, l.hw, l.cin_pad, l.cout)
+            groups.setdefault(k, (kind, []))[1].append(i)
+    table = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    changed = {}
+    for k, (kind, layers) in groups.items():
+        i0 = layers[0]
+        cands = isolated(engine, i0, kind, n)
+        cur = engine.conv_config(i0, kind, n)
+        top = [c for _, c in cands[: a.top] if c != cur]
+        iso = {c: ms for ms, c in cands}
+        cur_ms = step_ms(step, a.steps, a.reps)
+        best, best_ms = cur, cur_ms
+        for c in top:
+            for i in layers:
+                engine._cfg_cache[(engine._layer_impl(i), kind, n, i)] = c
+            for _ in range(2):
+                step()
+            ms = step_ms(step, a.steps, a.reps)
+            print(f"  {k} {c} iso={iso.get(c, 0):.4f} step={ms:.4f} (cur {cur} {cur_ms:.4f})", flush=True)
+            if ms < best_ms * (1 - a.min_gain):
+                best, best_ms = c, ms
+        for i in layers:
+            engine._cfg_cache[(engine._layer_impl(i), kind, n, i)] = best
+        for _ in range(2):
+            step()
+        if best != cur:
+            changed[k] = [best[0], best[1], bool(best[2]), iso.get(best, 0.0)]
+        print(json.dumps({"key": k, "layers": layers, "choice": list(best), "was": list(cur),
+                          "step_ms": round(best_ms, 4), "was_ms": round(cur_ms, 4)}), flush=True)
+    final = step_ms(step, a.steps, a.reps * 2)
+    print(json.dumps({"start_step_ms": round(base, 4), "final_step_ms": round(final, 4),
+                      "changed": changed}), flush=True)
+    if changed and not a.dry_run:
+        table.update(changed)
+        with open(a.out, "w") as f:
+            json.dump(table, f, indent=0, sort_keys=True)
+        print("wrote", a.out, flush=True)
+
+
+if __name__ == "__main__":
+    main()
