@@ -32,6 +32,10 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st);
 long dpa_wgrad0_part_floats(int N);
+long dpa_conv0_part_floats(int N);
+int dpa_conv0_fwd(const float* x, const float* w, int CP, float* z, float* part, int N, const float* gamma,
+                  const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
+                  float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
@@ -455,6 +459,34 @@ void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale
       "bn_bwd_wgrad0");
 }
 
+// First VGG layer forward (first_layer.hip): direct fp32 3x3 conv of x [N,32,32,4] with w [64,3,3,CP]
+// into z [N,32,32,64].  Training (part given): BN batch statistics from the conv epilogue, then the
+// finalize (running stats, scale/shift); eval (part None): the conv only.
+void conv0_fwd(Tensor x, Tensor w, Tensor z, OptT part, OptT gamma, OptT beta, OptT bias, OptT rmean, OptT rvar,
+               OptT nbt, OptT mean, OptT invstd, OptT scale, OptT shift, double momentum, double eps) {
+  need(x, "x");
+  need(w, "w");
+  need(z, "z");
+  const int N = x.size(0);
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4, "conv0_fwd: x [N,32,32,4]");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) >= 3,
+              "conv0_fwd: w [64,3,3,CP]");
+  TORCH_CHECK(z.numel() == (int64_t)N * 32 * 32 * 64, "conv0_fwd: z [N,32,32,64]");
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    need(*part, "part");
+    TORCH_CHECK(part->numel() >= dpa_conv0_part_floats(N), "conv0_fwd: part too small");
+    for (const OptT* o : {&gamma, &beta, &mean, &invstd, &scale, &shift})
+      TORCH_CHECK(o->has_value() && (*o)->defined() && (*o)->numel() == 64, "conv0_fwd: channel vectors [64]");
+    pp = fp(*part);
+  }
+  long long* nb = nbt.has_value() && nbt->defined() ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr;
+  chk(dpa_conv0_fwd(fp(x), fp(w), (int)w.size(3), fp(z), pp, N, ofp(gamma), ofp(beta), ofp(bias), ofp(rmean),
+                    ofp(rvar), nb, ofp(mean), ofp(invstd), ofp(scale), ofp(shift), (float)momentum, (float)eps,
+                    cur_stream()),
+      "conv0_fwd");
+}
+
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
             int64_t act, OptT res, OptT dres) {
@@ -716,6 +748,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none());
   m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0);
+  m.def("conv0_fwd", &conv0_fwd, py::arg("x"), py::arg("w"), py::arg("z"), py::arg("part") = py::none(),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("bias") = py::none(),
+        py::arg("rmean") = py::none(), py::arg("rvar") = py::none(), py::arg("nbt") = py::none(),
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("scale") = py::none(),
+        py::arg("shift") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5);
+  m.def("conv0_part_floats", [](int64_t N) { return dpa_conv0_part_floats((int)N); });
   m.def("wgrad0_part_floats", [](int64_t N) { return dpa_wgrad0_part_floats((int)N); });
   m.def("fc_ce_train", &fc_ce_train);
   m.def("fc_ce_eval", &fc_ce_eval);

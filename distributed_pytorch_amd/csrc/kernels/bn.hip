@@ -894,6 +894,16 @@ int dpa_bn_fwd_stats(const void* src, int nsplit, void* z, float* part, int M, i
                                   nbt, mean, invstd, scale, shift, momentum, eps, st);
 }
 
+// Finalize from (mean, M2) partials of nblk row blocks of rpb rows each (the producer is not
+// bn_stats_kernel, e.g. the first-layer conv's epilogue, first_layer.hip).
+int dpa_bn_finalize(const float* part, int nblk, int rpb, int M, int C, const float* gamma, const float* beta,
+                    const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
+                    float* scale, float* shift, float momentum, float eps, hipStream_t st) {
+  bn_finalize_kernel<<<cdiv(C, 4), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
+                                                  bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
+  return (int)hipGetLastError();
+}
+
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
                        const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st) {
   bn_eval_params_kernel<<<cdiv(C, 256), 256, 0, st>>>(gamma, beta, bias, rmean, rvar, scale, shift, C, eps);

@@ -222,6 +222,12 @@ class VGGEngine:
                              and os.environ.get("DPA_FUSED_WGRAD0", "1") == "1"
                              and l0.hw == 32 and l0.cout == 64 and l0.pool and l0.cin <= 3)
         self.wpart = (torch.empty(self.K.wgrad0_part_floats(N), **f32) if self.fused_wgrad0 else None)
+        # Layer 0 forward: direct fp32 conv of the 3-channel input with the BN statistics in its epilogue
+        # (first_layer.hip); DPA_FUSED_CONV0=0 runs the implicit-GEMM conv + statistics pass (A/B)
+        self.fused_conv0 = (dev.type == "cuda" and hasattr(self.K, "conv0_fwd")
+                            and os.environ.get("DPA_FUSED_CONV0", "1") == "1"
+                            and l0.hw == 32 and l0.cout == 64 and l0.cin <= 3)
+        self.part0 = torch.empty(self.K.conv0_part_floats(N), **f32) if self.fused_conv0 else None
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -547,10 +553,20 @@ class VGGEngine:
         n = x.shape[0]
         L = self.spec.convs
         buffers_wait = pre_forward() if pre_forward is not None else None
-        if self.x0p is not None:
+        if self.x0p is not None and not (self.fused_conv0 and self.fused_wgrad0):  # plane kernels read x0p
             K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(L):
             z, st = self.z[i][:n], self.stats[i]
+            if i == 0 and self.fused_conv0:
+                if buffers_wait is not None:
+                    buffers_wait()
+                    buffers_wait = None
+                K.conv0_fwd(x, P[f"{l.conv_key}.weight"], z, self.part0, P[f"{l.bn_key}.weight"],
+                            P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
+                            self.buffers[f"{l.bn_key}.running_var"], self.nbt[i:i + 1], st["mean"], st["invstd"],
+                            st["scale"], st["shift"], self.bn_momentum, self.bn_eps)
+                K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
+                continue
             ns = self._conv_fwd(i, x, n, reduce=False)
             if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
                 buffers_wait()
@@ -648,10 +664,13 @@ class VGGEngine:
             raise RuntimeError("call begin_eval() after the last parameter update")
         n = x.shape[0]
         P = self.params
-        if self.x0p is not None:
+        if self.x0p is not None and not self.fused_conv0:
             self.K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(self.spec.convs):
-            self._conv_fwd(i, x, n, reduce=True)
+            if i == 0 and self.fused_conv0:
+                self.K.conv0_fwd(x, P[f"{l.conv_key}.weight"], self.z[0][:n])
+            else:
+                self._conv_fwd(i, x, n, reduce=True)
             self.K.bn_apply(self.z[i][:n], self._act_out(i, n), self.eval_ss[i]["scale"], self.eval_ss[i]["shift"],
                             l.pool)
         inp = self.a[-1][:n]
