@@ -185,6 +185,10 @@ def add_common_args(ap: argparse.ArgumentParser):
                         "resumable checkpoint (preemption drill for --resume)")
     g.add_argument("--no-eval", action="store_true")
     g.add_argument("--trace", action="store_true", help="emit roctx ranges (rocprofv3 --marker-trace)")
+    g.add_argument("--profile", action="store_true",
+                   help="re-run this command under rocprofv3 --kernel-trace --stats (prints the exact command; the "
+                        "program follows '--' directly)")
+    g.add_argument("--profile-dir", default="gpurun_out/prof_train")
     g.add_argument("--graph", action="store_true",
                    help="single rank: replay the training step as a captured HIP graph (graph_step.py)")
     g.add_argument("--json-metrics", default=None, help="append a JSON metrics line per epoch to this file")
@@ -273,6 +277,19 @@ def run(ctx: DistContext, mode: str, args):
     ctx.shutdown()
 
 
+def _maybe_profile(args, argv) -> Optional[int]:
+    """``--profile``: run this same command as a child under rocprofv3 (utils/benchlib.relaunch);
+    this process touches no GPU and exits with the child's code."""
+    if not getattr(args, "profile", False):
+        return None
+    import sys
+
+    from .utils import benchlib
+
+    argv = sys.argv[1:] if argv is None else list(argv)
+    return benchlib.relaunch(os.path.abspath(sys.argv[0]), argv, 1, True, args.profile_dir, 0)
+
+
 def main_cli(mode: str, argv=None):
     """``python main_{gather,all_reduce,part3}.py --master-ip IP --num-nodes N --rank R``"""
     ap = argparse.ArgumentParser(prog="Input arguments", description="gather ip, nunber of workers, rank")
@@ -281,6 +298,9 @@ def main_cli(mode: str, argv=None):
     ap.add_argument("--rank", required=True, type=int)
     add_common_args(ap)
     args = ap.parse_args(argv)
+    rc = _maybe_profile(args, argv)
+    if rc is not None:
+        raise SystemExit(rc)
     ctx = init_cli(args.master_ip, args.num_nodes, args.rank, port=args.port, device=args.device, comm=args.comm)
     run(ctx, mode, args)
 
@@ -290,6 +310,9 @@ def main_env(mode: str = "ddp", argv=None):
     ap = argparse.ArgumentParser(prog="Input arguments", description="gather ip, nunber of workers, rank")
     add_common_args(ap)
     args = ap.parse_args(argv)
+    rc = _maybe_profile(args, argv)
+    if rc is not None:
+        raise SystemExit(rc)
     print(f"[{os.getpid()}] Initializing process group with: {env_dict()}", flush=True)
     ctx = init_env(device=args.device, comm=args.comm)
     run(ctx, mode, args)
@@ -300,5 +323,8 @@ def main_single(argv=None):
     ap = argparse.ArgumentParser(prog="main.py")
     add_common_args(ap)
     args = ap.parse_args(argv)
+    rc = _maybe_profile(args, argv)
+    if rc is not None:
+        raise SystemExit(rc)
     ctx = init_single(args.device)
     run(ctx, "allreduce", args)
