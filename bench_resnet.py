@@ -17,7 +17,6 @@ import os
 import sys
 
 import torch
-import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -62,7 +61,7 @@ def main(argv=None):
 
     def step():
         opt.zero_grad()
-        loss = F.cross_entropy(ddp(x), t)
+        loss = ddp(x, t)  # fused GAP + Linear + softmax-CE head (ops/functional.HeadCE)
         loss.backward()
         opt.step(ddp.finish())
         return loss

@@ -12,6 +12,8 @@ int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float m
                  int first, unsigned short* planes, long ps, int np, hipStream_t s);
 int dpa_spin(long long usec, int* done, hipStream_t s);
 int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
+int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);
+int dpa_splitk_reduce_add(const float* slabs, int splits, void* out, const void* add, long n, int bf, hipStream_t s);
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
                    int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, int posmajor,
                    hipStream_t st);
@@ -32,6 +34,11 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st);
 long dpa_wgrad0_part_floats(int N);
+int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
+int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
+           float* loss, float* acc, int N, int J, hipStream_t st);
+int dpa_head_bwd_prep(const float* dlogits, const float* gout, float* dl, float* db, int N, int J, hipStream_t st);
+int dpa_gap_bwd(const float* dfeat, void* dx, int N, int HW, int C, int xbf, hipStream_t st);
 long dpa_conv0_part_floats(int N);
 int dpa_conv0_fwd(const float* x, const float* w, int CP, float* z, float* part, int N, const float* gamma,
                   const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
@@ -148,6 +155,29 @@ void spin(int64_t usec, Tensor done) {
   need(done, "done", at::kInt);
   TORCH_CHECK(usec >= 0 && usec <= 10000000, "spin: usec out of range");
   chk(dpa_spin(usec, done.data_ptr<int>(), cur_stream()), "spin");
+}
+
+// out += add (same shape, fp32 or bf16, contiguous)
+void add_inplace(Tensor out, Tensor add) {
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && add.is_contiguous() && out.numel() == add.numel() &&
+                  out.scalar_type() == add.scalar_type(),
+              "add_inplace: matching contiguous GPU tensors expected");
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "add_inplace: fp32 or bf16");
+  chk(dpa_add_inplace(out.data_ptr(), add.data_ptr(), out.numel(), bf ? 1 : 0, cur_stream()), "add_inplace");
+}
+
+// out = sum of `splits` fp32 slabs (slab[0 : splits * out.numel()]) + add
+void splitk_reduce_add(Tensor slab, int64_t splits, Tensor out, Tensor add) {
+  need(slab, "slab");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && add.is_contiguous() && out.numel() == add.numel() &&
+                  out.scalar_type() == add.scalar_type(),
+              "splitk_reduce_add: out / add mismatch");
+  TORCH_CHECK(slab.numel() >= splits * out.numel(), "splitk_reduce_add: slab too small");
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  chk(dpa_splitk_reduce_add(fp(slab), (int)splits, out.data_ptr(), add.data_ptr(), out.numel(), bf ? 1 : 0,
+                            cur_stream()),
+      "splitk_reduce_add");
 }
 
 void mean_of_w(Tensor in, Tensor out, int64_t W) {
@@ -487,6 +517,57 @@ void conv0_fwd(Tensor x, Tensor w, Tensor z, OptT part, OptT gamma, OptT beta, O
       "conv0_fwd");
 }
 
+// ---------------- generic classifier head (head.hip) ----------------
+// x [N,H,W,C] (bf16 or fp32) -> feat [N,C] fp32 (spatial mean)
+void gap(Tensor x, Tensor feat) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "gap: contiguous NHWC GPU tensor expected");
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "gap: x must be bf16 or fp32");
+  need(feat, "feat");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(feat.numel() == (int64_t)N * C, "gap: feat [N,C]");
+  chk(dpa_gap(x.data_ptr(), fp(feat), N, HW, C, bf ? 1 : 0, cur_stream()), "gap");
+}
+
+// logits [N,J] fp32, target [N] int64 -> loss_row [N], optional dlogits [N,J] = (softmax - onehot)/N,
+// optional correct_row [N] int32, loss [1] = batch mean, acc [2] += (loss, #correct)
+void softmax_ce(Tensor logits, Tensor target, Tensor loss_row, OptT dlogits, OptT correct_row, OptT loss, OptT acc) {
+  need(logits, "logits");
+  need(loss_row, "loss_row");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == at::kLong && target.is_contiguous(), "target int64");
+  const int N = logits.size(0), J = logits.size(1);
+  TORCH_CHECK(target.numel() == N && loss_row.numel() >= N, "softmax_ce: sizes");
+  int* cr = nullptr;
+  if (correct_row.has_value() && correct_row->defined()) {
+    TORCH_CHECK(correct_row->scalar_type() == at::kInt && correct_row->numel() >= N, "correct_row int32 [N]");
+    cr = correct_row->data_ptr<int>();
+  }
+  if (dlogits.has_value() && dlogits->defined()) TORCH_CHECK(dlogits->numel() == (int64_t)N * J, "dlogits [N,J]");
+  chk(dpa_ce(fp(logits), reinterpret_cast<const long long*>(target.data_ptr<int64_t>()), fp(loss_row), ofp(dlogits),
+             cr, ofp(loss), ofp(acc), N, J, cur_stream()),
+      "softmax_ce");
+}
+
+void head_bwd_prep(Tensor dlogits, Tensor gout, Tensor dl, Tensor db) {
+  need(dlogits, "dlogits");
+  need(gout, "gout");
+  need(dl, "dl");
+  need(db, "db");
+  const int N = dlogits.size(0), J = dlogits.size(1);
+  TORCH_CHECK(dl.numel() == dlogits.numel() && db.numel() == J && gout.numel() >= 1, "head_bwd_prep: sizes");
+  chk(dpa_head_bwd_prep(fp(dlogits), fp(gout), fp(dl), fp(db), N, J, cur_stream()), "head_bwd_prep");
+}
+
+void gap_bwd(Tensor dfeat, Tensor dx) {
+  need(dfeat, "dfeat");
+  TORCH_CHECK(dx.is_cuda() && dx.is_contiguous() && dx.dim() == 4, "gap_bwd: dx NHWC");
+  const bool bf = dx.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || dx.scalar_type() == at::kFloat, "gap_bwd: dx bf16 or fp32");
+  const int N = dx.size(0), HW = dx.size(1) * dx.size(2), C = dx.size(3);
+  TORCH_CHECK(dfeat.numel() == (int64_t)N * C, "gap_bwd: dfeat [N,C]");
+  chk(dpa_gap_bwd(fp(dfeat), dx.data_ptr(), N, HW, C, bf ? 1 : 0, cur_stream()), "gap_bwd");
+}
+
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
             int64_t act, OptT res, OptT dres) {
@@ -720,6 +801,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("planes") = py::none());
   m.def("spin", &spin, py::arg("usec"), py::arg("done"));
   m.def("mean_of_w", &mean_of_w);
+  m.def("add_inplace", &add_inplace);
+  m.def("splitk_reduce_add", &splitk_reduce_add);
   m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("dgrad") = false, py::arg("reduce") = true,
         py::arg("posmajor") = false);
@@ -748,6 +831,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none());
   m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0);
+  m.def("gap", &gap);
+  m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("target"), py::arg("loss_row"),
+        py::arg("dlogits") = py::none(), py::arg("correct_row") = py::none(), py::arg("loss") = py::none(),
+        py::arg("acc") = py::none());
+  m.def("head_bwd_prep", &head_bwd_prep);
+  m.def("gap_bwd", &gap_bwd);
   m.def("conv0_fwd", &conv0_fwd, py::arg("x"), py::arg("w"), py::arg("z"), py::arg("part") = py::none(),
         py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("bias") = py::none(),
         py::arg("rmean") = py::none(), py::arg("rvar") = py::none(), py::arg("nbt") = py::none(),

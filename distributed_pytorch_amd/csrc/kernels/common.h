@@ -68,9 +68,17 @@ __device__ __forceinline__ void st_out4(float4* o, long i, float4 v) { o[i] = v;
 __device__ __forceinline__ void st_out4(ushort4* o, long i, float4 v) {
   o[i] = make_ushort4(bf16_rne(v.x), bf16_rne(v.y), bf16_rne(v.z), bf16_rne(v.w));
 }
+__device__ __forceinline__ float4 ld_add4(const float4* a, long i) { return a[i]; }
+__device__ __forceinline__ float4 ld_add4(const ushort4* a, long i) {
+  const ushort4 h = a[i];
+  return make_float4(bf16_f(h.x), bf16_f(h.y), bf16_f(h.z), bf16_f(h.w));
+}
+// add (optional, out's type): out = sum of the slabs + add -- a second gradient contribution to the
+// same tensor folded into the reduction instead of a separate elementwise pass
 template <int G, typename TO>
 __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __restrict__ slabs,
-                                                               TO* __restrict__ out, long n4, int splits) {
+                                                               TO* __restrict__ out, long n4, int splits,
+                                                               const TO* __restrict__ add) {
   __shared__ float4 part[G > 1 ? G : 1][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const long i = (long)blockIdx.x * 64 + c;
@@ -85,35 +93,42 @@ __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __r
       s.w += v.w;
     }
   }
-  if constexpr (G == 1) {
-    if (i < n4) st_out4(out, i, s);
-  } else {
+  if constexpr (G > 1) {
     part[g][c] = s;
     __syncthreads();
-    if (g == 0 && i < n4) {
+    if (g != 0) return;
 #pragma unroll
-      for (int j = 1; j < G; ++j) {
-        s.x += part[j][c].x;
-        s.y += part[j][c].y;
-        s.z += part[j][c].z;
-        s.w += part[j][c].w;
-      }
-      st_out4(out, i, s);
+    for (int j = 1; j < G; ++j) {
+      s.x += part[j][c].x;
+      s.y += part[j][c].y;
+      s.z += part[j][c].z;
+      s.w += part[j][c].w;
     }
+  }
+  if (i < n4) {
+    if (add) {
+      const float4 a = ld_add4(add, i);
+      s.x += a.x;
+      s.y += a.y;
+      s.z += a.z;
+      s.w += a.w;
+    }
+    st_out4(out, i, s);
   }
 }
 
-// out: float4 (fp32) or ushort4 (bf16, round-to-nearest-even)
+// out: float4 (fp32) or ushort4 (bf16, round-to-nearest-even); add: optional addend of out's type
 template <typename TO>
-inline int launch_splitk_reduce_t(const float* slabs, TO* o4, long n4, int splits, hipStream_t st) {
+inline int launch_splitk_reduce_t(const float* slabs, TO* o4, long n4, int splits, hipStream_t st,
+                                  const TO* add = nullptr) {
   const long blocks = (n4 + 63) / 64;
   const float4* in4 = reinterpret_cast<const float4*>(slabs);
   if (splits >= 16 && blocks < 4096)
-    splitk_reduce_kernel<16, TO><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits);
+    splitk_reduce_kernel<16, TO><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits, add);
   else if (splits >= 4 && blocks < 16384)
-    splitk_reduce_kernel<4, TO><<<blocks, 256, 0, st>>>(in4, o4, n4, splits);
+    splitk_reduce_kernel<4, TO><<<blocks, 256, 0, st>>>(in4, o4, n4, splits, add);
   else
-    splitk_reduce_kernel<1, TO><<<blocks, 64, 0, st>>>(in4, o4, n4, splits);
+    splitk_reduce_kernel<1, TO><<<blocks, 64, 0, st>>>(in4, o4, n4, splits, add);
   return (int)hipGetLastError();
 }
 inline int launch_splitk_reduce(const float* slabs, float* out, long n4, int splits, hipStream_t st) {

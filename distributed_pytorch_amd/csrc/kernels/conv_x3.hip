@@ -1161,7 +1161,7 @@ template <bool DG>
 int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st) {
   const int BM = halo_bm(tile), BC = halo_bc(tile);
   if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM) - 1) return -6;
-  if (obf && (np != 1 || (splits > 1 && !reduce))) return -4;
+  if (obf && np != 1) return -4;  // bf16 output from one-plane operands (unreduced slabs stay fp32)
   a.M = a.N * a.H * a.W;
   a.gm = cdiv(a.M, BM);
   a.gn = cdiv(a.Nout, halo_bn(tile));
@@ -1259,7 +1259,7 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   a.gn = cdiv(Kout, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor ? 1 : 0;
-  if (obf && (np != 1 || (a.splits > 1 && !reduce))) return -4;
+  if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;
   a.slab = a.splits > 1 ? (long)a.M * Kout : 0;
@@ -1315,7 +1315,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   a.gn = cdiv(C, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor ? 1 : 0;
-  if (obf && (np != 1 || (a.splits > 1 && !reduce))) return -4;
+  if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)dx;
   a.outb = (u16*)dx;
   a.slab = a.splits > 1 ? (long)a.M * C : 0;

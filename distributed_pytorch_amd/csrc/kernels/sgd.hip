@@ -90,3 +90,32 @@ extern "C" int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStre
   mean_of_w_kernel<<<grid_for(n, 256), 256, 0, s>>>(in, out, n, W);
   return (int)hipGetLastError();
 }
+
+// out += add over float4 / bf16x4 groups (a gradient contribution joined where it cannot be folded
+// into a producing kernel, ops/functional.GradJoin)
+template <typename T>
+__global__ __launch_bounds__(256) void add_inplace_kernel(T* __restrict__ out, const T* __restrict__ add, long n4) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 a = ld_add4(add, i), o = ld_add4(out, i);
+    st_out4(out, i, make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w));
+  }
+}
+
+extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s) {
+  if (n % 4) return -1;
+  const long n4 = n / 4;
+  if (bf)
+    add_inplace_kernel<ushort4><<<grid_for(n4, 256), 256, 0, s>>>((ushort4*)out, (const ushort4*)add, n4);
+  else
+    add_inplace_kernel<float4><<<grid_for(n4, 256), 256, 0, s>>>((float4*)out, (const float4*)add, n4);
+  return (int)hipGetLastError();
+}
+
+// out = sum of `splits` fp32 slabs of out's size + add (fp32 or bf16 out / add)
+extern "C" int dpa_splitk_reduce_add(const float* slabs, int splits, void* out, const void* add, long n, int bf,
+                                     hipStream_t s) {
+  if (n % 4) return -1;
+  if (bf) return launch_splitk_reduce_t(slabs, (ushort4*)out, n / 4, splits, s, (const ushort4*)add);
+  return launch_splitk_reduce_t(slabs, (float4*)out, n / 4, splits, s, (const float4*)add);
+}

@@ -3,7 +3,9 @@
 
 ``ResNet`` is built from the NHWC kernel layers (ops/layers.py): every conv runs the gfx950
 implicit-GEMM kernels (bf16 MFMA, or x3 fp32-grade), every BatchNorm is fused with its ReLU /
-residual-add+ReLU, stem max-pool / global average pool / FC head use torch ops (minor).
+residual-add+ReLU, the stem max-pool is the native NHWC pool, and the head (global average pool +
+Linear + softmax-CE) is one autograd node over head.hip + two hipBLASLt GEMMs
+(``model(x, target)`` returns the loss; ``model(x)`` the logits).
 Parameter / buffer names and shapes (state_dict) match torchvision's ``resnet50`` so checkpoints
 interchange.  ``ResNetRef`` is the same network from stock torch NCHW modules: the numerics
 oracle for tests.
@@ -16,6 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import functional as Fn
 from ..ops.layers import BatchNorm2d, Conv2d, MaxPool2d
 
 LAYERS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3], "resnet152": [3, 8, 36, 3]}
@@ -35,12 +38,19 @@ class Bottleneck(nn.Module):
         self.bn3 = BatchNorm2d(cout, "add_relu")
         self.downsample = (nn.Sequential(Conv2d(cin, cout, 1, stride, 0, impl), BatchNorm2d(cout, "none"))
                            if downsample else None)
+        # x's gradient has two contributions (conv1, and the identity or the downsample conv): they
+        # are summed inside the last one's data-gradient reduction instead of by autograd (GradJoin)
+        self._join = Fn.GradJoin(2)
 
     def forward(self, x):
-        out = self.bn1(self.conv1(x))
+        j = self._join if (self.training and torch.is_grad_enabled() and x.requires_grad) else None
+        if j is not None:
+            j.reset()
+        out = self.bn1(self.conv1(x, j))
         out = self.bn2(self.conv2(out))
-        identity = self.downsample[1](self.downsample[0](x)) if self.downsample is not None else x
-        return self.bn3(self.conv3(out), identity)
+        if self.downsample is not None:
+            return self.bn3(self.conv3(out), self.downsample[1](self.downsample[0](x, j)))
+        return self.bn3(self.conv3(out), x, res_join=j)
 
 
 class ResNet(nn.Module):
@@ -62,6 +72,7 @@ class ResNet(nn.Module):
                 cin = width * 4
             setattr(self, f"layer{li + 1}", nn.Sequential(*blocks))
         self.fc = nn.Linear(cin, num_classes)
+        self.fc.weight._dpa_direct = self.fc.bias._dpa_direct = True  # the head writes their optimizer slots
         self._init()
 
     def _init(self):
@@ -74,10 +85,16 @@ class ResNet(nn.Module):
                     m.weight.zero_()
                     m.weight[..., :m.cin].copy_(w.permute(0, 2, 3, 1))
 
-    def forward(self, x):
+    def features(self, x):
         x = self.maxpool(self.bn1(self.conv1(x)))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        return self.fc(x.to(self.fc.weight.dtype).mean(dim=(1, 2)))
+        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+
+    def forward(self, x, target=None):
+        """Logits, or with ``target`` the batch-mean cross-entropy through the fused head."""
+        f = self.features(x)
+        if target is not None:
+            return Fn.head_ce(f, self.fc.weight, self.fc.bias, target)
+        return Fn.head_logits(f, self.fc.weight, self.fc.bias)
 
 
 def resnet50(num_classes: int = 1000, impl: str = "bf16") -> ResNet:

@@ -224,23 +224,90 @@ def conv_config(kind: str, M: int, Ngemm: int, Kred: int, hw_small: bool) -> Tup
     return c
 
 
+class GradJoin:
+    """Joins the gradient contributions of several autograd nodes to ONE tensor without an
+    elementwise add pass.  In a ResNet bottleneck the block input x feeds conv1 and the residual
+    (the identity into bn3's add+ReLU, or the downsample conv): autograd would sum their gradients
+    with an extra read-read-write pass over x's gradient.  Instead every contributor calls
+    ``contribute``: all but the last stash their gradient and hand autograd None (a zero
+    contribution, nothing to add); the last one folds the stash into its own output — inside the
+    data-gradient split-K reduction when its conv splits K (``splitk_reduce_add``), else with one
+    in-place add — and returns the sum.  Order-independent; ``reset()`` at every forward."""
+
+    __slots__ = ("n", "left", "buf")
+
+    def __init__(self, n: int):
+        self.n = n
+        self.reset()
+
+    def reset(self):
+        self.left, self.buf = self.n, None
+
+    def last(self) -> bool:
+        return self.left == 1
+
+    def stash(self, g: torch.Tensor) -> None:
+        if self.buf is None:
+            self.buf = g
+        elif _native(g):
+            _ext.require().add_inplace(self.buf, g.contiguous())
+        else:
+            self.buf = self.buf + g
+        self.left -= 1
+
+    def take(self) -> Optional[torch.Tensor]:
+        """For the last contributor: the stashed sum (None if nothing was stashed); resets."""
+        b = self.buf
+        self.reset()
+        return b
+
+    def contribute(self, g: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """A contributor whose gradient is already materialised: stash it (returns None), or as the
+        last one return it plus the stash."""
+        if g is None:
+            self.left -= 1
+            return None if self.left > 0 else self.take()
+        if not self.last():
+            self.stash(g)
+            return None
+        b = self.take()
+        if b is None:
+            return g
+        if _native(g):
+            _ext.require().add_inplace(g, b.contiguous())
+            return g
+        return g + b
+
+
 class Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, impl: str):
-        N, H, W, C = x.shape
-        K, R, S, _ = w.shape
+    def forward(ctx, x, w, stride: int, pad: int, impl: str, join: Optional[GradJoin] = None):
+        N, H, W, Cx = x.shape
+        K, R, S, C = w.shape  # C: the weight's (padded) input channels; x may carry fewer (network input)
         P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
         ctx.geom = (N, H, W, C, K, R, S, stride, pad, P, Q)
         ctx.impl = impl
         ctx.w_param = w
+        ctx.cx = Cx
+        ctx.join = join
         note_use(w)
         if not _native(x):
+            if Cx != C:
+                x = F.pad(x, (0, C - Cx))
             z = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
             ctx.save_for_backward(x, w)
             return z.permute(0, 2, 3, 1).contiguous()
         Kx = _ext.require()
         np_ = NPLANES[impl]
-        xp, wp = split_planes(x, np_), weight_planes(w, np_)
+        if Cx != C:
+            # channel padding happens in the plane split (pad_split8): no padded fp32 copy of the input
+            if C != 8 or Cx > 8:
+                raise ValueError(f"conv2d_nhwc: input has {Cx} channels, weight {C} (only padding to 8 is fused)")
+            xp = torch.empty(np_, N, H, W, 8, device=x.device, dtype=torch.bfloat16)
+            Kx.pad_split8(x.float().contiguous(), xp)
+        else:
+            xp = split_planes(x, np_)
+        wp = weight_planes(w, np_)
         act_dtype = torch.bfloat16 if np_ == 1 else torch.float32
         ctx.x_dtype = x.dtype if np_ == 3 else torch.bfloat16
         z = torch.empty(N, P, Q, K, device=x.device, dtype=act_dtype)
@@ -269,28 +336,43 @@ class Conv2dNHWC(torch.autograd.Function):
             dzn = dz.permute(0, 3, 1, 2)
             if ctx.needs_input_grad[0]:
                 dx = torch.nn.grad.conv2d_input(xn.shape, wn, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
+                if ctx.cx != C:
+                    dx = dx[..., :ctx.cx]
             if ctx.needs_input_grad[1]:
                 dw = torch.nn.grad.conv2d_weight(xn, wn.shape, dzn, stride=stride, padding=pad).permute(0, 2, 3, 1)
                 slot = grad_slot(ctx.w_param)
                 if slot is not None:
                     dw = slot.copy_(dw)
-            return dx, dw, None, None, None
+            if ctx.join is not None and ctx.needs_input_grad[0]:
+                dx = ctx.join.contribute(dx.contiguous())
+            return dx, dw, None, None, None, None
         Kx = _ext.require()
         xp, wp = a, b
         np_ = xp.shape[0]
         if np_ == 1 and dz.dtype != torch.bfloat16:
             dz = dz.to(torch.bfloat16)
         dzp = split_planes(dz, np_)
+        join = ctx.join
         if ctx.needs_input_grad[0]:
             dx = torch.empty(N, H, W, C, device=dz.device, dtype=ctx.x_dtype)
+            # last contributor of a GradJoin: the stashed gradient is folded into this data gradient
+            addend = join.take() if (join is not None and join.last() and ctx.cx == C) else None
 
-            def run_d(tile, s, pm):
+            def run_d(tile, s, pm, add=None):
                 slab = WS.get("slab", s * N * H * W * C, dz.device) if s > 1 else None
-                Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm)
+                if add is None:
+                    Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm)
+                    return
+                Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, s == 1, pm)
+                if s > 1:
+                    Kx.splitk_reduce_add(slab, s, dx, add)  # dx = sum of slabs + stash, one pass
+                else:
+                    Kx.add_inplace(dx, add)
 
             cfg = choose_config(ctx.impl, "dgrad", geom, N * H * W, C, R * S * K, H * W <= 16, run_d,
                                 lambda s: 4 * s * N * H * W * C)
-            run_d(cfg[0], Kx.x3_splits(R * S * K, cfg[1]), cfg[2])
+            run_d(cfg[0], Kx.x3_splits(R * S * K, cfg[1]), cfg[2],
+                  addend.to(dx.dtype).contiguous() if addend is not None else None)
         if ctx.needs_input_grad[1]:
             dw = grad_slot(ctx.w_param)
             if dw is None:
@@ -303,18 +385,26 @@ class Conv2dNHWC(torch.autograd.Function):
             cfg = choose_config(ctx.impl, "wgrad", geom, N * P * Q, K, R * S * C, P * Q <= 16, run_w,
                                 lambda s: 4 * s * K * R * S * C)
             run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
-        return dx, dw, None, None, None
+        if dx is not None and ctx.cx != C:
+            dx = dx[..., :ctx.cx].contiguous()
+        if join is not None and dx is not None and addend is None:
+            dx = join.contribute(dx)  # not last (stash; autograd gets None), or a sliced input
+        return dx, dw, None, None, None, None
 
 
-def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, impl: str = "bf16"):
+def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, impl: str = "bf16",
+                join: Optional[GradJoin] = None):
+    """``join``: x's gradient is one of several contributions (GradJoin) to be summed without an
+    extra pass."""
     if impl not in NPLANES:
         raise ValueError(f"impl must be one of {list(NPLANES)}")
-    return Conv2dNHWC.apply(x.contiguous(), w, int(stride), int(pad), impl)
+    return Conv2dNHWC.apply(x.contiguous(), w, int(stride), int(pad), impl, join)
 
 
 class BnActNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z, gamma, beta, res, rmean, rvar, nbt, training: bool, momentum: float, eps: float, act: int):
+    def forward(ctx, z, gamma, beta, res, rmean, rvar, nbt, training: bool, momentum: float, eps: float, act: int,
+                res_join: Optional[GradJoin] = None):
         N, H, W, C = z.shape
         dev = z.device
         K = _ext.require() if _native(z) else cpu_ref
@@ -330,6 +420,7 @@ class BnActNHWC(torch.autograd.Function):
         a = torch.empty_like(z)
         K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None)
         ctx.act, ctx.training = act, training
+        ctx.res_join = res_join
         ctx.params = (gamma, beta)
         if training:
             note_use(gamma)
@@ -358,17 +449,23 @@ class BnActNHWC(torch.autograd.Function):
         coef = torch.empty(3 * C, **f32)
         K.bn_bwd(da, 1, da, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, None, dz, False, ctx.act,
                  res, dres)
-        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        if ctx.res_join is not None and dres is not None:
+            dres = ctx.res_join.contribute(dres)
+        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, training: bool = True,
-                momentum: float = 0.1, eps: float = 1e-5, act: str = "relu", residual: Optional[torch.Tensor] = None):
+                momentum: float = 0.1, eps: float = 1e-5, act: str = "relu", residual: Optional[torch.Tensor] = None,
+                res_join: Optional[GradJoin] = None):
+    """``res_join``: the residual's gradient is one contribution of a GradJoin (ResNet identity)."""
     a = ACT[act]
     if a == 2 and residual is None:
         raise ValueError("act='add_relu' needs a residual")
     res = residual.to(z.dtype).contiguous() if residual is not None else None
+    if res is not residual:
+        res_join = None  # a converted copy: its gradient flows back through the conversion, not the join
     return BnActNHWC.apply(z.contiguous(), gamma, beta, res, running_mean, running_var, num_batches_tracked,
-                           bool(training), float(momentum), float(eps), a)
+                           bool(training), float(momentum), float(eps), a, res_join)
 
 
 class MaxPoolNHWC(torch.autograd.Function):
@@ -416,3 +513,112 @@ def kaiming_uniform_krsc(K: int, R: int, S: int, C: int, c_true: Optional[int] =
     out = torch.zeros(K, R, S, C)
     out[..., :c_true] = w.permute(0, 2, 3, 1)
     return out
+
+
+# ------------------------------------------------------------------ classifier head
+def _head_fwd(x, weight, bias):
+    """feat = GAP(x) fp32 [N,C] (head.hip), logits = feat @ W^T + b (hipBLASLt)."""
+    if not _native(x):
+        feat = x.to(weight.dtype).mean(dim=(1, 2))
+    else:
+        feat = torch.empty(x.shape[0], x.shape[-1], device=x.device, dtype=torch.float32)
+        _ext.require().gap(x, feat)
+    return feat, torch.addmm(bias, feat, weight.t())
+
+
+def _head_bwd(dlogits, gscale, feat, weight, wparam, bparam, shape, dtype):
+    """Gradients of GAP + Linear from dlogits * gscale (gscale: 1-element device tensor): db and dW
+    straight into the optimizer arena when the DDP wrapper offers slots."""
+    N, H, W, C = shape
+    if not _native(feat):
+        dl = dlogits * gscale
+        dfeat = dl @ weight
+        dx = (dfeat / (H * W))[:, None, None, :].expand(N, H, W, C).to(dtype).contiguous()
+        dw, db = dl.t() @ feat, dl.sum(0)
+        sw, sb = grad_slot(wparam), grad_slot(bparam)
+        if sw is not None:
+            dw = sw.copy_(dw)
+        if sb is not None:
+            db = sb.copy_(db)
+        return dx, dw, db
+    K = _ext.require()
+    dev = feat.device
+    dl = torch.empty_like(dlogits)
+    db = grad_slot(bparam)
+    if db is None:
+        db = torch.empty(weight.shape[0], device=dev, dtype=torch.float32)
+    K.head_bwd_prep(dlogits, gscale, dl, db)  # dl = dlogits * g, db = column sums (fixed order)
+    dfeat = torch.mm(dl, weight)
+    dw = grad_slot(wparam)
+    if dw is None:
+        dw = torch.empty_like(weight)
+    torch.mm(dl.t(), feat, out=dw)
+    dx = torch.empty(shape, device=dev, dtype=dtype)
+    K.gap_bwd(dfeat, dx)
+    return dx, dw, db
+
+
+class HeadLinear(torch.autograd.Function):
+    """logits = Linear(GAP(x)): global average pool (head.hip) + hipBLASLt GEMM, one autograd node."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        note_use(weight)
+        note_use(bias)
+        feat, logits = _head_fwd(x, weight, bias)
+        ctx.save_for_backward(feat, weight)
+        ctx.w_b, ctx.x_meta = (weight, bias), (x.shape, x.dtype)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        feat, weight = ctx.saved_tensors
+        one = torch.ones(1, device=feat.device, dtype=feat.dtype)
+        dx, dw, db = _head_bwd(dlogits.contiguous().to(feat.dtype), one, feat, weight, *ctx.w_b, *ctx.x_meta)
+        return dx, dw, db
+
+
+class HeadCE(torch.autograd.Function):
+    """Global average pool + Linear + softmax cross-entropy (mean) in one autograd node
+    (csrc/kernels/head.hip; the two GEMMs are plain hipBLASLt GEMMs through torch.mm).  The loss
+    gradient is formed in the forward (as the VGG head does, fc_ce.hip); the backward scales it by
+    the incoming gradient, reduces the bias gradient, and writes weight / bias gradients straight
+    into the optimizer arena when the DDP wrapper offers a slot (``grad_slot``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, target):
+        N = x.shape[0]
+        note_use(weight)
+        note_use(bias)
+        feat, logits = _head_fwd(x, weight, bias)
+        if not _native(x):
+            loss = F.cross_entropy(logits, target)
+            p = torch.softmax(logits, 1)
+            p[torch.arange(N), target] -= 1.0
+            dlogits = p / N
+        else:
+            dev = x.device
+            loss_row = torch.empty(N, device=dev, dtype=torch.float32)
+            dlogits = torch.empty_like(logits)
+            loss = torch.empty((), device=dev, dtype=torch.float32)
+            _ext.require().softmax_ce(logits, target, loss_row, dlogits, None, loss.view(1), None)
+        ctx.save_for_backward(feat, dlogits, weight)
+        ctx.w_b, ctx.x_meta = (weight, bias), (x.shape, x.dtype)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        feat, dlogits, weight = ctx.saved_tensors
+        g = gloss.reshape(1).to(dtype=feat.dtype).contiguous()
+        dx, dw, db = _head_bwd(dlogits, g, feat, weight, *ctx.w_b, *ctx.x_meta)
+        return dx, dw, db, None
+
+
+def head_ce(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Batch-mean cross-entropy of Linear(GAP(x)) (x NHWC bf16/fp32; weight [J,C], bias [J] fp32)."""
+    return HeadCE.apply(x.contiguous(), weight, bias, target.contiguous())
+
+
+def head_logits(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """Linear(GAP(x)) logits, differentiable (for callers that apply their own loss)."""
+    return HeadLinear.apply(x.contiguous(), weight, bias)

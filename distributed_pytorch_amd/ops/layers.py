@@ -28,10 +28,10 @@ class Conv2d(nn.Module):
         self._register_state_dict_hook(Conv2d._to_oihw)
         self._register_load_state_dict_pre_hook(self._from_oihw)
 
-    def forward(self, x):
-        if x.shape[-1] != self.cin_pad:  # network input: zero-pad channels to the operand granularity
-            x = torch.nn.functional.pad(x, (0, self.cin_pad - x.shape[-1]))
-        return Fn.conv2d_nhwc(x, self.weight, self.stride, self.padding, self.impl)
+    def forward(self, x, join=None):
+        # a network input with fewer channels than cin_pad is zero-padded inside the op (on GPU in
+        # the bf16 plane split, pad_split8: no padded copy of the input)
+        return Fn.conv2d_nhwc(x, self.weight, self.stride, self.padding, self.impl, join)
 
     @staticmethod
     def _to_oihw(module, sd, prefix, local_metadata):
@@ -66,10 +66,10 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
-    def forward(self, z, residual=None):
+    def forward(self, z, residual=None, res_join=None):
         nbt = self.num_batches_tracked.view(1) if self.training else None
         return Fn.bn_act_nhwc(z, self.weight, self.bias, self.running_mean, self.running_var, nbt, self.training,
-                              self.momentum, self.eps, self.act, residual)
+                              self.momentum, self.eps, self.act, residual, res_join)
 
     def extra_repr(self):
         return f"{self.c}, act={self.act}"

@@ -151,6 +151,7 @@ class DistributedDataParallel(nn.Module):
     def _reset(self):
         self._pending = [len(b) for b in self._buckets]
         self._issued = [False] * len(self._buckets)
+        self._seen = [False] * len(self._params)
 
     def _send_buffers(self):
         with self.comm.region():
@@ -173,6 +174,7 @@ class DistributedDataParallel(nn.Module):
     # ---------------------------------------------------------------- gradient buckets
     def _make_hook(self, i: int):
         def hook(p):
+            self._seen[i] = True
             if self._direct[i]:
                 # a parameter used more than once in the forward gets its gradient summed by
                 # autograd into a fresh tensor: move it into the arena slot the collectives and the
@@ -215,6 +217,10 @@ class DistributedDataParallel(nn.Module):
     def finish(self) -> float:
         """After backward: issue what is left, order the compute stream after the collectives and
         return the gradient scale (1/W) for the optimizer."""
+        for i, (p, d) in enumerate(zip(self._params, self._direct)):
+            if d and not self._seen[i]:  # a slot-written parameter that got no gradient this step
+                with torch.no_grad():
+                    self._gflat.view(i, p).zero_()
         for b in range(len(self._buckets)):
             if not self._issued[b]:
                 self._issue(b)
@@ -223,10 +229,15 @@ class DistributedDataParallel(nn.Module):
         return 1.0 / self.world
 
     def zero_grad(self, set_to_none: bool = False):
-        self._gflat.flat.zero_()
-        for p, d in zip(self._params, self._direct):
-            if d:
-                p.grad = None  # backward hands autograd the arena view again
+        """Parameters whose backward writes their arena slot (``_dpa_direct``: every conv / BN / head
+        parameter of the kernel layers) need no memset -- the slot is overwritten, and finish() zeroes
+        the slot of any that got no gradient; the others accumulate into their view, which is zeroed."""
+        with torch.no_grad():
+            for i, (p, d) in enumerate(zip(self._params, self._direct)):
+                if d:
+                    p.grad = None  # backward hands autograd the arena view again
+                else:
+                    self._gflat.view(i, p).zero_()
 
     @property
     def flat_params(self) -> torch.Tensor:

@@ -103,3 +103,35 @@ def test_ddp_arena_holds_gradient_of_a_weight_used_twice():
             arena = ddp._gflat.view(i, po[n])
             assert torch.allclose(arena, p.grad, rtol=1e-10, atol=1e-12), (it, n)
             assert torch.allclose(po[n].grad, p.grad, rtol=1e-10, atol=1e-12), (it, n)
+
+
+def test_fused_head_loss_matches_reference():
+    """model(x, target): GAP + Linear + softmax-CE in one node (ops/functional.HeadCE) == stock
+    cross_entropy on the reference network, loss and every gradient (float64)."""
+    ours, ref = _pair([1, 1, 1, 1])
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(3, 3, 40, 40, generator=g, dtype=torch.float64)
+    t = torch.randint(0, 10, (3,), generator=g)
+    lo = ours(x.permute(0, 2, 3, 1).contiguous(), t)
+    lr = torch.nn.functional.cross_entropy(ref(x), t)
+    assert torch.allclose(lo, lr, rtol=1e-10, atol=1e-12)
+    (2.5 * lo).backward()
+    (2.5 * lr).backward()
+    po = dict(ours.named_parameters())
+    for name, p in ref.named_parameters():
+        q = po[name].grad
+        if q.dim() == 4:
+            q = q[..., :p.shape[1]].permute(0, 3, 1, 2)
+        err = (q - p.grad).abs().max() / p.grad.abs().max().clamp_min(1e-12)
+        assert err < 1e-8, (name, float(err))
+
+
+def test_gradjoin_order_independent():
+    from distributed_pytorch_amd.ops.functional import GradJoin
+
+    a, b = torch.randn(5), torch.randn(5)
+    for first, second in ((a, b), (b, a)):
+        j = GradJoin(2)
+        assert j.contribute(first.clone()) is None
+        assert torch.allclose(j.contribute(second.clone()), a + b)
+        assert j.left == 2 and j.buf is None  # reset for the next step
