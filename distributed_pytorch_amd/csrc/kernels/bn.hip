@@ -844,6 +844,7 @@ __global__ __launch_bounds__(1024) void wgrad0_reduce_kernel(const float* __rest
   }
 }
 
+
 template <typename TZ>
 int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
@@ -956,4 +957,5 @@ int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, c
   wgrad0_reduce_kernel<<<64, 1024, 0, st>>>(wpart, nblk, 64, dw, CP);
   return (int)hipGetLastError();
 }
+
 }  // extern "C"

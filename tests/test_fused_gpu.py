@@ -148,3 +148,4 @@ def test_fused_conv0_step_and_eval_match_unfused(monkeypatch):
     assert _rel(b1, b0) < 1e-5
     assert _rel(g1, g0) < 5e-2
     assert _rel(o1, o0) < 1e-3
+

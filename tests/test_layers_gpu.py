@@ -215,26 +215,47 @@ def test_head_kernels_match_torch():
 
 
 def test_resnet_fused_loss_step_matches_reference():
-    """Small ResNet (x3) trained through model(x, target) — fused head, GradJoin residual sums,
-    channel padding in the plane split — vs the stock-torch oracle in fp64."""
-    from distributed_pytorch_amd.models.resnet import ResNet, ResNetRef
+    """Small ResNet (x3) trained through model(x, target) -- fused head, GradJoin residual sums,
+    channel padding in the plane split -- against (a) the same network through the logits head +
+    stock cross_entropy + autograd's own residual sums, which must agree to fp32 rounding, and (b) the
+    stock-torch oracle in fp64.  Against fp64 a few tensors of a random-init network sit behind a
+    ReLU whose input is ~0 at some element: fp32 rounding flips that mask bit (stock torch fp32 does
+    too), so (b) bounds the median tensor tightly and every tensor loosely."""
+    from distributed_pytorch_amd.models import resnet as R
 
     torch.manual_seed(0)
-    ours = ResNet([1, 2, 1, 1], 10, impl="x3").cuda()
-    ref = ResNetRef([1, 2, 1, 1], 10).double()
-    ref.load_state_dict({k: v.cpu() for k, v in ours.state_dict().items()})
+    base = R.ResNet([1, 2, 1, 1], 10, impl="x3")
+    sd = base.state_dict()
+    ref = R.ResNetRef([1, 2, 1, 1], 10).double()
+    ref.load_state_dict(sd)
     g = torch.Generator().manual_seed(3)
     x = torch.randn(8, 3, 64, 64, generator=g, dtype=torch.float64)
     t = torch.randint(0, 10, (8,), generator=g)
-    lo = ours(x.permute(0, 2, 3, 1).float().contiguous().cuda(), t.cuda())
     lr = F.cross_entropy(ref(x), t)
-    lo.backward()
     lr.backward()
-    torch.cuda.synchronize()
-    assert abs(lo.item() - lr.item()) < 1e-3 * max(1.0, abs(lr.item()))
-    po = dict(ours.named_parameters())
+    xin = x.permute(0, 2, 3, 1).float().contiguous().cuda()
+    grads = []
+    for fused in (True, False):
+        m = R.ResNet([1, 2, 1, 1], 10, impl="x3")
+        m.load_state_dict(sd)
+        m = m.cuda()
+        if not fused:  # logits head + stock loss, residual gradients summed by autograd
+            for blk in m.modules():
+                if isinstance(blk, R.Bottleneck):
+                    blk._join = R.Fn.GradJoin(2)
+                    blk._join.contribute = lambda gr: gr  # every contribution goes to autograd
+        lo = m(xin, t.cuda()) if fused else F.cross_entropy(m(xin), t.cuda())
+        lo.backward()
+        torch.cuda.synchronize()
+        assert abs(lo.item() - lr.item()) < 1e-4 * max(1.0, abs(lr.item()))
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    errs = []
     for name, p in ref.named_parameters():
-        q = po[name].grad
-        if q.dim() == 4:
-            q = q[..., :p.shape[1]].permute(0, 3, 1, 2)
-        assert rel(q, p.grad) < 2e-2, name
+        a, b = grads[0][name], grads[1][name]
+        assert rel(a, b) < 1e-5, name
+        q = a[..., :p.shape[1]].permute(0, 3, 1, 2) if a.dim() == 4 else a
+        e = rel(q, p.grad)
+        assert e < 0.2, name
+        errs.append(e)
+    errs.sort()
+    assert errs[len(errs) // 2] < 5e-3, errs
