@@ -13,7 +13,6 @@ int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float m
 int dpa_spin(long long usec, int* done, hipStream_t s);
 int dpa_mean_of_w(const float* in, float* out, long n, int W, hipStream_t s);
 int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);
-int dpa_splitk_reduce_add(const float* slabs, int splits, void* out, const void* add, long n, int bf, hipStream_t s);
 int dpa_conv_fprop(const float* x, const float* w, float* out, float* slab, int N, int H, int W, int C, int Kout,
                    int R, int S, int stride, int pad, int splits, int tile, int dgrad, int reduce, int posmajor,
                    hipStream_t st);
@@ -63,7 +62,7 @@ int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int n
 int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
                       int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
-                      int tile, int reduce, int posmajor, int np, int obf, hipStream_t st);
+                      int tile, int reduce, int posmajor, int np, int obf, hipStream_t st, const void* add);
 int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
                     int bf, hipStream_t st);
 int dpa_maxpool_bwd(const void* dy, const unsigned char* arg, void* dx, int N, int H, int W, int C, int k, int s,
@@ -165,19 +164,6 @@ void add_inplace(Tensor out, Tensor add) {
   const bool bf = out.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "add_inplace: fp32 or bf16");
   chk(dpa_add_inplace(out.data_ptr(), add.data_ptr(), out.numel(), bf ? 1 : 0, cur_stream()), "add_inplace");
-}
-
-// out = sum of `splits` fp32 slabs (slab[0 : splits * out.numel()]) + add
-void splitk_reduce_add(Tensor slab, int64_t splits, Tensor out, Tensor add) {
-  need(slab, "slab");
-  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && add.is_contiguous() && out.numel() == add.numel() &&
-                  out.scalar_type() == add.scalar_type(),
-              "splitk_reduce_add: out / add mismatch");
-  TORCH_CHECK(slab.numel() >= splits * out.numel(), "splitk_reduce_add: slab too small");
-  const bool bf = out.scalar_type() == at::kBFloat16;
-  chk(dpa_splitk_reduce_add(fp(slab), (int)splits, out.data_ptr(), add.data_ptr(), out.numel(), bf ? 1 : 0,
-                            cur_stream()),
-      "splitk_reduce_add");
 }
 
 void mean_of_w(Tensor in, Tensor out, int64_t W) {
@@ -340,7 +326,7 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
 // dz3 [NP,N,Hd,Wd,K], w3 [NP,K,R,S,C] (forward weight planes), dx [N,H,W,C] fp32: data gradient of
 // conv(x, w, stride, pad); stride a power of two.
 void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, bool posmajor) {
+                   int64_t tile, bool reduce, bool posmajor, OptT add) {
   need_planes(dz3, "dz3");
   need_planes(w3, "w3");
   const int np = dz3.size(0);
@@ -362,9 +348,16 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
     TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * C, "conv_x3_dgrad: slab too small");
     sl = fp(*slab);
   }
+  const void* ap = nullptr;
+  if (add.has_value() && add->defined()) {
+    TORCH_CHECK(add->is_cuda() && add->is_contiguous() && add->numel() == dx.numel() &&
+                    add->scalar_type() == dx.scalar_type(),
+                "conv_x3_dgrad: add must match dx (shape, dtype, contiguous)");
+    ap = add->data_ptr();
+  }
   chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), op, sl, N, Hd, Wd, K, C, R, S, (int)stride,
                         (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf,
-                        cur_stream()),
+                        cur_stream(), ap),
       "conv_x3_dgrad");
 }
 
@@ -802,7 +795,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("spin", &spin, py::arg("usec"), py::arg("done"));
   m.def("mean_of_w", &mean_of_w);
   m.def("add_inplace", &add_inplace);
-  m.def("splitk_reduce_add", &splitk_reduce_add);
   m.def("conv_fprop", &conv_fprop, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("slab"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("dgrad") = false, py::arg("reduce") = true,
         py::arg("posmajor") = false);
@@ -818,7 +810,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
-        py::arg("posmajor") = false);
+        py::arg("posmajor") = false, py::arg("add") = py::none());
   m.def("split_planes", &split_planes);
   m.def("pad_split8", &pad_split8);
   m.def("bn_part_floats", &bn_part_floats);

@@ -27,6 +27,8 @@
 // waves of 64x32.  Each thread stages one 16-byte chunk per plane per operand per k step.
 #include "common.h"
 
+extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);  // sgd.hip
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -1158,7 +1160,8 @@ int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
 
 // -6: the conv does not fit the halo tile (channels, or rows wider than BM/4 - 1 pixels)
 template <bool DG>
-int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st) {
+int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st,
+             const void* add = nullptr) {
   const int BM = halo_bm(tile), BC = halo_bc(tile);
   if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM) - 1) return -6;
   if (obf && np != 1) return -4;  // bf16 output from one-plane operands (unreduced slabs stay fp32)
@@ -1168,6 +1171,7 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
   a.cps = cdiv(a.C / BC, splits);
   a.out = splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;
+  if (add && splits > 1 && !reduce) return -4;
   a.slab = splits > 1 ? (long)a.M * a.Nout : 0;
   int rc;
   if (obf && splits == 1)
@@ -1176,10 +1180,12 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
     rc = launch_halo_tile<DG, 3, false>(a, tile, splits, st);
   else
     rc = launch_halo_tile<DG, 1, false>(a, tile, splits, st);
-  if (rc || splits == 1 || !reduce) return rc;
+  if (rc) return rc;
+  if (splits == 1) return add ? dpa_add_inplace(out, add, (long)a.M * a.Nout, obf, st) : 0;
+  if (!reduce) return 0;
   const long n4 = (long)a.M * a.Nout / 4;
-  if (obf) return launch_splitk_reduce_t(slab, (ushort4*)out, n4, splits, st);
-  return launch_splitk_reduce(slab, (float*)out, n4, splits, st);
+  if (obf) return launch_splitk_reduce_t(slab, (ushort4*)out, n4, splits, st, (const ushort4*)add);
+  return launch_splitk_reduce_t(slab, (float4*)out, n4, splits, st, (const float4*)add);
 }
 
 int halo_bytes(unsigned& xb, long xel, unsigned& wb, long wel) {
@@ -1276,9 +1282,13 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
 // Data gradient of conv(x [N,H,W,C], w [K,R,S,C], stride, pad) -> dZ [N,Hd,Wd,K]:
 // dx [N,H,W,C] fp32 (or slabs) from dz planes [NP][N,Hd,Wd,K] and the forward weight planes.
 // stride must be a power of two.
+// add (optional, dx's type): dx = dgrad + add -- a second gradient contribution to the same tensor.
+// With split-K it is folded into the reduction (no extra pass); with one split an in-place add
+// follows (an epilogue read of the addend made the bf16 dgrad kernels ~1.7x slower: the loads sit
+// in front of the stores).
 int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx, float* slab, int N, int Hd, int Wd,
                       int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
-                      int posmajor, int np, int obf, hipStream_t st) {
+                      int posmajor, int np, int obf, hipStream_t st, const void* add) {
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
     HArgs h{};
@@ -1292,7 +1302,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
     h.C = K;
     h.Nout = C;
     if (halo_bytes(h.xbytes, (long)N * H * W * K, h.wbytes, (long)K * 9 * C)) return -5;
-    return run_halo<true>(h, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st);
+    return run_halo<true>(h, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st, add);
   }
   Args a{};
   a.x = dz;
@@ -1318,13 +1328,15 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)dx;
   a.outb = (u16*)dx;
+  if (add && a.splits > 1 && !reduce) return -4;
   a.slab = a.splits > 1 ? (long)a.M * C : 0;
   const int rc = launch_any<XM_DGRAD>(a, tile, np, obf && a.splits == 1, st);
   if (rc) return rc;
+  if (a.splits == 1 && add) return dpa_add_inplace(dx, add, (long)a.M * C, obf, st);
   if (a.splits > 1 && reduce) {
     const long n4 = (long)a.M * C / 4;
-    if (obf) return launch_splitk_reduce_t(slab, (ushort4*)dx, n4, a.splits, st);
-    return launch_splitk_reduce(slab, (float*)dx, n4, a.splits, st);
+    if (obf) return launch_splitk_reduce_t(slab, (ushort4*)dx, n4, a.splits, st, (const ushort4*)add);
+    return launch_splitk_reduce_t(slab, (float4*)dx, n4, a.splits, st, (const float4*)add);
   }
   return 0;
 }

@@ -111,11 +111,3 @@ extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipSt
     add_inplace_kernel<float4><<<grid_for(n4, 256), 256, 0, s>>>((float4*)out, (const float4*)add, n4);
   return (int)hipGetLastError();
 }
-
-// out = sum of `splits` fp32 slabs of out's size + add (fp32 or bf16 out / add)
-extern "C" int dpa_splitk_reduce_add(const float* slabs, int splits, void* out, const void* add, long n, int bf,
-                                     hipStream_t s) {
-  if (n % 4) return -1;
-  if (bf) return launch_splitk_reduce_t(slabs, (ushort4*)out, n / 4, splits, s, (const ushort4*)add);
-  return launch_splitk_reduce_t(slabs, (float4*)out, n / 4, splits, s, (const float4*)add);
-}

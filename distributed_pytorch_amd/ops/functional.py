@@ -359,15 +359,9 @@ class Conv2dNHWC(torch.autograd.Function):
             addend = join.take() if (join is not None and join.last() and ctx.cx == C) else None
 
             def run_d(tile, s, pm, add=None):
+                # add: dx = dgrad + stash, in the kernel's store (one split) or its split-K reduction
                 slab = WS.get("slab", s * N * H * W * C, dz.device) if s > 1 else None
-                if add is None:
-                    Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm)
-                    return
-                Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, s == 1, pm)
-                if s > 1:
-                    Kx.splitk_reduce_add(slab, s, dx, add)  # dx = sum of slabs + stash, one pass
-                else:
-                    Kx.add_inplace(dx, add)
+                Kx.conv_x3_dgrad(dzp, wp, dx, slab, stride, pad, s, tile, True, pm, add)
 
             cfg = choose_config(ctx.impl, "dgrad", geom, N * H * W, C, R * S * K, H * W <= 16, run_d,
                                 lambda s: 4 * s * N * H * W * C)

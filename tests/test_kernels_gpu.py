@@ -381,3 +381,33 @@ def test_halo_rejects_unsupported_shapes():
     out = torch.empty(1, 8, 8, 16, device="cuda")
     with pytest.raises(RuntimeError):
         C.conv_x3_fprop(x3, w3, out, None, 1, 1, 1, 16, True, False)
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 8, 64, 128, 1, 1, 0), (2, 8, 8, 64, 64, 1, 2, 0), (4, 16, 16, 32, 64, 3, 1, 1)])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("tile", [5, 6, 16])
+@pytest.mark.parametrize("obf", [False, True])
+def test_conv_x3_dgrad_with_addend(shape, splits, tile, obf):
+    """dx = dgrad + add, folded into the epilogue (one split) or the split-K reduction (GradJoin's
+    residual-gradient sum); fp32 output with 3 planes, bf16 output with 1 plane."""
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    if tile == 16 and (R != 3 or st != 1):
+        pytest.skip("halo tiles are 3x3/s1 only")
+    np_ = 1 if obf else 3
+    g = torch.Generator().manual_seed(17 + splits)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(True)
+    w = torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, dy)
+    add = torch.randn(N, H, W, Cin, generator=g)
+    dt = torch.bfloat16 if obf else torch.float32
+    addd = add.to(dt).cuda()
+    dx = torch.empty(N, H, W, Cin, device="cuda", dtype=dt)
+    slab = torch.empty(splits * N * H * W * Cin, device="cuda") if splits > 1 else None
+    C.conv_x3_dgrad(_planes(dy.float().permute(0, 2, 3, 1), np_), _planes(w.float().permute(0, 2, 3, 1), np_), dx,
+                    slab, st, pd, splits, tile, True, False, addd)
+    torch.cuda.synchronize()
+    ref = gx.permute(0, 2, 3, 1) + addd.double().cpu()
+    assert rel_err(dx, ref) < (2e-2 if obf else 1e-5)
