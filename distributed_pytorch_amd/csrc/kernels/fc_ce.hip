@@ -9,14 +9,15 @@
 #include "common.h"
 
 namespace {
-constexpr int MAXJ = 16;
-
-constexpr int MAXCL = 16;  // Cin / 64 values per lane kept in registers (Cin <= 1024)
+// Compile-time bounds: MAXJ classes, MAXCL = Cin / 64 values per lane kept in registers.  The VGG
+// head (J = 10, Cin = 512) runs the <10, 8> instance, anything else up to J = 16, Cin = 1024 the
+// generic one (every loop over MAXJ / MAXCL is fully unrolled, so tight bounds mean no dead lanes).
+constexpr int GEN_J = 16, GEN_CL = 16;
 
 // W [J][Cin] is staged once per block into LDS (one round of independent 16-B loads), the row
 // (Cin/64 values per lane) is held in registers, and the J wave reductions are interleaved: the
 // kernel pays ~two global-memory latencies instead of a chain of dependent L2 round trips.
-template <bool TRAIN>
+template <bool TRAIN, int MAXJ, int MAXCL>
 __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias,
                                                          const long long* __restrict__ target,
@@ -110,6 +111,7 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
 // grid: cdiv(Cin,8) + 1 blocks of 256 threads = 8 columns x 32 row-groups.  dlogits [B][J] is
 // staged in LDS; each thread issues its rows' x loads together, the row-groups are combined
 // through LDS in a fixed order (deterministic).  The last block reduces db and the batch-mean loss.
+template <int MAXJ>
 __global__ __launch_bounds__(256) void fc_ce_wgrad_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ dlogits,
                                                           const float* __restrict__ loss_row, float* __restrict__ dw,
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256) void fc_ce_wgrad_kernel(const float* __restric
     }
   } else {
     __shared__ float sh[256];
-    __shared__ float sj[16][MAXJ + 1];
+    __shared__ float sj[16][17];  // 16 row groups x 16 class lanes (+1 pad), independent of MAXJ
     // db: thread (j = t % 16, g = t / 16) sums rows g, g+16, ...
     const int jj = t % 16, g = t / 16;
     float s = 0.f;
@@ -221,19 +223,31 @@ extern "C" {
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st) {
-  if (J > MAXJ || Cin > 64 * MAXCL || Cin % 4 || (long)B * J * 4 > 48 * 1024) return -2;
-  fc_ce_rows_kernel<true><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits, dx, nullptr,
-                                                                nullptr, B, Cin, J);
-  fc_ce_wgrad_kernel<<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out, loss_accum, B,
-                                                               Cin, J);
+  if (J > GEN_J || Cin > 64 * GEN_CL || Cin % 4 || (long)B * J * 4 > 48 * 1024) return -2;
+  if (J <= 10 && Cin <= 512) {
+    fc_ce_rows_kernel<true, 10, 8><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits, dx,
+                                                                          nullptr, nullptr, B, Cin, J);
+    fc_ce_wgrad_kernel<10><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
+                                                                     loss_accum, B, Cin, J);
+  } else {
+    fc_ce_rows_kernel<true, GEN_J, GEN_CL><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits,
+                                                                                dx, nullptr, nullptr, B, Cin, J);
+    fc_ce_wgrad_kernel<GEN_J><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
+                                                                        loss_accum, B, Cin, J);
+  }
   return (int)hipGetLastError();
 }
 
 int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                    int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st) {
-  if (J > MAXJ || Cin > 64 * MAXCL || Cin % 4) return -2;
-  fc_ce_rows_kernel<false><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, nullptr, nullptr, correct_row, logits,
-                                                       B, Cin, J);
+  if (J > GEN_J || Cin > 64 * GEN_CL || Cin % 4) return -2;
+  if (J <= 10 && Cin <= 512)
+    fc_ce_rows_kernel<false, 10, 8><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, nullptr, nullptr,
+                                                                           correct_row, logits, B, Cin, J);
+  else
+    fc_ce_rows_kernel<false, GEN_J, GEN_CL><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, nullptr,
+                                                                                 nullptr, correct_row, logits, B,
+                                                                                 Cin, J);
   if (acc) eval_accum_kernel<<<1, 256, 0, st>>>(loss_row, correct_row, acc, B);
   return (int)hipGetLastError();
 }
