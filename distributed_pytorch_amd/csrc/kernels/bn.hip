@@ -32,19 +32,32 @@
 namespace {
 
 constexpr int RT = 1024;  // forward-statistics block size
-// Backward reduce: 256-thread blocks with a 4 KB LDS tree, ~512 of them (512: +2.2 % step
-// throughput over 1024 and +0.7 % over 256, fewer partial rows for the finalize).  The backward reduce runs
-// beside the weight-gradient convs of the other stream; a 1024-thread / 48 KB block could not be
-// placed on a CU holding conv blocks and waited for whole CUs to drain (3-6x slower in the step).
-// DPA_BN_BWD_BLOCK=1024 selects the old single-stream geometry (1024 threads, ~256 blocks) for A/B.
+// Backward reduce geometry, by tensor size (M rows x C/4 float4 lanes):
+// * up to WIDE_MIN_F4 lanes (every VGG-11 layer at batch 256): 256-thread blocks with a 4 KB LDS
+//   tree, ~512 of them.  In the VGG engine the reduce runs beside the weight-gradient convs of the
+//   other stream; a 1024-thread / 48 KB block could not be placed on a CU holding conv blocks and
+//   waited for whole CUs to drain (3-6x slower in the step); 512 blocks: +2.2 % step throughput
+//   over 1024 and +0.7 % over 256 (fewer partial rows for the finalize).
+// * larger tensors (ResNet-50 at batch 128: 3.2M-25.7M lanes per BN; autograd runs them on one
+//   stream): 1024-thread blocks, ~256 of them — 512 x 256 left ResNet-50 at 7,035 img/s against
+//   7,485 (measured A/B, 2048 x 256: 7,454).
+// DPA_BN_BWD_BLOCK=256|1024 forces one geometry for every layer, DPA_BN_BWD_BLOCKS the small-block
+// grid size (A/B switches).
 constexpr int RTB = 256;
 constexpr int BWD_BLOCKS = 512;
-inline bool bwd_wide() {
-  static const bool w = [] {
+constexpr long WIDE_MIN_F4 = 3L << 20;
+inline int bwd_force() {
+  static const int f = [] {
     const char* e = std::getenv("DPA_BN_BWD_BLOCK");
-    return e && std::atoi(e) == 1024;
+    return e ? std::atoi(e) : 0;
   }();
-  return w;
+  return f;
+}
+inline bool bwd_wide(long M, int C) {
+  const int f = bwd_force();
+  if (f == 1024) return true;
+  if (f == 256) return false;
+  return M * (long)(C >> 2) > WIDE_MIN_F4;
 }
 // channels per backward-finalize block: 8 (32 partial rows of each in flight) or 4 (64 rows;
 // DPA_BN_FIN_CPB=4).  Equal within noise in the step (158.5k vs 158.2k img/s), 8 is kept.
@@ -55,13 +68,13 @@ inline int fin_cpb() {
   }();
   return v;
 }
-inline int bwd_rt() { return bwd_wide() ? RT : RTB; }
-inline int bwd_blocks() {
+inline int bwd_rt(long M, int C) { return bwd_wide(M, C) ? RT : RTB; }
+inline int bwd_blocks(long M, int C) {
   static const int nb = [] {
-    const char* e = std::getenv("DPA_BN_BWD_BLOCKS");  // A/B of the backward reduce grid size
+    const char* e = std::getenv("DPA_BN_BWD_BLOCKS");
     return e ? std::atoi(e) : BWD_BLOCKS;
   }();
-  return bwd_wide() ? 256 : nb;
+  return bwd_wide(M, C) ? 256 : nb;
 }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
@@ -100,6 +113,8 @@ __host__ inline int red_rows_per_block(int M, int C, int rt = RT, int blocks = 2
   rpb = ((rpb + g.RPI - 1) / g.RPI) * g.RPI;
   return rpb < g.RPI ? g.RPI : rpb;
 }
+
+inline int bwd_rows_per_block(int M, int C) { return red_rows_per_block(M, C, bwd_rt(M, C), bwd_blocks(M, C)); }
 
 // In-block tree over the RPI row lanes of each channel lane (fixed order): on return sh[t] for
 // lane_r == 0 holds the block sum.  Caller has stored sh[t] and synchronised.
@@ -676,10 +691,11 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
                   hipStream_t st) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
-  const int rpb = red_rows_per_block(Mo, C, bwd_rt(), bwd_blocks());
+  const int rpb = bwd_rows_per_block(Mo, C);
   const int nblk = (Mo + rpb - 1) / rpb;
+  const bool wide = bwd_wide(Mo, C);
 #define RED(P, A)                                                                                                 \
-  if (bwd_wide())                                                                                                 \
+  if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
                                                             N, H, W, C, rpb);                                     \
   else                                                                                                            \
@@ -877,7 +893,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
 extern "C" {
 // floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (3 per ...)
 long dpa_bn_part_floats(int M, int C, int bwd) {
-  const int rpb = bwd ? red_rows_per_block(M, C, bwd_rt(), bwd_blocks()) : red_rows_per_block(M, C);
+  const int rpb = bwd ? bwd_rows_per_block(M, C) : red_rows_per_block(M, C);
   const long nblk = (M + rpb - 1) / rpb;
   return nblk * C * (bwd ? 3 : 2);
 }
