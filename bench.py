@@ -175,6 +175,7 @@ def main(argv=None):
     graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
                if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
     el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev)
+    engine.check_signals()
     loss = float(engine.loss.item())
     ms = el / a.steps * 1e3
     img_s = a.batch * ctx.world * a.steps / el

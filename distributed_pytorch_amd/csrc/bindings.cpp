@@ -62,7 +62,10 @@ int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int n
 int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
                       int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
-                      int tile, int reduce, int posmajor, int np, int obf, hipStream_t st, const void* add);
+                      int tile, int reduce, int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig,
+                      int sig_val);
+int dpa_wait_signal(const int* sig, int val, long long timeout_us, int* tmo, hipStream_t st);
+int dpa_set_signal(int* sig, int val, hipStream_t st);
 int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
                     int bf, hipStream_t st);
 int dpa_maxpool_bwd(const void* dy, const unsigned char* arg, void* dx, int N, int H, int W, int C, int k, int s,
@@ -150,6 +153,24 @@ void sgd_flat(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double
 
 // Diagnostics: occupy the current stream for ~usec microseconds (one wave, bounded loop) and then
 // write 1 to done[0].  Used to hold a collective behind a long kernel (watchdog timeout test).
+// one int32 word on the GPU (a stream-signal flag or timeout word)
+int* signal_ptr(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kInt32 && t.numel() >= 1, what,
+              ": signal word must be a CUDA int32 tensor");
+  return t.data_ptr<int>();
+}
+
+// the current stream waits (one polling wave) until sig[0] >= val; tmo[0] = 1 after timeout_us
+void wait_signal(Tensor sig, int64_t val, int64_t timeout_us, Tensor tmo) {
+  chk(dpa_wait_signal(signal_ptr(sig, "wait_signal"), (int)val, timeout_us, signal_ptr(tmo, "wait_signal"),
+                      cur_stream()),
+      "wait_signal");
+}
+
+void set_signal(Tensor sig, int64_t val) {
+  chk(dpa_set_signal(signal_ptr(sig, "set_signal"), (int)val, cur_stream()), "set_signal");
+}
+
 void spin(int64_t usec, Tensor done) {
   need(done, "done", at::kInt);
   TORCH_CHECK(usec >= 0 && usec <= 10000000, "spin: usec out of range");
@@ -326,7 +347,7 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
 // dz3 [NP,N,Hd,Wd,K], w3 [NP,K,R,S,C] (forward weight planes), dx [N,H,W,C] fp32: data gradient of
 // conv(x, w, stride, pad); stride a power of two.
 void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, bool posmajor, OptT add) {
+                   int64_t tile, bool reduce, bool posmajor, OptT add, OptT sig, int64_t sig_val) {
   need_planes(dz3, "dz3");
   need_planes(w3, "w3");
   const int np = dz3.size(0);
@@ -355,9 +376,11 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
                 "conv_x3_dgrad: add must match dx (shape, dtype, contiguous)");
     ap = add->data_ptr();
   }
+  int* sp = nullptr;
+  if (sig.has_value() && sig->defined()) sp = signal_ptr(*sig, "conv_x3_dgrad");
   chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), op, sl, N, Hd, Wd, K, C, R, S, (int)stride,
                         (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf,
-                        cur_stream(), ap),
+                        cur_stream(), ap, sp, (int)sig_val),
       "conv_x3_dgrad");
 }
 
@@ -810,7 +833,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
-        py::arg("posmajor") = false, py::arg("add") = py::none());
+        py::arg("posmajor") = false, py::arg("add") = py::none(), py::arg("sig") = py::none(),
+        py::arg("sig_val") = 0);
+  m.def("wait_signal", &wait_signal, py::arg("sig"), py::arg("val"), py::arg("timeout_us"), py::arg("tmo"));
+  m.def("set_signal", &set_signal, py::arg("sig"), py::arg("val"));
   m.def("split_planes", &split_planes);
   m.def("pad_split8", &pad_split8);
   m.def("bn_part_floats", &bn_part_floats);

@@ -41,6 +41,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // ---- fp32 -> bf16 operand planes (round-to-nearest-even): x = x0 (+ x1 + x2) ----
 // NP = 3 carries the full 24-bit fp32 mantissa (conv_x3.hip header); NP = 1 is plain bf16.
 typedef unsigned short u16;
+typedef __attribute__((address_space(1))) int gint;  // global-memory int (agent-scope atomics)
+
+// Kernel-start stream signal (engine.py, two-stream backward): one lane of the first workgroup
+// stores `val` to `sig` with a relaxed agent-scope atomic store.  When any workgroup of a kernel
+// runs, every earlier kernel of its stream has completed and its writes were released at that
+// kernel boundary, so a consumer on another stream that sees `val` (signal.hip wait kernel) may
+// run the dependent kernels next without a queue marker on the producer stream.
+__device__ __forceinline__ void start_signal(int* sig, int val) {
+  if (sig != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    __hip_atomic_store((gint*)sig, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ u16 bf16_rne(float f) {
   unsigned u = __float_as_uint(f);
   u += 0x7FFFu + ((u >> 16) & 1u);

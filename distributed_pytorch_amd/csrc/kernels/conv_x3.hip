@@ -76,6 +76,8 @@ struct Args {
   int gm, gn, splits, posmajor;
   int imask, ishift;  // input dilation (DGRAD of a strided conv): 2^ishift, imask = 2^ishift - 1
   FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
+  int* sig;  // optional kernel-start stream signal (common.h start_signal)
+  int sig_val;
 };
 
 __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& img, unsigned& oh, unsigned& ow) {
@@ -137,6 +139,7 @@ __device__ __forceinline__ void mfma_tile(f32x16 (&acc)[TM][TN], const bf16x8 (&
 // OB: epilogue stores bf16 (round-to-nearest-even) to a.outb instead of fp32 (bf16 activations).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP, int BK, int NSTAGE, bool OB = false>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) {
+  start_signal(a.sig, a.sig_val);
   constexpr bool WG = MODE == XM_WGRAD;
   constexpr bool DG = MODE == XM_DGRAD;
   constexpr bool ARC = WG, BRC = WG || DG;  // operand images row-contiguous ([k][col]) in LDS
@@ -565,6 +568,8 @@ struct HArgs {
   long slab;
   int N, H, W, C, Nout, M;  // C: reduction channels
   int gm, gn, cps;          // row / column tiles, reduction chunks per split
+  int* sig;                 // optional kernel-start stream signal (common.h start_signal)
+  int sig_val;
 };
 
 // staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
@@ -572,6 +577,7 @@ __host__ __device__ constexpr int halo_slots(int BM) { return BM + BM / 2 + 1; }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, bool OB>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs a) {
+  start_signal(a.sig, a.sig_val);
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -1288,10 +1294,12 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
 // in front of the stores).
 int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx, float* slab, int N, int Hd, int Wd,
                       int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
-                      int posmajor, int np, int obf, hipStream_t st, const void* add) {
+                      int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig, int sig_val) {
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
     HArgs h{};
+    h.sig = sig;
+    h.sig_val = sig_val;
     h.x = dz;
     h.xps = dzps;
     h.w = w;
@@ -1305,6 +1313,8 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
     return run_halo<true>(h, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st, add);
   }
   Args a{};
+  a.sig = sig;
+  a.sig_val = sig_val;
   a.x = dz;
   a.xps = dzps;
   a.w = w;

@@ -207,6 +207,16 @@ class VGGEngine:
                         else None)
         self._wev = [DevEvent() for _ in L] if self.wstream is not None else None
         self._join = StreamJoin() if self.wstream is not None else None
+        # kernel-start signals instead of per-layer events on the critical-path stream (signal.hip):
+        # the data-gradient conv of layer i stores the step's epoch into ksig[i] when it starts, the
+        # wgrad stream polls it.  Plane (x3 / bf16) convs only; never under graph capture (a graph may
+        # order the polling kernel before its producer).  DPA_KSIGNAL=0: events everywhere.
+        self.ksignal = (self.wstream is not None and os.environ.get("DPA_KSIGNAL", "1") == "1"
+                        and hasattr(self.K, "wait_signal"))
+        self.ksig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None
+        self.ksig_tmo = torch.zeros(1, dtype=torch.int32, device=dev) if self.ksignal else None
+        self._sig_epoch = 0
+        self.ksig_timeout_us = int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "2000000"))
         self.slab = torch.empty(1, **f32)
         self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
         for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
@@ -499,15 +509,20 @@ class VGGEngine:
             self.K.conv_fprop(xin, self.params[f"{l.conv_key}.weight"], z, slab, 1, 1, s, tile, False, reduce, pm)
         return 1 if (reduce or s == 1) else s
 
-    def _conv_dgrad(self, i: int, n: int) -> int:
-        """Data gradient of layer i into g[i-1] (or slabs); returns the unreduced split count."""
+    def _conv_dgrad(self, i: int, n: int, sig_val: int = 0) -> int:
+        """Data gradient of layer i into g[i-1] (or slabs); returns the unreduced split count.
+        ``sig_val`` > 0: the kernel stores it into ksig[i] when it starts (plane convs only)."""
         l = self.spec.convs[i]
         tile, s, pm = self.conv_config(i, "dgrad", n)
         self._ensure_slab(self._slab_need(i, "dgrad", n))
         slab = self.slab if s > 1 else None
         out = self.g[i - 1][:n]
         if self.planes[i]:
-            self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm)
+            if sig_val > 0:
+                self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm,
+                                     sig=self.ksig[i:i + 1], sig_val=sig_val)
+            else:
+                self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm)
         else:
             self.K.conv_fprop(self.dz[i][:n], self.params[f"{l.conv_key}.weight"], out, slab, 1, 1, s, tile, True,
                               False, pm)
@@ -587,6 +602,10 @@ class VGGEngine:
         gsplit = 1  # split-K slabs of g[i] left unreduced by the previous dgrad (summed inside bn_bwd)
         ws = self.wstream
         main = torch.cuda.current_stream(self.device) if ws is not None else None
+        epoch = 0
+        if self.ksignal and not torch.cuda.is_current_stream_capturing():
+            self._sig_epoch += 1
+            epoch = self._sig_epoch
         for i in range(len(L) - 1, -1, -1):
             l = L[i]
             st = self.stats[i]
@@ -622,6 +641,18 @@ class VGGEngine:
             # two streams: the critical path (dgrad -> BN backward of layer i-1) is issued first on
             # the main stream; wgrad(i) follows bn_bwd(i) on the wgrad stream, and the bucket's
             # collective is ordered after it (the comm region waits on the stream current here)
+            if epoch and self.planes[i]:
+                # no queue marker on the main stream: dgrad(i) signals its own start, which implies
+                # bn_bwd(i) (dz) has completed; the wgrad stream polls for it (signal.hip)
+                gsplit = self._conv_dgrad(i, n, sig_val=epoch)
+                if params_free is not None:
+                    params_free(names)
+                with torch.cuda.stream(ws):
+                    K.wait_signal(self.ksig[i:i + 1], epoch, self.ksig_timeout_us, self.ksig_tmo)
+                    self._conv_wgrad(i, x, n)
+                    if grad_ready is not None:
+                        grad_ready(names)
+                continue
             ev = self._wev[i]
             ev.record(main)
             if i > 0:
@@ -642,6 +673,13 @@ class VGGEngine:
         """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
         self.K.sgd_flat(self.params.flat, self.grads.flat, self.mom.flat, self.lr, self.momentum, self.weight_decay,
                         grad_scale, self.steps_taken == 0, offset, count, self.wplanes)
+
+    def check_signals(self):
+        """Raise if a wgrad-stream wait gave up (its producer's signal never arrived: the weight
+        gradients of that step were computed from an unfinished BN backward).  Synchronises."""
+        if self.ksig_tmo is not None and int(self.ksig_tmo.item()) != 0:
+            raise RuntimeError("VGGEngine: a wgrad-stream signal wait timed out "
+                               f"(DPA_KSIGNAL_TIMEOUT_US={self.ksig_timeout_us}); weight gradients are invalid")
 
     def finish_step(self):
         self.steps_taken += 1

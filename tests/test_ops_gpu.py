@@ -451,20 +451,24 @@ def test_other_vgg_depths_step_matches_torch(name):
             assert (du - dr).norm().item() <= 1e-2 * dr.norm().item(), k  # deep + batch 16: ill-conditioned
 
 
-def test_wgrad_stream_matches_single_stream(monkeypatch):
-    """Weight gradients on the second HIP stream (the default) train bit-identically to the
-    single-stream schedule: the event/stream ordering loses no dependency."""
+@pytest.mark.parametrize("impl", ["x3", "bf16"])
+def test_wgrad_stream_matches_single_stream(monkeypatch, impl):
+    """Weight gradients on the second HIP stream train bit-identically to the single-stream
+    schedule, both with per-layer events and with the kernel-start signals (the default,
+    signal.hip): the cross-stream ordering loses no dependency."""
     from distributed_pytorch_amd.engine import VGGEngine
 
     g = torch.Generator().manual_seed(5)
     xs = [torch.randn(64, 32, 32, 4, generator=g) for _ in range(3)]
     ts = [torch.randint(0, 10, (64,), generator=g) for _ in range(3)]
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("DPA_WGRAD_STREAM", flag)
-        e = VGGEngine("VGG11", "cuda", max_batch=64, impl="x3", lr=0.01)
+    for stream, ksig in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("DPA_WGRAD_STREAM", stream)
+        monkeypatch.setenv("DPA_KSIGNAL", ksig)
+        e = VGGEngine("VGG11", "cuda", max_batch=64, impl=impl, lr=0.01)
         e.init_parameters(seed=3)
-        assert (e.wstream is not None) == (flag == "1")
+        assert (e.wstream is not None) == (stream == "1")
+        assert e.ksignal == (stream == "1" and ksig == "1")
         for x, t in zip(xs, ts):
             x = x.cuda()
             x[..., 3] = 0
@@ -472,8 +476,12 @@ def test_wgrad_stream_matches_single_stream(monkeypatch):
             e.sgd_step()
             e.finish_step()
         torch.cuda.synchronize()
+        e.check_signals()
+        if e.ksignal:
+            assert e.ksig[1:].tolist() == [3] * (len(e.spec.convs) - 1)  # every side layer signalled 3 steps
         outs.append(e.params.flat.clone())
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.parametrize("impl", ["x3", "bf16"])
