@@ -31,7 +31,7 @@ int dpa_bn_apply(const void* z, float* a, unsigned short* a3, int np, const floa
 int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
-               int pool, int act, const void* res, void* dres, int zbf, hipStream_t st);
+               int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -45,7 +45,7 @@ int dpa_conv0_fwd(const float* x, const float* w, int CP, float* z, float* part,
 int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
-                      float* dw, int CP, int N, hipStream_t st);
+                      float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st);
@@ -158,6 +158,10 @@ int* signal_ptr(const Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kInt32 && t.numel() >= 1, what,
               ": signal word must be a CUDA int32 tensor");
   return t.data_ptr<int>();
+}
+
+int* opt_signal(const OptT& t, const char* what) {
+  return (t.has_value() && t->defined()) ? signal_ptr(*t, what) : nullptr;
 }
 
 // the current stream waits (one polling wave) until sig[0] >= val; tmo[0] = 1 after timeout_us
@@ -376,8 +380,7 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
                 "conv_x3_dgrad: add must match dx (shape, dtype, contiguous)");
     ap = add->data_ptr();
   }
-  int* sp = nullptr;
-  if (sig.has_value() && sig->defined()) sp = signal_ptr(*sig, "conv_x3_dgrad");
+  int* sp = opt_signal(sig, "conv_x3_dgrad");
   chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), op, sl, N, Hd, Wd, K, C, R, S, (int)stride,
                         (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf,
                         cur_stream(), ap, sp, (int)sig_val),
@@ -485,7 +488,7 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t
 // x [N,32,32,4], dw [64,3,3,CP], wpart >= wgrad0_part_floats(N).
 void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean,
                    Tensor invstd, Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias,
-                   Tensor x, Tensor wpart, Tensor dw) {
+                   Tensor x, Tensor wpart, Tensor dw, OptT sig, int64_t sig_val) {
   for (auto* t : {&gsrc, &g, &z, &scale, &shift, &mean, &invstd, &gamma, &part, &coef, &dgamma, &dbeta, &x, &wpart, &dw})
     need(*t, "bn_bwd_wgrad0 operand");
   const int N = z.size(0);
@@ -501,7 +504,7 @@ void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale
   TORCH_CHECK(coef.numel() >= 3 * 64 && scale.numel() == 64 && gamma.numel() == 64, "bn_bwd_wgrad0: channel vectors");
   chk(dpa_bn_bwd_wgrad0(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma),
                         fp(part), fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), fp(x), fp(wpart), fp(dw),
-                        (int)dw.size(3), N, cur_stream()),
+                        (int)dw.size(3), N, cur_stream(), opt_signal(sig, "bn_bwd_wgrad0"), (int)sig_val),
       "bn_bwd_wgrad0");
 }
 
@@ -586,7 +589,7 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
@@ -625,7 +628,7 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 bf ? 1 : 0, cur_stream()),
+                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val),
       "bn_bwd");
 }
 
@@ -847,8 +850,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"), py::arg("scale"),
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
-        py::arg("res") = py::none(), py::arg("dres") = py::none());
-  m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0);
+        py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
+        py::arg("sig_val") = 0);
+  m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
+        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
+        py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("x"), py::arg("wpart"),
+        py::arg("dw"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
   m.def("gap", &gap);
   m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("target"), py::arg("loss_row"),
         py::arg("dlogits") = py::none(), py::arg("correct_row") = py::none(), py::arg("loss") = py::none(),

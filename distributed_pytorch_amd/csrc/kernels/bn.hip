@@ -407,7 +407,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
                                                             float* __restrict__ part, int N, int H, int W, int C,
-                                                            int rpb) {
+                                                            int rpb, int* sig, int sig_val) {
+  start_signal(sig, sig_val);
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
   const int lane_c = t % gg.TPR, lane_r = t / gg.TPR;
@@ -688,7 +689,7 @@ template <typename TZ>
 void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                   const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                   float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
-                  hipStream_t st) {
+                  hipStream_t st, int* sig = nullptr, int sig_val = 0) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = bwd_rows_per_block(Mo, C);
@@ -697,10 +698,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
 #define RED(P, A)                                                                                                 \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
-                                                            N, H, W, C, rpb);                                     \
+                                                            N, H, W, C, rpb, sig, sig_val);                       \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
-                                                              part, N, H, W, C, rpb)
+                                                              part, N, H, W, C, rpb, sig, sig_val)
   if (pool) {
     RED(true, 0);
   } else if (act == 0) {
@@ -865,10 +866,10 @@ template <typename TZ>
 int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-                const TZ* res, TZ* dres, hipStream_t st) {
+                const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val) {
   if (nsplit < 1) nsplit = 1;
   bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
-                   C, pool, act, res, st);
+                   C, pool, act, res, st, sig, sig_val);
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
@@ -943,16 +944,16 @@ int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, c
 int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-               const void* res, void* dres, int zbf, hipStream_t st) {
+               const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && (!res || !dres))) return -2;
   if (zbf && nsplit > 1) return -2;
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st);
+                            (u16*)dres, st, sig, sig_val);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st);
+                            (float*)dres, st, sig, sig_val);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.
@@ -962,11 +963,11 @@ long dpa_wgrad0_part_floats(int N) { return (long)N * (16 / WB0_RPB) * 64 * 27; 
 int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
-                      float* dw, int CP, int N, hipStream_t st) {
+                      float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val) {
   if (nsplit < 1) nsplit = 1;
   if (CP < 3) return -2;
   bn_bwd_stats<float>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, 32,
-                      32, 64, 1, 0, nullptr, st);
+                      32, 64, 1, 0, nullptr, st, sig, sig_val);
   const float* gg = nsplit > 1 ? g : gsrc;
   const int nblk = N * (16 / WB0_RPB);
   bn_bwd_wgrad0_kernel<<<nblk, 256, 0, st>>>(gg, z, scale, shift, coef, x, wpart);

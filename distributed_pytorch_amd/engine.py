@@ -214,9 +214,12 @@ class VGGEngine:
         self.ksignal = (self.wstream is not None and os.environ.get("DPA_KSIGNAL", "1") == "1"
                         and hasattr(self.K, "wait_signal"))
         self.ksig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None
+        self.bsig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None  # BN bwd starts
         self.ksig_tmo = torch.zeros(1, dtype=torch.int32, device=dev) if self.ksignal else None
         self._sig_epoch = 0
         self.ksig_timeout_us = int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "2000000"))
+        # params_free hands the sync a later kernel's signal instead of recording an event (A/B: 0)
+        self.free_signal = os.environ.get("DPA_FREE_SIGNAL", "1") == "1"
         self.slab = torch.empty(1, **f32)
         self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
         for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
@@ -561,13 +564,21 @@ class VGGEngine:
         Callbacks (the gradient-sync strategy's hooks):
           ``grad_ready(names)``  every kernel writing those gradients has been enqueued; called with
                                  the stream that ran the last of them current (wgrad stream or main);
-          ``params_free(names)`` every kernel of this step READING those parameters (or their bf16
-                                 planes) has been enqueued; called with the main stream current.
+          ``params_free(names, signal=None)`` every kernel of this step READING those parameters
+                                 (or their bf16 planes) has been enqueued; called with the main
+                                 stream current.  ``signal`` (when not None): a (flag, value) pair
+                                 that a LATER main-stream kernel raises when it starts — waiting for
+                                 it (``wait_signal``) orders after those readers without a queue
+                                 marker on the main stream.
         Once both have fired for a tensor its optimizer step may run while backward continues."""
         K, P, G = self.K, self.params, self.grads
         n = x.shape[0]
         L = self.spec.convs
         buffers_wait = pre_forward() if pre_forward is not None else None
+        epoch = 0
+        if self.ksignal and not torch.cuda.is_current_stream_capturing():
+            self._sig_epoch += 1
+            epoch = self._sig_epoch
         if self.x0p is not None and not (self.fused_conv0 and self.fused_wgrad0):  # plane kernels read x0p
             K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(L):
@@ -597,15 +608,42 @@ class VGGEngine:
                       self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
         if grad_ready is not None:
             grad_ready(["fc1.weight", "fc1.bias"])
+        # Kernel-start signals (epoch > 0, signal.hip): each BN backward raises bsig[i] when it starts,
+        # so every main-stream kernel enqueued before it (the data-gradient conv of layer i+1, the
+        # head) has completed.  params_free is therefore reported AFTER the next BN backward is
+        # enqueued, with its signal: the sync's update waits on it instead of an event recorded on
+        # the main stream.  Likewise layer i+1's wgrad-stream work (wait for dgrad(i+1)'s start
+        # signal, wgrad, grad_ready) is enqueued after bn_bwd(i).  A wait is thus always enqueued
+        # after the kernel that raises its signal: it completes even if streams share a hardware
+        # queue.
+        sigs = bool(epoch) and self.free_signal
+        free_later: List[List[str]] = []  # params_free calls waiting for the next BN backward
+        side_later: Optional[tuple] = None  # (layer, names) whose wgrad-stream work is deferred
         if params_free is not None:
-            params_free(["fc1.weight", "fc1.bias"])
+            if sigs:
+                free_later.append(["fc1.weight", "fc1.bias"])
+            else:
+                params_free(["fc1.weight", "fc1.bias"])
         gsplit = 1  # split-K slabs of g[i] left unreduced by the previous dgrad (summed inside bn_bwd)
         ws = self.wstream
         main = torch.cuda.current_stream(self.device) if ws is not None else None
-        epoch = 0
-        if self.ksignal and not torch.cuda.is_current_stream_capturing():
-            self._sig_epoch += 1
-            epoch = self._sig_epoch
+
+        def side_work(j: int, nm: List[str]):
+            with torch.cuda.stream(ws):
+                K.wait_signal(self.ksig[j:j + 1], epoch, self.ksig_timeout_us, self.ksig_tmo)
+                self._conv_wgrad(j, x, n)
+                if grad_ready is not None:
+                    grad_ready(nm)
+
+        def after_bn(i: int):
+            nonlocal free_later, side_later
+            for nm in free_later:
+                params_free(nm, signal=(self.bsig[i:i + 1], epoch))
+            free_later = []
+            if side_later is not None:
+                side_work(*side_later)
+                side_later = None
+
         for i in range(len(L) - 1, -1, -1):
             l = L[i]
             st = self.stats[i]
@@ -613,11 +651,13 @@ class VGGEngine:
             g = self.g[i][:n]
             dzbuf = self.dz3[i][:, :n] if self.planes[i] else self.dz[i][:n]
             names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
+            bsig = dict(sig=self.bsig[i:i + 1], sig_val=epoch) if epoch else {}
             if i == 0 and self.fused_wgrad0:
                 K.bn_bwd_wgrad0(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                                 st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
                                 G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], x, self.wpart,
-                                G[f"{l.conv_key}.weight"])
+                                G[f"{l.conv_key}.weight"], **bsig)
+                after_bn(i)
                 if grad_ready is not None:
                     grad_ready(names)
                 if params_free is not None:
@@ -625,7 +665,8 @@ class VGGEngine:
                 continue
             K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                      st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                     G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool)
+                     G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig)
+            after_bn(i)
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
                 # Layer 0's wgrad has nothing left to overlap with, so it stays on the main stream (a
@@ -636,7 +677,10 @@ class VGGEngine:
                 if i > 0:
                     gsplit = self._conv_dgrad(i, n)
                 if params_free is not None:  # dgrad(i) was the last reader of layer i's weights
-                    params_free(names)
+                    if sigs and i > 0:
+                        free_later.append(names)
+                    else:
+                        params_free(names)
                 continue
             # two streams: the critical path (dgrad -> BN backward of layer i-1) is issued first on
             # the main stream; wgrad(i) follows bn_bwd(i) on the wgrad stream, and the bucket's
@@ -646,24 +690,33 @@ class VGGEngine:
                 # bn_bwd(i) (dz) has completed; the wgrad stream polls for it (signal.hip)
                 gsplit = self._conv_dgrad(i, n, sig_val=epoch)
                 if params_free is not None:
-                    params_free(names)
-                with torch.cuda.stream(ws):
-                    K.wait_signal(self.ksig[i:i + 1], epoch, self.ksig_timeout_us, self.ksig_tmo)
-                    self._conv_wgrad(i, x, n)
-                    if grad_ready is not None:
-                        grad_ready(names)
+                    if sigs:
+                        free_later.append(names)
+                    else:
+                        params_free(names)
+                if sigs:
+                    side_later = (i, names)
+                else:
+                    side_work(i, names)
                 continue
             ev = self._wev[i]
             ev.record(main)
             if i > 0:
                 gsplit = self._conv_dgrad(i, n)
             if params_free is not None:
-                params_free(names)
+                if sigs:
+                    free_later.append(names)
+                else:
+                    params_free(names)
             ev.wait(ws)
             with torch.cuda.stream(ws):
                 self._conv_wgrad(i, x, n)
                 if grad_ready is not None:
                     grad_ready(names)
+        for nm in free_later:  # no BN backward left to carry a signal
+            params_free(nm)
+        if side_later is not None:
+            side_work(*side_later)
         if ws is not None:
             self._join(main, ws)
         self._eval_dirty = True
@@ -673,6 +726,10 @@ class VGGEngine:
         """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
         self.K.sgd_flat(self.params.flat, self.grads.flat, self.mom.flat, self.lr, self.momentum, self.weight_decay,
                         grad_scale, self.steps_taken == 0, offset, count, self.wplanes)
+
+    def wait_signal(self, signal):
+        """The current stream waits (one polling wave, bounded) for a ``(flag, value)`` signal."""
+        self.K.wait_signal(signal[0], signal[1], self.ksig_timeout_us, self.ksig_tmo)
 
     def check_signals(self):
         """Raise if a wgrad-stream wait gave up (its producer's signal never arrived: the weight

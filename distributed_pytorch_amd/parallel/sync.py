@@ -45,7 +45,7 @@ _POST_FORWARD_BUFFERS = os.environ.get("DPA_BUF_BCAST", "post") != "pre"
 
 
 class Bucket:
-    __slots__ = ("names", "lo", "hi", "pending", "issued", "busy", "stepped", "free_ev")
+    __slots__ = ("names", "lo", "hi", "pending", "issued", "busy", "stepped", "free_ev", "free_sig")
 
     def __init__(self, names: List[str], lo: int, hi: int):
         self.names = list(names)
@@ -55,6 +55,7 @@ class Bucket:
         self.issued = False         # collective enqueued
         self.stepped = False        # optimizer step of this slice enqueued
         self.free_ev = None         # main-stream event after the last reader of the parameters
+        self.free_sig = None        # ... or a later main-stream kernel's start signal (flag, value)
 
     @property
     def numel(self):
@@ -173,6 +174,7 @@ class GradSync:
             b.busy = set(b.names)
             b.issued = False
             b.stepped = False
+            b.free_sig = None
 
     def grad_ready(self, names: List[str]):
         for n in names:
@@ -186,9 +188,10 @@ class GradSync:
                 self._issue(b)
             self._maybe_step(b)
 
-    def params_free(self, names: List[str]):
+    def params_free(self, names: List[str], signal=None):
         """Engine hook (main stream current): no kernel of this step still to be enqueued reads
-        these parameters."""
+        these parameters.  ``signal``: a kernel-start signal of a later main-stream kernel (engine
+        forward_backward); the update waits on it instead of an event recorded here."""
         if not self.fuse_step:
             return
         for n in names:
@@ -198,7 +201,8 @@ class GradSync:
             b.busy.discard(n)
             if b.busy:
                 continue
-            if b.free_ev is not None:
+            b.free_sig = signal
+            if b.free_ev is not None and signal is None:
                 b.free_ev.record(torch.cuda.current_stream(self.engine.device))
             self._maybe_step(b)
 
@@ -219,8 +223,8 @@ class GradSync:
             self.engine.sgd_step(scale, b.lo, b.numel)
             return
         self._join(s, torch.cuda.current_stream(self.engine.device))
-        b.free_ev.wait(s)
         with torch.cuda.stream(s):
+            self._wait_free(b)
             self.engine.sgd_step(scale, b.lo, b.numel)
 
     def _step_ready(self, b: Bucket) -> bool:
@@ -230,9 +234,15 @@ class GradSync:
         """The bucket's SGD on the current stream (the comm stream, inside a region), after the
         main-stream event that follows the last reader of its parameters."""
         b.stepped = True
-        if b.free_ev is not None:
-            b.free_ev.wait(torch.cuda.current_stream(self.engine.device))
+        self._wait_free(b)
         self.engine.sgd_step(self.grad_scale(), b.lo, b.numel)
+
+    def _wait_free(self, b: Bucket):
+        """Order the current stream after the last reader of b's parameters."""
+        if b.free_sig is not None:
+            self.engine.wait_signal(b.free_sig)
+        elif b.free_ev is not None:
+            b.free_ev.wait(torch.cuda.current_stream(self.engine.device))
 
     def _issue(self, b: Bucket):
         b.issued = True

@@ -479,6 +479,7 @@ def test_wgrad_stream_matches_single_stream(monkeypatch, impl):
         e.check_signals()
         if e.ksignal:
             assert e.ksig[1:].tolist() == [3] * (len(e.spec.convs) - 1)  # every side layer signalled 3 steps
+            assert e.bsig.tolist() == [3] * len(e.spec.convs)  # ... and every BN backward
         outs.append(e.params.flat.clone())
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], outs[2])
