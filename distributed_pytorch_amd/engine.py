@@ -217,7 +217,7 @@ class VGGEngine:
         self.bsig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None  # BN bwd starts
         self.ksig_tmo = torch.zeros(1, dtype=torch.int32, device=dev) if self.ksignal else None
         self._sig_epoch = 0
-        self.ksig_timeout_us = int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "2000000"))
+        self.ksig_timeout_us = int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "60000000"))
         # params_free hands the sync a later kernel's signal instead of recording an event (A/B: 0)
         self.free_signal = os.environ.get("DPA_FREE_SIGNAL", "1") == "1"
         self.slab = torch.empty(1, **f32)

@@ -246,6 +246,7 @@ def run(ctx: DistContext, mode: str, args):
         stopped = train_model(engine, train_loader, sync, epoch, ctx, args, start_batch=start_batch, stats=stats,
                               budget=budget)
         start_batch = 0
+        engine.check_signals()  # the epoch's cross-stream waits all saw their producers
         if budget is not None:
             budget -= stats.get("iters_run", 0)
         if stopped is not None:  # preempted mid-epoch: checkpoint the position, no eval
