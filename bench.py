@@ -55,7 +55,7 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (reference: 256 per node)")
     ap.add_argument("--mode", default="ddp", choices=["ddp", "allreduce", "gather", "zero1"])
     ap.add_argument("--model", default="VGG11")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"])
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--device", default="auto")
@@ -200,6 +200,7 @@ def main(argv=None):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     cw = benchlib.comm_world(ctx.comm)
+    checksum = float(engine.params.flat.double().sum().item())  # cross-mode oracle
 
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(ctx.world)
@@ -233,6 +234,7 @@ def main(argv=None):
             "comm_diag": diag,
             "vs_torch_eager_fp32": round(img_s / (TORCH_EAGER_IMG_S_PER_GPU * ctx.world), 3),
             "final_loss": round(loss, 4),
+            "param_checksum": checksum,
         }
         print(json.dumps(rec), flush=True)
     ctx.shutdown()

@@ -97,7 +97,12 @@ _TORCH_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.Re
 
 class TorchComm(Comm):
     """torch.distributed process group.  Every op waits on its Work right after issue: on GPU
-    (nccl) that is a device-side wait of the side stream, on CPU (gloo) a host wait."""
+    (nccl) that is a device-side wait of the side stream, on CPU (gloo) a host wait.
+
+    GPU tensors over a gloo group (``--comm gloo``: several ranks sharing one GPU, which RCCL does
+    not allow — the multi-rank rehearsal of the GPU engine on a one-GPU box) are staged through
+    host memory: the side stream is drained, the collective runs on a CPU copy, the result is
+    copied back on the side stream."""
 
     name = "torch"
 
@@ -107,6 +112,9 @@ class TorchComm(Comm):
         self.world = dist.get_world_size(group)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.stage = self.device.type == "cuda" and dist.get_backend(group) == "gloo"
+        if self.stage:
+            self.name = "gloo-staged"
         self._join_in = StreamJoin() if self.side is not None else None
         self._join_out = StreamJoin() if self.side is not None else None
 
@@ -123,7 +131,20 @@ class TorchComm(Comm):
         if work is not None:
             work.wait()
 
+    def _staged(self, fn, *ts):
+        """Run fn on host copies of ts (gloo + GPU tensors), then copy every result back."""
+        hs = [t.detach().cpu() for t in ts]  # drains the current (side) stream up to here
+        fn(*hs)
+        for t, h in zip(ts, hs):
+            t.copy_(h)
+
     def all_reduce(self, t, op="sum"):
+        if self.stage:
+            self._staged(lambda h: dist.all_reduce(h, dist.ReduceOp.SUM if op == "avg" else _TORCH_OPS[op],
+                                                   group=self.group), t)
+            if op == "avg":
+                t.div_(self.world)
+            return
         if op == "avg":
             self._w(dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group, async_op=True))
             t.div_(self.world)
@@ -131,14 +152,25 @@ class TorchComm(Comm):
         self._w(dist.all_reduce(t, _TORCH_OPS[op], group=self.group, async_op=True))
 
     def broadcast(self, t, root=0):
+        if self.stage:
+            self._staged(lambda h: dist.broadcast(h, src=root, group=self.group), t)
+            return
         self._w(dist.broadcast(t, src=root, group=self.group, async_op=True))
 
     def gather(self, send, recv, root=0):
+        if self.stage:
+            hs = send.detach().cpu()
+            hr = recv.detach().cpu() if self.rank == root else None
+            dist.gather(hs.view(-1), gather_list=list(hr.view(self.world, -1).unbind(0)) if hr is not None else None,
+                        dst=root, group=self.group)
+            if hr is not None:
+                recv.copy_(hr)
+            return
         gl = list(recv.view(self.world, -1).unbind(0)) if self.rank == root else None
         self._w(dist.gather(send.view(-1), gather_list=gl, dst=root, group=self.group, async_op=True))
 
     def reduce_scatter(self, send, recv, op="sum"):
-        if self.device.type == "cpu":  # gloo has no reduce_scatter: all_reduce a copy, keep own shard
+        if self.device.type == "cpu" or self.stage:  # gloo has no reduce_scatter: all_reduce a copy, keep own shard
             tmp = send.clone()
             self.all_reduce(tmp, op)
             recv.copy_(tmp.view(self.world, -1)[self.rank].view_as(recv))
@@ -146,6 +178,11 @@ class TorchComm(Comm):
         self._w(dist.reduce_scatter_tensor(recv, send, _TORCH_OPS[op], group=self.group, async_op=True))
 
     def all_gather(self, send, recv):
+        if self.stage:
+            hs, hr = send.detach().cpu(), recv.detach().cpu()
+            dist.all_gather(list(hr.view(self.world, -1).unbind(0)), hs.view(-1), group=self.group)
+            recv.copy_(hr)
+            return
         if self.device.type == "cpu":  # gloo: list form (send may alias its slot of recv)
             src = send.clone()
             self._w(dist.all_gather(list(recv.view(self.world, -1).unbind(0)), src.view(-1), group=self.group,

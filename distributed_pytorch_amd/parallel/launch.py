@@ -113,6 +113,10 @@ def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=Non
         if store is not None:
             raise RuntimeError("native rendezvous drives RCCL only: use DPA_RENDEZVOUS=torch (gloo) on CPU")
         return TorchComm(device=device)
+    if kind == "gloo":  # GPU tensors staged through gloo: several ranks may share one GPU (rehearsal)
+        if store is not None:
+            raise RuntimeError("--comm gloo needs the torch rendezvous")
+        return TorchComm(device=device)
     if kind == "torch":
         if store is not None:
             raise RuntimeError("--comm torch needs the torch rendezvous")

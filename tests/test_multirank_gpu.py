@@ -1,0 +1,56 @@
+"""Multi-rank rehearsal of the GPU training path on a one-GPU box.
+
+RCCL refuses two ranks on one GPU, so these runs put 2 ranks on the same device and move the
+gradients through gloo with host staging (``--comm gloo``, parallel/comm.py TorchComm).  Everything
+else is the multi-GPU code path of bench.py: the N-rank launcher (parallel/spawn.py), the engine's
+two-stream backward with kernel-start signals, the sync strategies (bucketed DDP / per-tensor
+all-reduce / gather-scatter / ZeRO-1) on a side stream, the per-bucket fused SGD and the
+cross-rank replica check.  Each mode must end with bit-identical parameters on both ranks, and —
+the reference's correctness oracle (the three modes give bit-identical parameters at
+the same seed) — every mode with the same parameters as every other: with two ranks a sum of two
+gradients and its halving are exact in any order."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODES = ["ddp", "allreduce", "gather", "zero1"]
+
+
+def _run(mode):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "gloo", "--mode", mode,
+           "--steps", "3", "--warmup", "2", "--solo-steps", "0", "--diag-steps", "1", "--launch-timeout", "100"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, r.stdout[-2000:]
+    return json.loads(lines[-1])
+
+
+@pytest.fixture(scope="module")
+def runs():
+    return {}
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_two_ranks_share_one_gpu(runs, mode):
+    d = _run(mode)
+    runs[mode] = d
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2", d
+    assert d["config"]["sync_mode"] == mode, d
+    assert d["replicas_identical"] is True and d["replica_param_max_diff"] == 0.0, d
+    assert d["value"] > 0 and d["final_loss"] == d["final_loss"], d
+
+
+def test_modes_agree_bitwise(runs):
+    if len(runs) < len(MODES):
+        pytest.skip("needs every mode's run")
+    sums = {m: runs[m]["param_checksum"] for m in MODES}
+    assert len(set(sums.values())) == 1, sums
