@@ -54,3 +54,29 @@ def test_modes_agree_bitwise(runs):
         pytest.skip("needs every mode's run")
     sums = {m: runs[m]["param_checksum"] for m in MODES}
     assert len(set(sums.values())) == 1, sums
+
+
+def test_four_ranks_ddp_share_one_gpu():
+    """W = 4 (bucket all-reduce of four contributions, 1/W folded into the update)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--comm", "gloo", "--mode", "ddp",
+           "--steps", "2", "--warmup", "1", "--solo-steps", "0", "--diag-steps", "0", "--batch", "64",
+           "--launch-timeout", "100"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 4 and d["replicas_identical"] is True, d
+
+
+def test_resnet_generic_ddp_two_ranks():
+    """The generic path (autograd + hook DDP over the flat arena, parallel/ddp.py) with a real
+    communicator: ResNet-50 at a small batch and image size, replicas bitwise identical."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench_resnet.py"), "--gpus", "2", "--comm", "gloo", "--steps", "2",
+           "--warmup", "1", "--batch", "8", "--image", "64", "--launch-timeout", "100"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["replicas_identical"] is True, d
