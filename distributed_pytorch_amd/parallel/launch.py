@@ -100,6 +100,28 @@ def _native_store(host: str, port: int, rank: int, world: int) -> NativeStore:
     return NativeStore(host, port, rank, world, timeout_s=_timeout().total_seconds())
 
 
+def native_store_from_env(rank: int, world: int) -> NativeStore:
+    """The native rendezvous store of an env:// job.  Its port:
+    * ``DPA_STORE_PORT`` when set (the framework's own launcher picks a free one);
+    * under torchrun (``TORCHELASTIC_USE_AGENT_STORE=True``): rank 0 binds an ephemeral port and
+      publishes it through the elastic agent's store at MASTER_PORT — one key, read by the other
+      ranks; no process group is created — so a busy neighbouring port cannot break the job;
+    * otherwise MASTER_PORT + 1."""
+    host = os.environ["MASTER_ADDR"]
+    if "DPA_STORE_PORT" in os.environ:
+        return _native_store(host, int(os.environ["DPA_STORE_PORT"]), rank, world)
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+        agent = dist.TCPStore(host, int(os.environ["MASTER_PORT"]), None, False, _timeout())
+        key = "dpa/native_store_port/{}/{}".format(os.environ.get("TORCHELASTIC_RUN_ID", "run"),
+                                                   os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if rank == 0:
+            st = _native_store(host, 0, rank, world)
+            agent.set(key, str(st.port))
+            return st
+        return _native_store(host, int(agent.get(key).decode()), rank, world)
+    return _native_store(host, int(os.environ["MASTER_PORT"]) + 1, rank, world)
+
+
 def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=None) -> Comm:
     if world == 1:
         # DPA_FORCE_COMM=1 runs the real RCCL communicator even on one GPU (a 1-rank communicator:
@@ -172,8 +194,7 @@ def init_env(device: str = "auto", comm: str = "rccl") -> DistContext:
     init, store = False, None
     if world > 1:
         if _rendezvous(dev, comm) == "native":
-            port = int(os.environ.get("DPA_STORE_PORT", int(os.environ["MASTER_PORT"]) + 1))
-            store = _native_store(os.environ["MASTER_ADDR"], port, rank, world)
+            store = native_store_from_env(rank, world)
         else:
             dist.init_process_group(backend="gloo", init_method="env://", timeout=_timeout())
             init = True

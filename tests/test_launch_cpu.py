@@ -98,3 +98,41 @@ def test_bench_self_launch_two_ranks_cpu():
     assert rec["config"]["global_batch"] == 8
     assert rec["replicas_identical"] is True and rec["rccl_world"] == 2
     assert rec["scaling_efficiency"] is not None and rec["value"] > 0
+
+
+def test_native_store_port_via_torchrun_agent_store(tmp_path):
+    """Under torchrun the native store's port is published through the elastic agent's store (a
+    TCPStore at MASTER_PORT): rank 0 binds an ephemeral port, the others read it."""
+    import torch.distributed as dist
+
+    from distributed_pytorch_amd import _ext
+
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    port = spawn.free_port()
+    agent = dist.TCPStore("127.0.0.1", port, None, True)  # stands in for the torchrun agent's store
+    out = tmp_path / "out"
+    out.mkdir()
+    s = _script(tmp_path, f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        from distributed_pytorch_amd.parallel.launch import native_store_from_env
+        r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+        st = native_store_from_env(r, w)
+        st.set(f"k{{r}}", str(r * 10))
+        st.barrier("b")
+        vals = [int(st.get(f"k{{q}}")) for q in range(w)]
+        open(os.path.join({str(out)!r}, f"{{r}}.txt"), "w").write(f"{{st.port}} {{vals}}")
+        st.close()
+        """)
+    env = {"TORCHELASTIC_USE_AGENT_STORE": "True", "TORCHELASTIC_RUN_ID": "t1", "MASTER_PORT": str(port)}
+    procs = []
+    for r in range(3):
+        e = dict(os.environ, RANK=str(r), WORLD_SIZE="3", MASTER_ADDR="127.0.0.1", **env)
+        e.pop("DPA_STORE_PORT", None)
+        procs.append(subprocess.Popen([sys.executable, s], env=e))
+    assert all(p.wait(timeout=120) == 0 for p in procs)
+    res = [(out / f"{r}.txt").read_text().split(" ", 1) for r in range(3)]
+    assert len({p for p, _ in res}) == 1 and int(res[0][0]) not in (port, port + 1)
+    assert all(v == "[0, 10, 20]" for _, v in res)
+    del agent

@@ -80,3 +80,20 @@ def test_resnet_generic_ddp_two_ranks():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["replicas_identical"] is True, d
+
+
+def test_torchrun_launch_two_ranks():
+    """The driver's launch form: torch.distributed.run --nproc-per-node 2 ... bench.py --gpus 2."""
+    from distributed_pytorch_amd.parallel.spawn import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm",
+           "gloo", "--steps", "3", "--warmup", "1", "--solo-steps", "2", "--diag-steps", "1"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPA_STORE_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["config"]["launcher"] == "torchrun" and d["replicas_identical"] is True, d
+    assert d["solo_img_s"] and d["scaling_efficiency"] is not None, d
