@@ -334,10 +334,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c4 = (int)(i % C4);
-    const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
-    const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
+  auto body = [&](long i, int c4, float4 sc, float4 sh) {
     if (!POOL) {
       if constexpr (ACT == 0) {
         store4<NP>(a, a3, ps, i, affine_relu(ld4(z, i), sc, sh));
@@ -352,11 +349,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
         store4<NP>(a, a3, ps, i, u);
       }
     } else {
-      long t = i / C4;
-      const int ow = (int)(t % Wo);
-      t /= Wo;
-      const int oh = (int)(t % Ho);
-      const int n = (int)(t / Ho);
+      const unsigned t = (unsigned)(i / C4);  // pooled pixel (VGG sizes: < 2^32)
+      const unsigned ow = t % (unsigned)Wo, t2 = t / (unsigned)Wo;
+      const unsigned oh = t2 % (unsigned)Ho, n = t2 / (unsigned)Ho;
       const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * C4 + c4;
       const float4 v00 = affine_relu(ld4(z, base), sc, sh);
       const float4 v01 = affine_relu(ld4(z, base + C4), sc, sh);
@@ -367,6 +362,18 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
                              fmaxf(fmaxf(v00.y, v01.y), fmaxf(v10.y, v11.y)),
                              fmaxf(fmaxf(v00.z, v01.z), fmaxf(v10.z, v11.z)),
                              fmaxf(fmaxf(v00.w, v01.w), fmaxf(v10.w, v11.w))));
+    }
+  };
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (stride % C4 == 0) {  // every element of this thread has the same channel group (launcher's grid)
+    const int c4 = (int)(i0 % C4);
+    const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
+    const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
+    for (long i = i0; i < total; i += stride) body(i, c4, sc, sh);
+  } else {
+    for (long i = i0; i < total; i += stride) {
+      const int c4 = (int)(i % C4);
+      body(i, c4, reinterpret_cast<const float4*>(scale)[c4], reinterpret_cast<const float4*>(shift)[c4]);
     }
   }
 }
@@ -428,7 +435,32 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
       const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
       const float4 mu = reinterpret_cast<const float4*>(mean)[c4];
       const float4 is = reinterpret_cast<const float4*>(invstd)[c4];
-      for (int r = r0 + lane_r; r < r1; r += gg.RPI) {
+      int r = r0 + lane_r;
+      // two rows' loads in flight: the 1024-thread geometry of large tensors (ResNet-50, +6 %);
+      // the 256-thread blocks that run beside the VGG weight-gradient convs keep one row
+      if (RTB == RT && !POOL && nsplit == 1) {
+        for (; r + gg.RPI < r1; r += 2 * gg.RPI) {
+          const long gi0 = (long)r * gg.C4 + c4, gi1 = gi0 + (long)gg.RPI * gg.C4;
+          const float4 g0 = ld4(gsrc, gi0), g1 = ld4(gsrc, gi1);
+          const float4 z0 = ld4(z, gi0), z1 = ld4(z, gi1);
+          const float4 r0v = ACT == 2 ? ld4(res, gi0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 r1v = ACT == 2 ? ld4(res, gi1) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float za = F4GET(z0, k), zb = F4GET(z1, k);
+            const float dya = act_grad<ACT>(fmaf(za, F4GET(sc, k), F4GET(sh, k)), F4GET(r0v, k), F4GET(g0, k));
+            const float dyb = act_grad<ACT>(fmaf(zb, F4GET(sc, k), F4GET(sh, k)), F4GET(r1v, k), F4GET(g1, k));
+            const float xa = (za - F4GET(mu, k)) * F4GET(is, k), xb = (zb - F4GET(mu, k)) * F4GET(is, k);
+            sdy[k] += dya;
+            sdx[k] = fmaf(dya, xa, sdx[k]);
+            sx[k] += xa;
+            sdy[k] += dyb;
+            sdx[k] = fmaf(dyb, xb, sdx[k]);
+            sx[k] += xb;
+          }
+        }
+      }
+      for (; r < r1; r += gg.RPI) {
         const long gi = (long)r * gg.C4 + c4;
         float4 gv = ld4(gsrc, gi);
         for (int s = 1; s < nsplit; ++s) gv = f4add(gv, ld4(gsrc, s * slab4 + gi));
@@ -562,13 +594,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c4 = (int)(i % C4);
-    const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
-    const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
-    const float4 k1 = reinterpret_cast<const float4*>(coef)[c4];
-    const float4 k2 = reinterpret_cast<const float4*>(coef + C)[c4];
-    const float4 k3 = reinterpret_cast<const float4*>(coef + 2 * C)[c4];
+  struct Co {
+    float4 sc, sh, k1, k2, k3;
+  };
+  auto coefs = [&](int c4) {
+    return Co{reinterpret_cast<const float4*>(scale)[c4], reinterpret_cast<const float4*>(shift)[c4],
+              reinterpret_cast<const float4*>(coef)[c4], reinterpret_cast<const float4*>(coef + C)[c4],
+              reinterpret_cast<const float4*>(coef + 2 * C)[c4]};
+  };
+  auto body = [&](long i, int c4, const Co& q) {
     const float4 gv = ld4(g, i);
     if (!POOL) {
       const float4 zv = ld4(z, i);
@@ -577,34 +611,45 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float zz = F4GET(zv, k);
-        const float dy = act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv, k), F4GET(gv, k));
+        const float dy = act_grad<ACT>(fmaf(zz, F4GET(q.sc, k), F4GET(q.sh, k)), F4GET(rv, k), F4GET(gv, k));
         dyv[k] = dy;
-        r[k] = F4GET(k1, k) * dy + F4GET(k2, k) * zz + F4GET(k3, k);
+        r[k] = F4GET(q.k1, k) * dy + F4GET(q.k2, k) * zz + F4GET(q.k3, k);
       }
       store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]));
       if constexpr (ACT == 2) st4(dres, i, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
     } else {
-      long t = i / C4;
-      const int ow = (int)(t % Wo);
-      t /= Wo;
-      const int oh = (int)(t % Ho);
-      const int n = (int)(t / Ho);
+      const unsigned t = (unsigned)(i / C4);  // pooled pixel (VGG sizes: < 2^32)
+      const unsigned ow = t % (unsigned)Wo, t2 = t / (unsigned)Wo;
+      const unsigned oh = t2 % (unsigned)Ho, n = t2 / (unsigned)Ho;
       const long base = (((long)n * H + 2 * oh) * W + 2 * ow) * C4 + c4;
       const long idx[4] = {base, base + C4, base + (long)W * C4, base + (long)W * C4 + C4};
       float4 zq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) zq[q] = ld4(z, idx[q]);
+      for (int u = 0; u < 4; ++u) zq[u] = ld4(z, idx[u]);
       float out[4][4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float d[4];
-        route1(F4GET(zq[0], k), F4GET(zq[1], k), F4GET(zq[2], k), F4GET(zq[3], k), F4GET(sc, k), F4GET(sh, k),
+        route1(F4GET(zq[0], k), F4GET(zq[1], k), F4GET(zq[2], k), F4GET(zq[3], k), F4GET(q.sc, k), F4GET(q.sh, k),
                F4GET(gv, k), d[0], d[1], d[2], d[3]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) out[q][k] = F4GET(k1, k) * d[q] + F4GET(k2, k) * F4GET(zq[q], k) + F4GET(k3, k);
+        for (int u = 0; u < 4; ++u)
+          out[u][k] = F4GET(q.k1, k) * d[u] + F4GET(q.k2, k) * F4GET(zq[u], k) + F4GET(q.k3, k);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) store4<NP>(dz, dz3, ps, idx[q], make_float4(out[q][0], out[q][1], out[q][2], out[q][3]));
+      for (int u = 0; u < 4; ++u)
+        store4<NP>(dz, dz3, ps, idx[u], make_float4(out[u][0], out[u][1], out[u][2], out[u][3]));
+    }
+  };
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (stride % C4 == 0) {  // every element of this thread has the same channel group (launcher's grid)
+    const int c4 = (int)(i0 % C4);
+    const Co q = coefs(c4);
+    for (long i = i0; i < total; i += stride) body(i, c4, q);
+  } else {
+    for (long i = i0; i < total; i += stride) {
+      const int c4 = (int)(i % C4);
+      body(i, c4, coefs(c4));
     }
   }
 }
@@ -613,6 +658,18 @@ int grid_1d(long n) {
   long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
   return (int)(g < 1 ? 1 : g);
+}
+
+// grid for a channel-interleaved elementwise pass over n float4 groups of C4 channel groups: when
+// the grid is capped, round it so the grid stride is a multiple of C4 (each thread then keeps one
+// channel group: per-channel coefficients loaded once, no 64-bit modulo per element)
+int grid_ch(long n, int C4) {
+  int g = grid_1d(n);
+  if ((long)g * 256 < n && C4 > 256 && C4 % 256 == 0) {
+    const int m = C4 / 256;
+    g = (g + m - 1) / m * m;
+  }
+  return g;
 }
 
 
@@ -650,7 +707,7 @@ int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, co
                   int C, int pool, int act, const TZ* res, hipStream_t st) {
   const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   const long ps = total * 4;
-  const int grid = grid_1d(total);
+  const int grid = grid_ch(total, C / 4);
   if (pool) {
     if (np == 0) bn_apply_launch<true, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
     else if (np == 1) bn_apply_launch<true, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
@@ -874,7 +931,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
   const TZ* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
   const long ps = (long)N * H * W * C;
-  const int grid = grid_1d(total);
+  const int grid = grid_ch(total, C / 4);
 #define BAP(P, NPT) bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C)
   if (pool) {
     if (np == 0) BAP(true, 0);

@@ -106,6 +106,41 @@ def test_bn_backward(shape):
     assert out[2].abs().max().item() < 1e-3 * ref[0].abs().max().item() + 1e-4  # dbias ~ 0
 
 
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_bn_backward_wide_geometry(act):
+    """BN backward of a tensor large enough for the 1024-thread reduce geometry (> 3M float4 lanes,
+    ResNet-50-sized: two rows' loads in flight), activation/residual variants, vs the fp32 reference."""
+    C_ = _C()
+    N, H, W, C = 16, 56, 56, 256
+    g = torch.Generator().manual_seed(11 + act)
+    z = torch.randn(N, H, W, C, generator=g)
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.5
+    mean, invstd = z.reshape(-1, C).mean(0), torch.rsqrt(z.reshape(-1, C).var(0, unbiased=False) + 1e-5)
+    scale, shift = gamma * invstd, beta - mean * gamma * invstd
+    gout = torch.randn(N, H, W, C, generator=g)
+    res = torch.randn(N, H, W, C, generator=g) if act == 2 else None
+    ref = [torch.zeros(C) for _ in range(3)]
+    dz_ref = torch.empty_like(z)
+    dres_ref = torch.empty_like(z) if act == 2 else None
+    cpu_ref.bn_bwd(gout, 1, gout, z, scale, shift, mean, invstd, gamma, None, None, ref[0], ref[1], ref[2], dz_ref,
+                   False, act, res, dres_ref)
+    d = lambda t: t.cuda()
+    part = torch.zeros(C_.bn_part_floats(N * H * W, C, True), device="cuda")
+    coef = torch.empty(3 * C, device="cuda")
+    out = [torch.zeros(C, device="cuda") for _ in range(3)]
+    dz = torch.empty(z.shape, device="cuda")
+    dres = torch.empty(z.shape, device="cuda") if act == 2 else None
+    gd = d(gout)
+    C_.bn_bwd(gd, 1, gd, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, out[0], out[1], out[2],
+              dz, False, act, d(res) if res is not None else None, dres)
+    torch.cuda.synchronize()
+    close(dz, dz_ref, 2e-5)
+    close(out[0], ref[0], 2e-5)
+    close(out[1], ref[1], 2e-5)
+    if act == 2:
+        close(dres, dres_ref, 1e-6)
+
+
 def test_bn_backward_matches_torch_autograd():
     """End-to-end oracle: torch's own BatchNorm2d(train)+ReLU+MaxPool backward (fp64)."""
     C_ = _C()
