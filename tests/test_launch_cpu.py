@@ -136,3 +136,36 @@ def test_native_store_port_via_torchrun_agent_store(tmp_path):
     assert len({p for p, _ in res}) == 1 and int(res[0][0]) not in (port, port + 1)
     assert all(v == "[0, 10, 20]" for _, v in res)
     del agent
+
+
+def test_native_store_under_real_torchrun(tmp_path):
+    """The same exchange under an actual torch.distributed.run launch (static rendezvous, the
+    driver's form): the elastic agent's store is reachable at MASTER_PORT and every rank gets the
+    native store."""
+    from distributed_pytorch_amd import _ext
+
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    out = tmp_path / "out"
+    out.mkdir()
+    s = _script(tmp_path, f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        from distributed_pytorch_amd.parallel.launch import native_store_from_env
+        r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+        assert os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True", dict(os.environ)
+        st = native_store_from_env(r, w)
+        st.set(f"k{{r}}", str(r + 1))
+        st.barrier("b")
+        tot = sum(int(st.get(f"k{{q}}")) for q in range(w))
+        open(os.path.join({str(out)!r}, f"{{r}}.txt"), "w").write(str(tot))
+        st.close()
+        """)
+    env = dict(os.environ)
+    for k in ("DPA_STORE_PORT", "WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(spawn.free_port()), s]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert [(out / f"{q}.txt").read_text() for q in range(3)] == ["6", "6", "6"]
