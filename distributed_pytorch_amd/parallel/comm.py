@@ -34,7 +34,10 @@ class Comm:
     name = "base"
 
     @contextlib.contextmanager
-    def region(self):
+    def region(self, join: bool = True):
+        """Collectives issued inside run on the communicator's stream, ordered after the work
+        queued so far on the current stream (``join=False``: the caller orders them itself, e.g.
+        with a kernel-start signal wait issued first inside the region)."""
         yield
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
@@ -119,11 +122,12 @@ class TorchComm(Comm):
         self._join_out = StreamJoin() if self.side is not None else None
 
     @contextlib.contextmanager
-    def region(self):
+    def region(self, join: bool = True):
         if self.side is None:
             yield
             return
-        self._join_in(self.side, torch.cuda.current_stream(self.device))
+        if join:
+            self._join_in(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             yield
 
@@ -249,8 +253,9 @@ class RcclComm(Comm):
         self._store = store
 
     @contextlib.contextmanager
-    def region(self):
-        self._join_in(self.stream, torch.cuda.current_stream(self.device))
+    def region(self, join: bool = True):
+        if join:
+            self._join_in(self.stream, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             yield
 

@@ -42,6 +42,7 @@ from .comm import Comm
 
 # DPA_BUF_BCAST=pre restores the per-forward buffer broadcast of torch DDP (A/B); default post
 _POST_FORWARD_BUFFERS = os.environ.get("DPA_BUF_BCAST", "post") != "pre"
+_SIGNAL_BUFFERS = os.environ.get("DPA_BUF_SIGNAL", "1") == "1"  # A/B switch (DDPSync)
 
 
 class Bucket:
@@ -340,6 +341,7 @@ class DDPSync(GradSync):
         self.broadcast_buffers = broadcast_buffers
         self._bufs_fresh = False  # replicas hold rank 0's running stats (sent after the last forward)
         self._bufs_sent = False   # ... sent during the current step
+        self._sig_bufs = False    # this step's broadcast waits on a kernel-start signal
 
     # DDP._sync_buffers (torch nn/parallel/distributed.py:2178): rank 0's BN running stats
     # overwrite every replica's before each training forward.  Nothing touches the running stats
@@ -348,19 +350,42 @@ class DDPSync(GradSync):
     # stream under the backward; the next forward then finds the replicas already in sync and
     # needs no stream hop.  The num_batches_tracked counters advance identically on every replica
     # after the start-up broadcast, so they are not re-sent.
-    def _send_buffers(self):
-        with self.comm.region():
+    #
+    # With the engine's kernel-start signals the broadcast waits on the signal that the first BN
+    # backward raises (forward and head complete) instead of an event recorded on the compute
+    # stream: it is issued from the first params_free that carries a signal (fc1 for VGG).
+    def _send_buffers(self, signal=None):
+        with self.comm.region(join=signal is None):
+            if signal is not None:
+                self.engine.wait_signal(signal)
             self.comm.broadcast(self.engine.buffers.flat, 0)
+        self._bufs_sent = self._bufs_fresh = True
+
+    def _post_forward_send(self) -> bool:
+        return self.active and self.broadcast_buffers and not self._bufs_sent and _POST_FORWARD_BUFFERS
 
     def begin_step(self):
         super().begin_step()
         self._bufs_sent = False
+        # a signal will come with the head's params_free (engine forward_backward, eager steps)
+        e = self.engine
+        self._sig_bufs = (_SIGNAL_BUFFERS and getattr(e, "ksignal", False) and getattr(e, "free_signal", False)
+                          and not torch.cuda.is_current_stream_capturing())
 
     def grad_ready(self, names: List[str]):
-        if self.active and self.broadcast_buffers and not self._bufs_sent and _POST_FORWARD_BUFFERS:
+        if self._post_forward_send() and not self._sig_bufs:
             self._send_buffers()  # the engine reports gradients only once the forward is done
-            self._bufs_sent = self._bufs_fresh = True
         super().grad_ready(names)
+
+    def params_free(self, names: List[str], signal=None):
+        if self._post_forward_send() and (signal is not None or not self._sig_bufs):
+            self._send_buffers(signal)
+        super().params_free(names, signal)
+
+    def finish(self) -> float:
+        if self._post_forward_send():  # no signal arrived (e.g. a caller without params_free)
+            self._send_buffers()
+        return super().finish()
 
     def pre_forward(self):
         if not self.active or not self.broadcast_buffers:
