@@ -635,6 +635,23 @@ class VGGEngine:
                 if grad_ready is not None:
                     grad_ready(nm)
 
+        joined = False
+
+        def drain_side():
+            """Before layer 0's gradients are reported from the main stream: layer 0 shares the last
+            bucket with layer 1, whose weight gradient runs on the wgrad stream, and the bucket's
+            collective is ordered after the stream that reports last.  Make the main stream wait
+            for the wgrad stream first (the end-of-backward join, moved up), so the collective sees
+            every producer of the bucket."""
+            nonlocal joined, side_later
+            if ws is None or joined:
+                return
+            if side_later is not None:
+                side_work(*side_later)
+                side_later = None
+            self._join(main, ws)
+            joined = True
+
         def after_bn(i: int):
             nonlocal free_later, side_later
             for nm in free_later:
@@ -658,6 +675,7 @@ class VGGEngine:
                                 G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], x, self.wpart,
                                 G[f"{l.conv_key}.weight"], **bsig)
                 after_bn(i)
+                drain_side()
                 if grad_ready is not None:
                     grad_ready(names)
                 if params_free is not None:
@@ -672,6 +690,8 @@ class VGGEngine:
                 # Layer 0's wgrad has nothing left to overlap with, so it stays on the main stream (a
                 # stream hop costs ~15 us on MI355X, tools/event_overhead.py)
                 self._conv_wgrad(i, x, n)
+                if i == 0:
+                    drain_side()
                 if grad_ready is not None:
                     grad_ready(names)
                 if i > 0:
@@ -717,7 +737,7 @@ class VGGEngine:
             params_free(nm)
         if side_later is not None:
             side_work(*side_later)
-        if ws is not None:
+        if ws is not None and not joined:
             self._join(main, ws)
         self._eval_dirty = True
         return self.loss
