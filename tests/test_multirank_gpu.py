@@ -97,3 +97,23 @@ def test_torchrun_launch_two_ranks():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["config"]["launcher"] == "torchrun" and d["replicas_identical"] is True, d
     assert d["solo_img_s"] and d["scaling_efficiency"] is not None, d
+
+
+def test_main_ddp_training_two_ranks(tmp_path):
+    """The reference's mode-C entry point (main_ddp.py under torchrun) trains on the GPU engine with
+    2 ranks: reference log lines, full-test-set evaluation on every rank, per-rank checkpoints."""
+    from distributed_pytorch_amd.parallel.spawn import free_port
+
+    ck = tmp_path / "ck"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "main_ddp.py"), "--comm", "gloo",
+           "--synthetic", "--train-size", "10240", "--test-size", "1024", "--checkpoint-dir", str(ck)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPA_STORE_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert out.count("Epoch: 1, Iteration: 1-20, Average Loss:") == 2, out[-3000:]  # 20 iterations per rank
+    assert out.count("Test set: Average loss:") == 2 and "/1024 (" in out, out[-3000:]
+    assert (ck / "rank0.pt").exists() and (ck / "rank1.pt").exists()
