@@ -306,6 +306,58 @@ def test_engine_step_matches_torch(impl):
             close(sd[k], v, 1e-4)
 
 
+def test_engine_trajectory_tracks_fp64():
+    """Eight SGD steps (lr 0.1, momentum 0.9, wd 1e-4) of the x3 engine vs torch fp64 autograd +
+    torch.optim.SGD from the same weights on the same batches: the loss trajectory and the final
+    parameters stay within a small factor of stock torch fp32's own distance from fp64."""
+    from distributed_pytorch_amd.engine import VGGEngine
+    from distributed_pytorch_amd.models import VGG11
+
+    torch.manual_seed(3)
+    ref = VGG11().double()
+    sd0 = {k: v.clone() for k, v in ref.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    N, S = 64, 8
+    xs = [torch.randn(N, 3, 32, 32, generator=g, dtype=torch.float64) for _ in range(S)]
+    ts = [torch.randint(0, 10, (N,), generator=g) for _ in range(S)]
+
+    def torch_run(dtype, dev):
+        m = VGG11().to(dev, dtype)
+        m.load_state_dict({k: v.to(dtype) if v.is_floating_point() else v for k, v in sd0.items()})
+        opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        losses = []
+        for x, t in zip(xs, ts):
+            opt.zero_grad()
+            loss = F.cross_entropy(m(x.to(dev, dtype)), t.to(dev))
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+        return losses, {n: p.detach().double().cpu() for n, p in m.named_parameters()}
+
+    l64, p64 = torch_run(torch.float64, "cpu")
+    l32, p32 = torch_run(torch.float32, "cpu")
+    e = VGGEngine("VGG11", "cuda", max_batch=N, impl="x3", lr=0.1)
+    e.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in sd0.items()})
+    le = []
+    for x, t in zip(xs, ts):
+        x4 = torch.zeros(N, 32, 32, 4)
+        x4[..., :3] = x.float().permute(0, 2, 3, 1)
+        e.forward_backward(x4.cuda(), t.cuda())
+        e.sgd_step()
+        e.finish_step()
+        le.append(float(e.loss.item()))
+    pe = {n: e._to_torch_layout(n, e.params[n]).cpu().double() for n in p64}
+
+    def dist(p):
+        num = sum(float((p[n] - p64[n]).norm() ** 2) for n in p64) ** 0.5
+        return num / sum(float(v.norm() ** 2) for v in p64.values()) ** 0.5
+
+    d32, de = dist(p32), dist(pe)
+    assert de <= 4.0 * d32 + 1e-6, (de, d32)
+    for a, b, c in zip(le, l32, l64):
+        assert abs(a - c) <= 4.0 * abs(b - c) + 1e-4 * abs(c), (le, l32, l64)
+
+
 @pytest.mark.parametrize("impl", ["fp32", "x3", "bf16"])
 def test_engine_training_converges_and_evaluates(impl):
     """A few steps on a learnable synthetic set: loss goes down, eval runs, x3 tracks fp32 closely."""
