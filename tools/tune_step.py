@@ -12,7 +12,12 @@ the lowest whole-step time (median of ``--reps`` runs of ``--steps`` steps).  A 
 by ``--min-gain`` (relative) to replace the current choice.  The result is merged into
 distributed_pytorch_amd/tuning/mi355x.json ([tile, splits, posmajor, isolated_ms]).
 
-    python tools/tune_step.py [--batch 256] [--impl x3] [--top 5] [--kinds wgrad,dgrad,fprop]
+    python tools/tune_step.py [--batch 256] [--impl x3] [--top 5] [--kinds wgrad,dgrad,fprop] [--per-split]
+
+``--per-split``: the candidates of a call are the fastest isolated configuration of EVERY split-K
+count instead of the ``--top`` fastest overall.  The isolated ranking favours many splits (short
+conv, long slab reduction); on the weight-gradient stream, which shares the chip with the critical
+path, a configuration with fewer splits can win in the step although it loses alone.
 """
 import argparse
 import json
@@ -87,6 +92,8 @@ def main():
     ap.add_argument("--kinds", default="wgrad,dgrad,fprop")
     ap.add_argument("--out", default=os.path.join(ROOT, "distributed_pytorch_amd", "tuning", "mi355x.json"))
     ap.add_argument("--dry-run", action="store_true", help="report, do not write the table")
+    ap.add_argument("--per-split", action="store_true",
+                    help="candidates: the fastest isolated config of every split count (not the --top overall)")
     a = ap.parse_args()
     args = bench.parse(["--batch", str(a.batch), "--impl", a.impl])
     dev = torch.device("cuda", 0)
@@ -111,7 +118,15 @@ def main():
         i0 = layers[0]
         cands = isolated(engine, i0, kind, n)
         cur = engine.conv_config(i0, kind, n)
-        top = [c for _, c in cands[: a.top] if c != cur]
+        if a.per_split:
+            seen, top = set(), []
+            for _, c in cands:  # fastest first: keep the best config of each split count
+                if c[1] not in seen:
+                    seen.add(c[1])
+                    if c != cur:
+                        top.append(c)
+        else:
+            top = [c for _, c in cands[: a.top] if c != cur]
         iso = {c: ms for ms, c in cands}
         cur_ms = step_ms(step, a.steps, a.reps)
         best, best_ms = cur, cur_ms
