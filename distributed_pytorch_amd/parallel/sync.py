@@ -21,13 +21,12 @@ Differences from the reference, all by design:
   exposed tail after backward is short) instead of DDP's 25 MiB/1 MiB;
 * all modes broadcast rank 0's parameters (and momenta, when resuming) once at start (SURVEY
   §5.4), so replicas cannot silently fork; BN buffers only in the modes that share them (ddp/zero1);
-* the optimizer step is fused per bucket into backward (``overlap=True``): once a bucket's
-  collective is issued AND the engine reports its parameters no longer read this step
+* optionally (``DPA_FUSED_STEP=1``) the optimizer step is fused per bucket into backward: once a
+  bucket's collective is issued AND the engine reports its parameters no longer read this step
   (``params_free``: dgrad of that layer enqueued), the fused SGD of that slice is queued behind the
-  collective on the comm stream.  The big late-layer
-  weights are updated while the early layers' backward still runs, so what is left after backward
-  is only the small tail bucket's collective and update.  Per-element SGD math is unchanged, so
-  results are bitwise identical to one SGD launch after ``finish()``.
+  collective on the comm stream, so only the small tail bucket's collective and update follow
+  backward.  Per-element SGD math is unchanged, so results are bitwise identical to the default
+  single SGD launch after ``finish()`` — which measures faster on MI355X (see GradSync).
 """
 from __future__ import annotations
 
@@ -123,10 +122,13 @@ class GradSync:
         self.world = comm.world
         self.active = comm.name != "null"  # a real communicator (also a forced 1-rank one)
         self.overlap = overlap
-        # DPA_FUSED_STEP: auto (default: with a real communicator, where the update hides behind the
-        # collectives of later buckets; for a lone rank the extra stream hops cost more than the
-        # ~40 us update they would hide, measured on MI355X) | 1 (always) | 0 (never)
-        fused = os.environ.get("DPA_FUSED_STEP", "auto")
+        # DPA_FUSED_STEP: 0 (default: one SGD over the arena after backward) | 1 (per-bucket SGD
+        # inside backward) | auto (per bucket with a real communicator).  Re-measured on MI355X after
+        # the kernel-start-signal changes (1-rank RCCL, interleaved pairs): the per-bucket updates on
+        # the comm stream delay the critical-path kernels by more than the ~32 us of update they
+        # take off the tail: DDP 166.5k vs 168.0k img/s, per-tensor all-reduce mode (34 buckets)
+        # 114-125k vs 154k (docs/PERF_NOTES.md).
+        fused = os.environ.get("DPA_FUSED_STEP", "0")
         self.fuse_step = overlap and self.fusable_step and (fused == "1" or (fused == "auto" and self.active))
         self._cuda = engine.device.type == "cuda"
         order = [["fc1.weight", "fc1.bias"]] + [

@@ -403,9 +403,12 @@ def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatc
     ts = [torch.randint(0, 10, (32,), generator=g) for _ in range(3)]
     outs = []
     # null comm with the update after backward, null comm with the per-bucket update fused into
-    # backward (wgrad stream), 1-rank RCCL with the fused update on the comm stream
-    runs = [(NullComm(), "0"), (NullComm(), "1"), (RcclComm(0, 1, dev, uid=C.rccl_unique_id()), "1")]
+    # backward (wgrad stream), 1-rank RCCL with the fused update on the comm stream, and 1-rank RCCL
+    # with the default single update after backward
+    runs = [(NullComm(), "0"), (NullComm(), "1"), (RcclComm(0, 1, dev, uid=C.rccl_unique_id()), "1"),
+            (lambda: RcclComm(0, 1, dev, uid=C.rccl_unique_id()), "0")]
     for comm, fused in runs:
+        comm = comm() if callable(comm) else comm
         monkeypatch.setenv("DPA_FUSED_STEP", fused)
         e = VGGEngine("VGG11", dev, max_batch=32, impl="x3", lr=0.01)
         e.init_parameters(seed=3)
@@ -422,7 +425,7 @@ def test_sync_modes_through_native_rccl_single_rank(mode, debug_sync, monkeypatc
         comm.check()
         outs.append(e.params.flat.clone())
         comm.close()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
 def test_bn_reductions_bitwise_reproducible():
