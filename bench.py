@@ -72,6 +72,11 @@ def parse(argv=None):
                          "min(steps, 30))")
     ap.add_argument("--diag-steps", type=int, default=5,
                     help="diagnostic steps after the timed region (exposed comm / per-bucket times; 0 = off)")
+    ap.add_argument("--comm-tune", default="auto", choices=["auto", "off"],
+                    help="N>1, ddp/allreduce modes: in the warmup, time a few gradient-sync plans (bucket size, "
+                         "tail bucket, per-bucket update inside backward) on the real fabric and keep the fastest "
+                         "(max over ranks, so every rank picks the same plan); off = --bucket-mb / defaults")
+    ap.add_argument("--comm-tune-steps", type=int, default=8, help="timed steps per plan and repetition")
     ap.add_argument("--profile", action="store_true",
                     help="re-run this command under rocprofv3 --kernel-trace --stats (prints the command)")
     ap.add_argument("--profile-dir", default="gpurun_out/prof")
@@ -80,6 +85,13 @@ def parse(argv=None):
 
 
 def build(a, dev, rank, world, comm):
+    engine, sync, batches = build_parts(a, dev, rank, world, comm)
+    return engine, sync, batches()
+
+
+def build_parts(a, dev, rank, world, comm):
+    """(engine, sync, batches): ``batches()`` starts a fresh endless iterator over the sharded
+    synthetic set (the warmup tuner draws its own, so the timed run sees the same data)."""
     train = synthetic_cifar(50000, 0)
     sampler = ShardSampler(len(train), world, rank, shuffle=True, seed=0)
     loader = DeviceLoader(train, a.batch, dev, sampler=sampler, train=True, seed=7919 + rank, drop_last=True)
@@ -94,7 +106,7 @@ def build(a, dev, rank, world, comm):
             yield from loader  # drop_last: every step has the full per-GPU batch
             ep += 1
 
-    return engine, sync, batches()
+    return engine, sync, batches
 
 
 def make_step(engine, sync, it, graphed=None, probe=None):
@@ -125,6 +137,77 @@ def make_step(engine, sync, it, graphed=None, probe=None):
 
     sync.finish = finish
     return step
+
+
+def comm_plans(a):
+    """Candidate gradient-sync plans (bucket_mb, tail_mb, per-bucket update) for the warmup tuner.
+    Per-tensor modes keep their granularity (the reference's semantics) and only try the update
+    placement; an explicit --bucket-mb pins the bucket size."""
+    fixed = a.bucket_mb
+    if a.mode == "ddp":
+        sizes = [fixed] if fixed is not None else [10.0, 25.0, 5.0]
+        plans = [(b, 2.0, False) for b in sizes] + [(sizes[0], 2.0, True), (sizes[0], 0.4, False)]
+    elif a.mode == "allreduce":
+        plans = [(fixed, 2.0, False), (fixed, 2.0, True)]
+    else:
+        plans = []
+    seen, out = set(), []
+    for p in plans:
+        if p not in seen:
+            seen.add(p)
+            out.append(p)
+    return out
+
+
+def tune_comm(a, engine, sync, ctx, dev, batches):
+    """Warmup-phase choice among ``comm_plans``: each plan runs ``--comm-tune-steps`` steps per
+    repetition (2 repetitions, interleaved); the score of a plan is its best repetition's time,
+    each repetition's time being the max over ranks, so every rank picks the same plan.  Returns
+    (sync, report).  Gradient-sync plans change only where and when collectives and the update
+    run: the numerics of every plan are identical (bitwise, tests/test_multirank_gpu.py).  The
+    tuning steps draw their own batches and the training state is restored afterwards, so the
+    run that follows is the same as without tuning."""
+    plans = comm_plans(a)
+    if ctx.world <= 1 or a.comm_tune == "off" or len(plans) < 2 or a.no_overlap:
+        return sync, None
+    it = batches()
+    snap = [t.clone() for t in (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt,
+                                engine.loss_accum)]
+    steps_taken = engine.steps_taken
+    syncs = {}
+    for p in plans:
+        s = make_sync(a.mode, engine, ctx.comm, bucket_mb=p[0], overlap=True, broadcast_init=False, tail_mb=p[1])
+        s.fuse_step = p[2] and s.fusable_step
+        syncs[p] = s
+    n = max(1, a.comm_tune_steps)
+    score = {}
+    for _rep in range(2):
+        for p in plans:
+            step = make_step(engine, syncs[p], it)
+            for _ in range(2):
+                step()
+            benchlib.device_barrier(ctx, dev)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                step()
+            benchlib.device_barrier(ctx, dev)
+            el = ctx.all_max(time.perf_counter() - t0) / n * 1e3
+            score[p] = min(score.get(p, el), el)
+    best = min(plans, key=lambda p: score[p])
+    benchlib.device_barrier(ctx, dev)
+    for dst, src in zip((engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt, engine.loss_accum),
+                        snap):
+        dst.copy_(src)
+    engine.steps_taken = steps_taken
+    engine.refresh_weight_planes()
+    engine._eval_dirty = True
+    for sy in syncs.values():
+        if hasattr(sy, "_bufs_fresh"):
+            sy._bufs_fresh = False  # the next forward broadcasts rank 0's (restored) buffers again
+    report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2]},
+              "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}": round(score[p], 4)
+                              for p in plans}}
+    return syncs[best], report
 
 
 def solo_phase(a, dev, steps, warmup):
@@ -171,7 +254,9 @@ def main(argv=None):
             solo_img_s = solo_phase(a, dev, solo_steps, min(a.warmup, 5))
         ctx.barrier()
 
-    engine, sync, it = build(a, dev, ctx.rank, ctx.world, ctx.comm)
+    engine, sync, batches = build_parts(a, dev, ctx.rank, ctx.world, ctx.comm)
+    sync, tune_report = tune_comm(a, engine, sync, ctx, dev, batches)
+    it = batches()
     graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
                if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
     el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev)
@@ -223,6 +308,7 @@ def main(argv=None):
             "config": {"model": a.model, "global_batch": a.batch * ctx.world, "seq_len": None, "image_size": 32,
                        "parallelism": f"dp{ctx.world}", "sync_mode": a.mode, "comm": ctx.comm.name,
                        "bucket_mb": [round(4 * b.numel / 2 ** 20, 3) for b in sync.buckets] if sync.active else None,
+                       "per_bucket_update": bool(sync.fuse_step), "comm_tune": tune_report,
                        "overlap": not a.no_overlap, "launcher": launcher,
                        "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
             "per_gpu_img_s": round(per_gpu, 1),

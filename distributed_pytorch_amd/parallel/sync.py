@@ -116,7 +116,8 @@ class GradSync:
     # each rank's own running stats (identical at a fresh start anyway: same seed, same init).
     shared_buffers = False
 
-    def __init__(self, engine, comm: Comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
+    def __init__(self, engine, comm: Comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True,
+                 tail_mb: float = 2.0):
         self.engine = engine
         self.comm = comm
         self.world = comm.world
@@ -134,7 +135,8 @@ class GradSync:
         order = [["fc1.weight", "fc1.bias"]] + [
             [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
             for l in reversed(engine.spec.convs)]
-        self.buckets = plan_buckets(engine.grads, order, bucket_mb)
+        self.bucket_mb, self.tail_mb = bucket_mb, tail_mb
+        self.buckets = plan_buckets(engine.grads, order, bucket_mb, tail_mb)
         self._by_name: Dict[str, Bucket] = {n: b for b in self.buckets for n in b.names}
         self._join = StreamJoin() if self._cuda else None
         if self._cuda:
@@ -296,8 +298,9 @@ class GatherScatterSync(GradSync):
 
     mode = "gather"
 
-    def __init__(self, engine, comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True):
-        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
+    def __init__(self, engine, comm, bucket_mb: float = 0.0, overlap: bool = True, broadcast_init: bool = True,
+                 tail_mb: float = 2.0):
+        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init, tail_mb)
         self._recv = None
         if comm.rank == 0 and self.active:
             mx = max(b.numel for b in self.buckets)
@@ -337,9 +340,9 @@ class DDPSync(GradSync):
     mode = "ddp"
 
     def __init__(self, engine, comm, bucket_mb: float = 10.0, overlap: bool = True, broadcast_init: bool = True,
-                 broadcast_buffers: bool = True):
+                 broadcast_buffers: bool = True, tail_mb: float = 2.0):
         self.shared_buffers = broadcast_buffers
-        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init)
+        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init, tail_mb)
         self.broadcast_buffers = broadcast_buffers
         self._bufs_fresh = False  # replicas hold rank 0's running stats (sent after the last forward)
         self._bufs_sent = False   # ... sent during the current step
@@ -415,8 +418,8 @@ class ZeroSync(DDPSync):
     fusable_step = False  # the update is sharded (owned slices after reduce-scatter, then all-gather)
 
     def __init__(self, engine, comm, bucket_mb: float = 10.0, overlap: bool = True, broadcast_init: bool = True,
-                 broadcast_buffers: bool = True):
-        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init, broadcast_buffers)
+                 broadcast_buffers: bool = True, tail_mb: float = 2.0):
+        super().__init__(engine, comm, bucket_mb, overlap, broadcast_init, broadcast_buffers, tail_mb)
         if self.active:
             for b in self.buckets:
                 if b.numel % (4 * self.world):
@@ -480,7 +483,7 @@ DEFAULT_BUCKET_MB = {"gather": 0.0, "allreduce": 0.0, "ddp": 10.0, "zero1": 10.0
 
 
 def make_sync(mode: str, engine, comm: Comm, bucket_mb: Optional[float] = None, overlap: bool = True,
-              broadcast_init: bool = True) -> GradSync:
+              broadcast_init: bool = True, tail_mb: float = 2.0) -> GradSync:
     cls = MODES[mode]
     bmb = DEFAULT_BUCKET_MB[mode] if bucket_mb is None else bucket_mb
-    return cls(engine, comm, bmb, overlap, broadcast_init)
+    return cls(engine, comm, bmb, overlap, broadcast_init, tail_mb=tail_mb)

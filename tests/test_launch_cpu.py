@@ -83,7 +83,8 @@ def test_bench_self_launch_two_ranks_cpu():
     spawn path the driver's 8-GPU run takes; one JSON line with the scaling fields."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", spawn.SPAWNED_ENV)}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
-                        "--batch", "4", "--steps", "2", "--warmup", "1", "--solo-steps", "1"],
+                        "--batch", "4", "--steps", "2", "--warmup", "1", "--solo-steps", "1",
+                        "--comm-tune-steps", "1"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -98,6 +99,21 @@ def test_bench_self_launch_two_ranks_cpu():
     assert rec["config"]["global_batch"] == 8
     assert rec["replicas_identical"] is True and rec["rccl_world"] == 2
     assert rec["scaling_efficiency"] is not None and rec["value"] > 0
+    # the warmup-time gradient-sync plan choice: every candidate timed, one chosen, reported
+    tune = rec["config"]["comm_tune"]
+    assert len(tune["ms_per_step"]) == 5 and all(v > 0 for v in tune["ms_per_step"].values())
+    ch = tune["chosen"]
+    assert rec["config"]["per_bucket_update"] == ch["per_bucket_update"]
+    key = f"b{ch['bucket_mb']}_t{ch['tail_mb']}_{'fused' if ch['per_bucket_update'] else 'after'}"
+    assert tune["ms_per_step"][key] == min(tune["ms_per_step"].values())
+    # the tuning steps leave no trace: the same run without tuning ends with the same parameters
+    r2 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+                         "--batch", "4", "--steps", "2", "--warmup", "1", "--solo-steps", "0", "--diag-steps", "0",
+                         "--comm-tune", "off"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    rec2 = json.loads([l for l in r2.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec2["config"]["comm_tune"] is None
+    assert rec2["param_checksum"] == rec["param_checksum"] and rec2["final_loss"] == rec["final_loss"]
 
 
 def test_native_store_port_via_torchrun_agent_store(tmp_path):
