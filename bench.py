@@ -193,7 +193,11 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
             benchlib.device_barrier(ctx, dev)
             el = ctx.all_max(time.perf_counter() - t0) / n * 1e3
             score[p] = min(score.get(p, el), el)
+    # the first plan is the default: another one must beat it by 1 % (run-to-run noise of a few
+    # steps), so the choice does not flap between equivalent plans
     best = min(plans, key=lambda p: score[p])
+    if score[best] > 0.99 * score[plans[0]]:
+        best = plans[0]
     benchlib.device_barrier(ctx, dev)
     for dst, src in zip((engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt, engine.loss_accum),
                         snap):

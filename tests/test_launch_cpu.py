@@ -105,7 +105,8 @@ def test_bench_self_launch_two_ranks_cpu():
     ch = tune["chosen"]
     assert rec["config"]["per_bucket_update"] == ch["per_bucket_update"]
     key = f"b{ch['bucket_mb']}_t{ch['tail_mb']}_{'fused' if ch['per_bucket_update'] else 'after'}"
-    assert tune["ms_per_step"][key] == min(tune["ms_per_step"].values())
+    best, default = min(tune["ms_per_step"].values()), next(iter(tune["ms_per_step"].values()))
+    assert tune["ms_per_step"][key] == best or (tune["ms_per_step"][key] == default and best > 0.99 * default)
     # the tuning steps leave no trace: the same run without tuning ends with the same parameters
     r2 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
                          "--batch", "4", "--steps", "2", "--warmup", "1", "--solo-steps", "0", "--diag-steps", "0",
