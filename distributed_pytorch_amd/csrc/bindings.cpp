@@ -31,7 +31,8 @@ int dpa_bn_apply(const void* z, float* a, unsigned short* a3, int np, const floa
 int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
-               int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val);
+               int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val,
+               const void* g2);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -589,7 +590,7 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
@@ -626,9 +627,15 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_bwd: gsrc too small");
   TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd: part too small");
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
+  const void* g2p = nullptr;
+  if (g2.has_value() && g2->defined()) {
+    TORCH_CHECK(g2->numel() == g.numel() && g2->scalar_type() == g.scalar_type() && nsplit == 1,
+                "bn_bwd: g2 must match g (type, size) and nsplit must be 1");
+    g2p = act_ptr(*g2, "g2", bf);
+  }
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val),
+                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p),
       "bn_bwd");
 }
 
@@ -851,7 +858,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
-        py::arg("sig_val") = 0);
+        py::arg("sig_val") = 0, py::arg("g2") = py::none());
   m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
         py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("x"), py::arg("wpart"),

@@ -404,7 +404,10 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 
 // Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat.  Rows are OUTPUT rows of
 // the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
-// the summed g is written to gout (consumed by the apply pass).  part layout: [block][3][C]
+// the summed g is written to gout (consumed by the apply pass).  g2 (optional, nsplit == 1): a second
+// contribution to the same gradient, summed on load here and in the apply pass instead of by a
+// separate add pass (ResNet: a block input's two gradient contributions, ops/functional.GradJoin).
+// part layout: [block][3][C]
 template <bool POOL, int ACT, typename TZ, int RTB>
 __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
                                                             int nsplit, const TZ* __restrict__ z,
@@ -414,7 +417,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
                                                             float* __restrict__ part, int N, int H, int W, int C,
-                                                            int rpb, int* sig, int sig_val) {
+                                                            int rpb, int* sig, int sig_val,
+                                                            const TZ* __restrict__ g2) {
   start_signal(sig, sig_val);
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
@@ -441,7 +445,11 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
       if (RTB == RT && !POOL && nsplit == 1) {
         for (; r + gg.RPI < r1; r += 2 * gg.RPI) {
           const long gi0 = (long)r * gg.C4 + c4, gi1 = gi0 + (long)gg.RPI * gg.C4;
-          const float4 g0 = ld4(gsrc, gi0), g1 = ld4(gsrc, gi1);
+          float4 g0 = ld4(gsrc, gi0), g1 = ld4(gsrc, gi1);
+          if (g2) {
+            g0 = f4add(g0, ld4(g2, gi0));
+            g1 = f4add(g1, ld4(g2, gi1));
+          }
           const float4 z0 = ld4(z, gi0), z1 = ld4(z, gi1);
           const float4 r0v = ACT == 2 ? ld4(res, gi0) : make_float4(0.f, 0.f, 0.f, 0.f);
           const float4 r1v = ACT == 2 ? ld4(res, gi1) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -465,6 +473,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
         float4 gv = ld4(gsrc, gi);
         for (int s = 1; s < nsplit; ++s) gv = f4add(gv, ld4(gsrc, s * slab4 + gi));
         if (nsplit > 1) st4(gout, gi, gv);
+        if (g2) gv = f4add(gv, ld4(g2, gi));  // a second gradient contribution (nsplit == 1 only)
         if (!POOL) {
           const float4 zv = ld4(z, gi);
           const float4 rv = ACT == 2 ? ld4(res, gi) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -589,7 +598,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
                                                            const float* __restrict__ coef, float* __restrict__ dz,
                                                            u16* __restrict__ dz3, long ps,
                                                            const TZ* __restrict__ res, TZ* __restrict__ dres,
-                                                           int N, int H, int W, int C) {
+                                                           int N, int H, int W, int C, const TZ* __restrict__ g2) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
@@ -603,7 +612,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
               reinterpret_cast<const float4*>(coef + 2 * C)[c4]};
   };
   auto body = [&](long i, int c4, const Co& q) {
-    const float4 gv = ld4(g, i);
+    float4 gv = ld4(g, i);
+    if (g2) gv = f4add(gv, ld4(g2, i));
     if (!POOL) {
       const float4 zv = ld4(z, i);
       const float4 rv = ACT == 2 ? ld4(res, i) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -723,20 +733,20 @@ int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, co
 template <bool POOL, int NP, typename TZ>
 void bn_bwd_apply_launch(int act, int grid, hipStream_t st, const TZ* g, const TZ* z, const float* scale,
                          const float* shift, const float* coef, float* dz, u16* dz3, long ps, const TZ* res, TZ* dres,
-                         int N, int H, int W, int C) {
+                         int N, int H, int W, int C, const TZ* g2) {
   if constexpr (POOL) {
     bn_bwd_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H,
-                                                                W, C);
+                                                                W, C, g2);
   } else {
     if (act == 0)
       bn_bwd_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C);
+                                                                   H, W, C, g2);
     else if (act == 1)
       bn_bwd_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C);
+                                                                   H, W, C, g2);
     else
       bn_bwd_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C);
+                                                                   H, W, C, g2);
   }
 }
 
@@ -746,7 +756,7 @@ template <typename TZ>
 void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                   const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                   float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
-                  hipStream_t st, int* sig = nullptr, int sig_val = 0) {
+                  hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = bwd_rows_per_block(Mo, C);
@@ -755,10 +765,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
 #define RED(P, A)                                                                                                 \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
-                                                            N, H, W, C, rpb, sig, sig_val);                       \
+                                                            N, H, W, C, rpb, sig, sig_val, g2);                   \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
-                                                              part, N, H, W, C, rpb, sig, sig_val)
+                                                              part, N, H, W, C, rpb, sig, sig_val, g2)
   if (pool) {
     RED(true, 0);
   } else if (act == 0) {
@@ -923,16 +933,17 @@ template <typename TZ>
 int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-                const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val) {
+                const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2) {
   if (nsplit < 1) nsplit = 1;
   bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
-                   C, pool, act, res, st, sig, sig_val);
+                   C, pool, act, res, st, sig, sig_val, g2);
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
   const long ps = (long)N * H * W * C;
   const int grid = grid_ch(total, C / 4);
-#define BAP(P, NPT) bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C)
+#define BAP(P, NPT) \
+  bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C, g2)
   if (pool) {
     if (np == 0) BAP(true, 0);
     else if (np == 1) BAP(true, 1);
@@ -997,20 +1008,22 @@ int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, c
 
 // gsrc: grad of the layer output (pooled shape if pool), or nsplit fp32 slabs of it (then the sum is
 // written to g).  Writes dz [N,H,W,C] (fp32, or bf16 planes dz3) and dgamma/dbeta/dbias; act 2 also
-// the residual gradient dres.  zbf: gsrc/g/z/res/dres are bf16 (nsplit must be 1).
+// the residual gradient dres.  zbf: gsrc/g/z/res/dres are bf16 (nsplit must be 1).  g2 (optional,
+// same type and shape as g, nsplit 1): the gradient is gsrc + g2, summed on load.
 int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-               const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val) {
+               const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && (!res || !dres))) return -2;
   if (zbf && nsplit > 1) return -2;
+  if (g2 && nsplit > 1) return -2;  // a second gradient operand is summed on load of an unsplit g only
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st, sig, sig_val);
+                            (u16*)dres, st, sig, sig_val, (const u16*)g2);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st, sig, sig_val);
+                            (float*)dres, st, sig, sig_val, (const float*)g2);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.

@@ -46,6 +46,12 @@ class Bottleneck(nn.Module):
         j = self._join if (self.training and torch.is_grad_enabled() and x.requires_grad) else None
         if j is not None:
             j.reset()
+            # x made by a BN backward that sums a second gradient operand on load: the join may leave
+            # its stash to it instead of an add pass; the hook adds it if autograd summed x's gradient
+            j.defer = Fn.DEFER_JOIN and bool(getattr(x, "_dpa_sum_on_load", False))
+            j.key = None
+            if j.defer:
+                x.register_hook(j.guard)
         out = self.bn1(self.conv1(x, j))
         out = self.bn2(self.conv2(out))
         if self.downsample is not None:
@@ -91,6 +97,8 @@ class ResNet(nn.Module):
 
     def forward(self, x, target=None):
         """Logits, or with ``target`` the batch-mean cross-entropy through the fused head."""
+        if self.training:
+            Fn.clear_deferred()
         f = self.features(x)
         if target is not None:
             return Fn.head_ce(f, self.fc.weight, self.fc.bias, target)

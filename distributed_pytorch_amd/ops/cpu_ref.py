@@ -133,12 +133,14 @@ def bn_apply(z, a, scale, shift, pool, act=0, res=None):
 
 
 def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool,
-           act=0, res=None, dres=None):
+           act=0, res=None, dres=None, sig=None, sig_val=0, g2=None):
     N, H, W, C = z.shape
     if nsplit > 1:
         g.copy_(gsrc[:nsplit * g.numel()].view(nsplit, -1).sum(0).view(g.shape))
     else:
         g = gsrc
+    if g2 is not None:  # a second contribution to the same gradient (native: summed on load)
+        g = g + g2
     with torch.enable_grad():
         u = (z * scale + shift).detach().requires_grad_(True)  # BN output, pre-activation
         y = _act(u, act, res)

@@ -224,6 +224,19 @@ def conv_config(kind: str, M: int, Ngemm: int, Kred: int, hw_small: bool) -> Tup
     return c
 
 
+# Deferred gradient contributions (GradJoin with ``defer``): data_ptr of a block input's gradient ->
+# (that gradient, the addend).  The gradient's consumer -- the BN backward that produced the block
+# input -- sums the addend on load (bn.hip ``g2``) instead of an elementwise add pass over it.
+_DEFERRED: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+DEFER_JOIN = os.environ.get("DPA_DEFER_JOIN", "1") == "1"  # A/B switch (0: add pass as before)
+DEFER_STATS = {"summed_on_load": 0}  # BN backwards that consumed a deferred contribution (tests)
+
+
+def clear_deferred():
+    """Drop deferred contributions of an abandoned backward (called at every training forward)."""
+    _DEFERRED.clear()
+
+
 class GradJoin:
     """Joins the gradient contributions of several autograd nodes to ONE tensor without an
     elementwise add pass.  In a ResNet bottleneck the block input x feeds conv1 and the residual
@@ -232,12 +245,20 @@ class GradJoin:
     ``contribute``: all but the last stash their gradient and hand autograd None (a zero
     contribution, nothing to add); the last one folds the stash into its own output — inside the
     data-gradient split-K reduction when its conv splits K (``splitk_reduce_add``), else with one
-    in-place add — and returns the sum.  Order-independent; ``reset()`` at every forward."""
+    in-place add — and returns the sum.  Order-independent; ``reset()`` at every forward.
 
-    __slots__ = ("n", "left", "buf")
+    ``defer`` (set per forward when the joined tensor was produced by a BN backward that can take a
+    second gradient operand, ``bn_act_nhwc`` outputs): when the last contributor's data gradient
+    has no split-K reduction to fold the stash into, the stash is not added at all but registered
+    with the returned gradient; the producing BN backward sums it on load.  ``guard`` (a hook on
+    the joined tensor) adds it explicitly if autograd summed the gradient with another one first."""
+
+    __slots__ = ("n", "left", "buf", "defer", "key")
 
     def __init__(self, n: int):
         self.n = n
+        self.defer = False
+        self.key = None
         self.reset()
 
     def reset(self):
@@ -254,6 +275,20 @@ class GradJoin:
         else:
             self.buf = self.buf + g
         self.left -= 1
+
+    def register(self, g: torch.Tensor, addend: torch.Tensor) -> None:
+        """Defer ``addend`` to g's consumer (see class doc)."""
+        self.key = g.data_ptr()
+        _DEFERRED[self.key] = (g, addend)
+
+    def guard(self, grad: torch.Tensor) -> Optional[torch.Tensor]:
+        """Hook on the joined tensor: its total gradient is not the registered one (autograd summed
+        other contributions into a new tensor) -> add the deferred addend here."""
+        key, self.key = self.key, None
+        if key is None or grad.data_ptr() == key:
+            return None
+        ent = _DEFERRED.pop(key, None)
+        return grad if ent is None else grad + ent[1]
 
     def take(self) -> Optional[torch.Tensor]:
         """For the last contributor: the stashed sum (None if nothing was stashed); resets."""
@@ -365,8 +400,14 @@ class Conv2dNHWC(torch.autograd.Function):
 
             cfg = choose_config(ctx.impl, "dgrad", geom, N * H * W, C, R * S * K, H * W <= 16, run_d,
                                 lambda s: 4 * s * N * H * W * C)
-            run_d(cfg[0], Kx.x3_splits(R * S * K, cfg[1]), cfg[2],
-                  addend.to(dx.dtype).contiguous() if addend is not None else None)
+            sk = Kx.x3_splits(R * S * K, cfg[1])
+            if addend is not None:
+                addend = addend.to(dx.dtype).contiguous()
+            # no split-K reduction to fold the stash into: leave it to the producing BN backward
+            defer = addend is not None and sk == 1 and join.defer
+            run_d(cfg[0], sk, cfg[2], None if defer else addend)
+            if defer:
+                join.register(dx, addend)
         if ctx.needs_input_grad[1]:
             dw = grad_slot(ctx.w_param)
             if dw is None:
@@ -427,6 +468,7 @@ class BnActNHWC(torch.autograd.Function):
         z, res, gamma, mean, invstd, scale, shift = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("bn_act_nhwc backward is only defined in training mode")
+        ent = _DEFERRED.pop(da.data_ptr(), None)  # a deferred second contribution to da (GradJoin.register)
         da = da.contiguous()
         N, H, W, C = z.shape
         native = _native(z)
@@ -441,8 +483,15 @@ class BnActNHWC(torch.autograd.Function):
         dres = torch.empty_like(z) if ctx.act == 2 else None
         part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), z.device, zero=True) if native else None
         coef = torch.empty(3 * C, **f32)
+        g2 = None  # ... summed on load by the kernels
+        if ent is not None:
+            if native and ent[1].dtype == da.dtype and ent[1].numel() == da.numel():
+                g2 = ent[1]
+                DEFER_STATS["summed_on_load"] += 1
+            else:
+                da = da + ent[1].view_as(da)
         K.bn_bwd(da, 1, da, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, None, dz, False, ctx.act,
-                 res, dres)
+                 res, dres, g2=g2)
         if ctx.res_join is not None and dres is not None:
             dres = ctx.res_join.contribute(dres)
         return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
@@ -458,8 +507,11 @@ def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, 
     res = residual.to(z.dtype).contiguous() if residual is not None else None
     if res is not residual:
         res_join = None  # a converted copy: its gradient flows back through the conversion, not the join
-    return BnActNHWC.apply(z.contiguous(), gamma, beta, res, running_mean, running_var, num_batches_tracked,
-                           bool(training), float(momentum), float(eps), a, res_join)
+    out = BnActNHWC.apply(z.contiguous(), gamma, beta, res, running_mean, running_var, num_batches_tracked,
+                          bool(training), float(momentum), float(eps), a, res_join)
+    # its backward sums a deferred second gradient contribution on load (GradJoin.defer)
+    out._dpa_sum_on_load = bool(training) and out.requires_grad and _native(out)
+    return out
 
 
 class MaxPoolNHWC(torch.autograd.Function):

@@ -267,3 +267,44 @@ def test_resnet_fused_loss_step_matches_reference():
         errs.append(e)
     errs.sort()
     assert errs[len(errs) // 2] < 5e-3, errs
+
+
+@pytest.mark.parametrize("impl", ["x3", "bf16"])
+def test_resnet_deferred_residual_gradient(monkeypatch, impl):
+    """A block input's second gradient contribution left to the producing BN backward (summed on
+    load, bn.hip g2) instead of an add pass.  x3: gradients bitwise those of the add-pass path (both
+    add in fp32).  bf16: the add pass rounds the sum to bf16 and the deferred path does not, so the
+    two differ by bf16 rounding propagated through the network; both are compared with the x3
+    (fp32-grade) gradients, and the deferred path must be no less accurate."""
+    from distributed_pytorch_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    sd = R.ResNet([1, 3, 1, 1], 10, impl=impl).state_dict()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(8, 64, 64, 3, generator=g).cuda()
+    t = torch.randint(0, 10, (8,), generator=g).cuda()
+
+    def run(impl_, defer):
+        monkeypatch.setattr(R.Fn, "DEFER_JOIN", defer)
+        m = R.ResNet([1, 3, 1, 1], 10, impl=impl_)
+        m.load_state_dict(sd)
+        m = m.cuda()
+        n0 = R.Fn.DEFER_STATS["summed_on_load"]
+        m(x, t).backward()
+        torch.cuda.synchronize()
+        used = R.Fn.DEFER_STATS["summed_on_load"] - n0
+        assert (used > 0) == defer, used
+        assert not R.Fn._DEFERRED
+        return {n: p.grad.detach().float().clone() for n, p in m.named_parameters()}
+
+    add_pass, deferred = run(impl, False), run(impl, True)
+    if impl == "x3":
+        for n in add_pass:
+            assert torch.equal(add_pass[n], deferred[n]), n
+        return
+    ref = run("x3", False)
+    e_add = sorted(rel(add_pass[n], ref[n]) for n in ref)
+    e_def = sorted(rel(deferred[n], ref[n]) for n in ref)
+    med = len(ref) // 2
+    assert e_def[med] <= 1.25 * e_add[med] + 1e-3, (e_def[med], e_add[med])
+    assert e_def[-1] <= 1.5 * e_add[-1] + 1e-2, (e_def[-1], e_add[-1])
