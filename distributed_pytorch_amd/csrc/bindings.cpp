@@ -27,12 +27,13 @@ int dpa_bn_fwd_stats(const void* src, int nsplit, void* z, float* part, int M, i
 int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias, const float* rmean,
                        const float* rvar, float* scale, float* shift, int C, float eps, hipStream_t st);
 int dpa_bn_apply(const void* z, float* a, unsigned short* a3, int np, const float* scale, const float* shift, int N,
-                 int H, int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st);
+                 int H, int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st,
+                 unsigned char* mask);
 int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val,
-               const void* g2);
+               const void* g2, const unsigned char* mask);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -450,9 +451,19 @@ void bn_eval_params(Tensor gamma, Tensor beta, OptT bias, Tensor rmean, Tensor r
 // a: fp32 [N,Ho,Wo,C] or bf16 planes [NP,N,Ho,Wo,C].  act: 0 relu, 1 none, 2 relu(. + res)
 // z (and res): fp32 or bf16 [N,H,W,C]; a: fp32 [N,Ho,Wo,C], bf16 [N,Ho,Wo,C] (one plane) or bf16
 // planes [NP,N,Ho,Wo,C]
-void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t act, OptT res) {
+// mask (optional, act 2): uint8 [z.numel() / 4] written with the ReLU mask the backward reads
+unsigned char* mask_ptr(const OptT& mask, const Tensor& z, const char* what) {
+  if (!mask.has_value() || !mask->defined()) return nullptr;
+  TORCH_CHECK(mask->is_cuda() && mask->is_contiguous() && mask->scalar_type() == at::kByte &&
+                  mask->numel() == z.numel() / 4,
+              what, ": mask must be a contiguous uint8 CUDA tensor of z.numel() / 4 bytes");
+  return mask->data_ptr<unsigned char>();
+}
+
+void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t act, OptT res, OptT mask) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
+  unsigned char* mp = mask_ptr(mask, z, "bn_apply");
   const void* rp = nullptr;
   if (act == 2) {
     TORCH_CHECK(res.has_value() && res->defined(), "bn_apply: act=2 needs the residual");
@@ -471,13 +482,13 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t
       TORCH_CHECK(a.is_cuda() && a.is_contiguous(), "bn_apply: a must be contiguous");
     }
     chk(dpa_bn_apply(zp, nullptr, up(a), np, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp,
-                     bf ? 1 : 0, cur_stream()),
+                     bf ? 1 : 0, cur_stream(), mp),
         "bn_apply");
   } else {
     need(a, "a");
     TORCH_CHECK(a.numel() == outn, "bn_apply: a shape");
     chk(dpa_bn_apply(zp, fp(a), nullptr, 0, fp(scale), fp(shift), N, H, W, C, pool ? 1 : 0, (int)act, rp, bf ? 1 : 0,
-                     cur_stream()),
+                     cur_stream(), mp),
         "bn_apply");
   }
 }
@@ -590,18 +601,23 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
   void* gp = act_ptr(g, "g", bf);
   const void* rp = nullptr;
   void* drp = nullptr;
+  const unsigned char* mp = mask_ptr(mask, z, "bn_bwd");
   if (act == 2) {
-    TORCH_CHECK(res.has_value() && res->defined() && dres.has_value() && dres->defined(),
-                "bn_bwd: act=2 needs res and dres");
-    TORCH_CHECK(res->numel() == z.numel() && dres->numel() == z.numel(), "bn_bwd: residual shape");
-    rp = act_ptr(*res, "res", bf);
+    // the ReLU mask of the forward (bn_apply mask=...) replaces the residual
+    TORCH_CHECK((mp || (res.has_value() && res->defined())) && dres.has_value() && dres->defined(),
+                "bn_bwd: act=2 needs (res or mask) and dres");
+    TORCH_CHECK(dres->numel() == z.numel(), "bn_bwd: residual shape");
+    if (!mp) {
+      TORCH_CHECK(res->numel() == z.numel(), "bn_bwd: residual shape");
+      rp = act_ptr(*res, "res", bf);
+    }
     drp = act_ptr(*dres, "dres", bf);
   }
   float* dzf = nullptr;
@@ -635,7 +651,7 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   }
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p),
+                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp),
       "bn_bwd");
 }
 
@@ -853,12 +869,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);
   m.def("bn_apply", &bn_apply, py::arg("z"), py::arg("a"), py::arg("scale"), py::arg("shift"), py::arg("pool"),
-        py::arg("act") = 0, py::arg("res") = py::none());
+        py::arg("act") = 0, py::arg("res") = py::none(), py::arg("mask") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"), py::arg("scale"),
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
-        py::arg("sig_val") = 0, py::arg("g2") = py::none());
+        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none());
   m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
         py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("x"), py::arg("wpart"),

@@ -324,12 +324,15 @@ __device__ __forceinline__ float4 affine_relu(float4 v, float4 sc, float4 sh) {
 
 // a = act(z*scale + shift [+ res]), optionally 2x2/s2 max-pooled (ACT 0 only).
 // z: [N,H,W,C]  a: [N,H/2,W/2,C] or [N,H,W,C]
+// mask (ACT 2, optional): one byte per 4 channels, bit k = (BN(z) + res > 0) of channel 4*c4 + k --
+// the backward reads it instead of re-reading the residual (0.25 instead of 2-4 bytes per element)
 template <bool POOL, int NP, int ACT, typename TZ>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z, float* __restrict__ a,
                                                        u16* __restrict__ a3, long ps,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const TZ* __restrict__ res,
-                                                       int N, int H, int W, int C) {
+                                                       int N, int H, int W, int C,
+                                                       unsigned char* __restrict__ mask) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
@@ -344,7 +347,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
                                fmaf(v.w, sc.w, sh.w));
         if constexpr (ACT == 2) {
           const float4 r = ld4(res, i);
-          u = make_float4(fmaxf(u.x + r.x, 0.f), fmaxf(u.y + r.y, 0.f), fmaxf(u.z + r.z, 0.f), fmaxf(u.w + r.w, 0.f));
+          const float4 t = make_float4(u.x + r.x, u.y + r.y, u.z + r.z, u.w + r.w);
+          if (mask)
+            mask[i] = (unsigned char)((t.x > 0.f) | ((t.y > 0.f) << 1) | ((t.z > 0.f) << 2) | ((t.w > 0.f) << 3));
+          u = make_float4(fmaxf(t.x, 0.f), fmaxf(t.y, 0.f), fmaxf(t.z, 0.f), fmaxf(t.w, 0.f));
         }
         store4<NP>(a, a3, ps, i, u);
       }
@@ -418,7 +424,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             const float* __restrict__ invstd,
                                                             float* __restrict__ part, int N, int H, int W, int C,
                                                             int rpb, int* sig, int sig_val,
-                                                            const TZ* __restrict__ g2) {
+                                                            const TZ* __restrict__ g2,
+                                                            const unsigned char* __restrict__ mask) {
   start_signal(sig, sig_val);
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
@@ -451,13 +458,17 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             g1 = f4add(g1, ld4(g2, gi1));
           }
           const float4 z0 = ld4(z, gi0), z1 = ld4(z, gi1);
-          const float4 r0v = ACT == 2 ? ld4(res, gi0) : make_float4(0.f, 0.f, 0.f, 0.f);
-          const float4 r1v = ACT == 2 ? ld4(res, gi1) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const bool mk = ACT == 2 && mask;
+          const float4 r0v = ACT == 2 && !mk ? ld4(res, gi0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 r1v = ACT == 2 && !mk ? ld4(res, gi1) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const unsigned m0 = mk ? mask[gi0] : 0u, m1 = mk ? mask[gi1] : 0u;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float za = F4GET(z0, k), zb = F4GET(z1, k);
-            const float dya = act_grad<ACT>(fmaf(za, F4GET(sc, k), F4GET(sh, k)), F4GET(r0v, k), F4GET(g0, k));
-            const float dyb = act_grad<ACT>(fmaf(zb, F4GET(sc, k), F4GET(sh, k)), F4GET(r1v, k), F4GET(g1, k));
+            const float dya = mk ? (((m0 >> k) & 1u) ? F4GET(g0, k) : 0.f)
+                                 : act_grad<ACT>(fmaf(za, F4GET(sc, k), F4GET(sh, k)), F4GET(r0v, k), F4GET(g0, k));
+            const float dyb = mk ? (((m1 >> k) & 1u) ? F4GET(g1, k) : 0.f)
+                                 : act_grad<ACT>(fmaf(zb, F4GET(sc, k), F4GET(sh, k)), F4GET(r1v, k), F4GET(g1, k));
             const float xa = (za - F4GET(mu, k)) * F4GET(is, k), xb = (zb - F4GET(mu, k)) * F4GET(is, k);
             sdy[k] += dya;
             sdx[k] = fmaf(dya, xa, sdx[k]);
@@ -476,11 +487,14 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
         if (g2) gv = f4add(gv, ld4(g2, gi));  // a second gradient contribution (nsplit == 1 only)
         if (!POOL) {
           const float4 zv = ld4(z, gi);
-          const float4 rv = ACT == 2 ? ld4(res, gi) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const bool mk = ACT == 2 && mask;
+          const float4 rv = ACT == 2 && !mk ? ld4(res, gi) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const unsigned m = mk ? mask[gi] : 0u;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float zz = F4GET(zv, k);
-            const float dy = act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv, k), F4GET(gv, k));
+            const float dy = mk ? (((m >> k) & 1u) ? F4GET(gv, k) : 0.f)
+                                : act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv, k), F4GET(gv, k));
             const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
             sdy[k] += dy;
             sdx[k] = fmaf(dy, xh, sdx[k]);
@@ -598,7 +612,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
                                                            const float* __restrict__ coef, float* __restrict__ dz,
                                                            u16* __restrict__ dz3, long ps,
                                                            const TZ* __restrict__ res, TZ* __restrict__ dres,
-                                                           int N, int H, int W, int C, const TZ* __restrict__ g2) {
+                                                           int N, int H, int W, int C, const TZ* __restrict__ g2,
+                                                           const unsigned char* __restrict__ mask) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
@@ -616,12 +631,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
     if (g2) gv = f4add(gv, ld4(g2, i));
     if (!POOL) {
       const float4 zv = ld4(z, i);
-      const float4 rv = ACT == 2 ? ld4(res, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool mk = ACT == 2 && mask;
+      const float4 rv = ACT == 2 && !mk ? ld4(res, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const unsigned m = mk ? mask[i] : 0u;
       float r[4], dyv[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float zz = F4GET(zv, k);
-        const float dy = act_grad<ACT>(fmaf(zz, F4GET(q.sc, k), F4GET(q.sh, k)), F4GET(rv, k), F4GET(gv, k));
+        const float dy = mk ? (((m >> k) & 1u) ? F4GET(gv, k) : 0.f)
+                            : act_grad<ACT>(fmaf(zz, F4GET(q.sc, k), F4GET(q.sh, k)), F4GET(rv, k), F4GET(gv, k));
         dyv[k] = dy;
         r[k] = F4GET(q.k1, k) * dy + F4GET(q.k2, k) * zz + F4GET(q.k3, k);
       }
@@ -699,33 +717,33 @@ int bn_fwd_stats_host(const TZ* src, int nsplit, TZ* z, float* part, int M, int 
 
 template <bool POOL, int NP, typename TZ>
 void bn_apply_launch(int act, int grid, hipStream_t st, const TZ* z, float* a, u16* a3, long ps, const float* scale,
-                     const float* shift, const TZ* res, int N, int H, int W, int C) {
+                     const float* shift, const TZ* res, int N, int H, int W, int C, unsigned char* mask) {
   if constexpr (POOL) {
-    bn_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+    bn_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
   } else {
     if (act == 0)
-      bn_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+      bn_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
     else if (act == 1)
-      bn_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+      bn_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
     else
-      bn_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C);
+      bn_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
   }
 }
 
 template <typename TZ>
 int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H, int W,
-                  int C, int pool, int act, const TZ* res, hipStream_t st) {
+                  int C, int pool, int act, const TZ* res, hipStream_t st, unsigned char* mask = nullptr) {
   const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   const long ps = total * 4;
   const int grid = grid_ch(total, C / 4);
   if (pool) {
-    if (np == 0) bn_apply_launch<true, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
-    else if (np == 1) bn_apply_launch<true, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
-    else bn_apply_launch<true, 3, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+    if (np == 0) bn_apply_launch<true, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
+    else if (np == 1) bn_apply_launch<true, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
+    else bn_apply_launch<true, 3, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
   } else {
-    if (np == 0) bn_apply_launch<false, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
-    else if (np == 1) bn_apply_launch<false, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
-    else bn_apply_launch<false, 3, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C);
+    if (np == 0) bn_apply_launch<false, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
+    else if (np == 1) bn_apply_launch<false, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
+    else bn_apply_launch<false, 3, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
   }
   return (int)hipGetLastError();
 }
@@ -733,20 +751,20 @@ int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, co
 template <bool POOL, int NP, typename TZ>
 void bn_bwd_apply_launch(int act, int grid, hipStream_t st, const TZ* g, const TZ* z, const float* scale,
                          const float* shift, const float* coef, float* dz, u16* dz3, long ps, const TZ* res, TZ* dres,
-                         int N, int H, int W, int C, const TZ* g2) {
+                         int N, int H, int W, int C, const TZ* g2, const unsigned char* mask) {
   if constexpr (POOL) {
     bn_bwd_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H,
-                                                                W, C, g2);
+                                                                W, C, g2, mask);
   } else {
     if (act == 0)
       bn_bwd_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C, g2);
+                                                                   H, W, C, g2, mask);
     else if (act == 1)
       bn_bwd_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C, g2);
+                                                                   H, W, C, g2, mask);
     else
       bn_bwd_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C, g2);
+                                                                   H, W, C, g2, mask);
   }
 }
 
@@ -756,7 +774,8 @@ template <typename TZ>
 void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                   const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                   float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
-                  hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr) {
+                  hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
+                  const unsigned char* mask = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = bwd_rows_per_block(Mo, C);
@@ -765,10 +784,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
 #define RED(P, A)                                                                                                 \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
-                                                            N, H, W, C, rpb, sig, sig_val, g2);                   \
+                                                            N, H, W, C, rpb, sig, sig_val, g2, mask);                   \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
-                                                              part, N, H, W, C, rpb, sig, sig_val, g2)
+                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask)
   if (pool) {
     RED(true, 0);
   } else if (act == 0) {
@@ -933,17 +952,18 @@ template <typename TZ>
 int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-                const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2) {
+                const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2,
+                const unsigned char* mask) {
   if (nsplit < 1) nsplit = 1;
   bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
-                   C, pool, act, res, st, sig, sig_val, g2);
+                   C, pool, act, res, st, sig, sig_val, g2, mask);
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);
   const long ps = (long)N * H * W * C;
   const int grid = grid_ch(total, C / 4);
 #define BAP(P, NPT) \
-  bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C, g2)
+  bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C, g2, mask)
   if (pool) {
     if (np == 0) BAP(true, 0);
     else if (np == 1) BAP(true, 1);
@@ -999,11 +1019,14 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
 // out: fp32 a (np == 0) or bf16 planes a3 [np][...] (np in {1, 3}).  act: 0 relu (pool allowed),
 // 1 none, 2 relu(. + res).  zbf: z and res are bf16.
 int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
-                 int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st) {
+                 int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st, unsigned char* mask) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && !res)) return -2;
+  if (mask && act != 2) return -2;
   if (zbf)
-    return bn_apply_host<u16>((const u16*)z, a, a3, np, scale, shift, N, H, W, C, pool, act, (const u16*)res, st);
-  return bn_apply_host<float>((const float*)z, a, a3, np, scale, shift, N, H, W, C, pool, act, (const float*)res, st);
+    return bn_apply_host<u16>((const u16*)z, a, a3, np, scale, shift, N, H, W, C, pool, act, (const u16*)res, st,
+                              mask);
+  return bn_apply_host<float>((const float*)z, a, a3, np, scale, shift, N, H, W, C, pool, act, (const float*)res, st,
+                              mask);
 }
 
 // gsrc: grad of the layer output (pooled shape if pool), or nsplit fp32 slabs of it (then the sum is
@@ -1013,17 +1036,19 @@ int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, c
 int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float* scale, const float* shift,
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
-               const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2) {
-  if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && (!res || !dres))) return -2;
+               const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2,
+               const unsigned char* mask) {
+  if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && ((!res && !mask) || !dres))) return -2;
+  if (mask && act != 2) return -2;
   if (zbf && nsplit > 1) return -2;
   if (g2 && nsplit > 1) return -2;  // a second gradient operand is summed on load of an unsplit g only
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st, sig, sig_val, (const u16*)g2);
+                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st, sig, sig_val, (const float*)g2);
+                            (float*)dres, st, sig, sig_val, (const float*)g2, mask);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.

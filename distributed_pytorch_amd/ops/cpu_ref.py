@@ -125,7 +125,7 @@ def _act(u, act, res):
     return torch.relu(u)
 
 
-def bn_apply(z, a, scale, shift, pool, act=0, res=None):
+def bn_apply(z, a, scale, shift, pool, act=0, res=None, mask=None):  # mask: native only (CPU keeps res)
     y = _act(z * scale + shift, act, res)
     if pool:
         y = _nhwc(F.max_pool2d(_nchw(y), 2, 2))
@@ -133,7 +133,7 @@ def bn_apply(z, a, scale, shift, pool, act=0, res=None):
 
 
 def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool,
-           act=0, res=None, dres=None, sig=None, sig_val=0, g2=None):
+           act=0, res=None, dres=None, sig=None, sig_val=0, g2=None, mask=None):
     N, H, W, C = z.shape
     if nsplit > 1:
         g.copy_(gsrc[:nsplit * g.numel()].view(nsplit, -1).sum(0).view(g.shape))

@@ -230,6 +230,7 @@ def conv_config(kind: str, M: int, Ngemm: int, Kred: int, hw_small: bool) -> Tup
 _DEFERRED: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
 DEFER_JOIN = os.environ.get("DPA_DEFER_JOIN", "1") == "1"  # A/B switch (0: add pass as before)
 DEFER_STATS = {"summed_on_load": 0}  # BN backwards that consumed a deferred contribution (tests)
+BN_RELU_MASK = os.environ.get("DPA_BN_RELU_MASK", "1") == "1"  # A/B switch (0: backward re-reads the residual)
 
 
 def clear_deferred():
@@ -453,19 +454,23 @@ class BnActNHWC(torch.autograd.Function):
         else:
             K.bn_eval_params(gamma, beta, None, rmean, rvar, scale, shift, eps)
         a = torch.empty_like(z)
-        K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None)
+        # add+ReLU in training on GPU: the kernel also writes the ReLU mask (1 byte per 4 channels),
+        # which the backward reads instead of the residual
+        mask = (torch.empty(z.numel() // 4, dtype=torch.uint8, device=dev)
+                if act == 2 and training and _native(z) and BN_RELU_MASK else None)
+        K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None, mask=mask)
         ctx.act, ctx.training = act, training
         ctx.res_join = res_join
         ctx.params = (gamma, beta)
         if training:
             note_use(gamma)
             note_use(beta)
-        ctx.save_for_backward(z, res if act == 2 else None, gamma, mean, invstd, scale, shift)
+        ctx.save_for_backward(z, res if act == 2 and mask is None else None, mask, gamma, mean, invstd, scale, shift)
         return a
 
     @staticmethod
     def backward(ctx, da):
-        z, res, gamma, mean, invstd, scale, shift = ctx.saved_tensors
+        z, res, mask, gamma, mean, invstd, scale, shift = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("bn_act_nhwc backward is only defined in training mode")
         ent = _DEFERRED.pop(da.data_ptr(), None)  # a deferred second contribution to da (GradJoin.register)
@@ -491,7 +496,7 @@ class BnActNHWC(torch.autograd.Function):
             else:
                 da = da + ent[1].view_as(da)
         K.bn_bwd(da, 1, da, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, None, dz, False, ctx.act,
-                 res, dres, g2=g2)
+                 res, dres, g2=g2, mask=mask)
         if ctx.res_join is not None and dres is not None:
             dres = ctx.res_join.contribute(dres)
         return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None

@@ -308,3 +308,28 @@ def test_resnet_deferred_residual_gradient(monkeypatch, impl):
     med = len(ref) // 2
     assert e_def[med] <= 1.25 * e_add[med] + 1e-3, (e_def[med], e_add[med])
     assert e_def[-1] <= 1.5 * e_add[-1] + 1e-2, (e_def[-1], e_add[-1])
+
+
+@pytest.mark.parametrize("impl", ["x3", "bf16"])
+def test_resnet_relu_mask_matches_residual_recompute(monkeypatch, impl):
+    """The add+ReLU BN backward reading the forward's ReLU mask (1 byte per 4 channels) instead of
+    re-reading the residual: the mask is the comparison the backward would recompute, so the
+    gradients are bitwise identical."""
+    from distributed_pytorch_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    sd = R.ResNet([1, 2, 1, 1], 10, impl=impl).state_dict()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 64, 64, 3, generator=g).cuda()
+    t = torch.randint(0, 10, (8,), generator=g).cuda()
+    grads = []
+    for use_mask in (False, True):
+        monkeypatch.setattr(R.Fn, "BN_RELU_MASK", use_mask)
+        m = R.ResNet([1, 2, 1, 1], 10, impl=impl)
+        m.load_state_dict(sd)
+        m = m.cuda()
+        m(x, t).backward()
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    for n in grads[0]:
+        assert torch.equal(grads[0][n], grads[1][n]), n
