@@ -186,3 +186,20 @@ def test_native_store_under_real_torchrun(tmp_path):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert [(out / f"{q}.txt").read_text() for q in range(3)] == ["6", "6", "6"]
+
+
+def test_comm_plans_per_mode():
+    """The warmup tuner's candidate gradient-sync plans: DDP tries bucket sizes, the tail bucket and
+    the update placement (default plan first); per-tensor all-reduce keeps its granularity and only
+    tries the update placement; gather / zero1 are not tuned; --bucket-mb pins the bucket size."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    p = bench.comm_plans(bench.parse(["--mode", "ddp"]))
+    assert p[0] == (10.0, 2.0, False) and len(p) == 5 and len(set(p)) == 5
+    assert {b for b, _, _ in p} == {10.0, 25.0, 5.0} and any(f for _, _, f in p) and any(t < 2 for _, t, _ in p)
+    p = bench.comm_plans(bench.parse(["--mode", "ddp", "--bucket-mb", "8"]))
+    assert {b for b, _, _ in p} == {8.0} and p[0] == (8.0, 2.0, False)
+    assert bench.comm_plans(bench.parse(["--mode", "allreduce"])) == [(None, 2.0, False), (None, 2.0, True)]
+    assert bench.comm_plans(bench.parse(["--mode", "gather"])) == []
+    assert bench.comm_plans(bench.parse(["--mode", "zero1"])) == []
