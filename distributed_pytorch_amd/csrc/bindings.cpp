@@ -50,7 +50,8 @@ int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, c
                       float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
-                    int Cin, int J, hipStream_t st);
+                    int Cin, int J, hipStream_t st, const float* bn_z, const float* bn_scale,
+                    const float* bn_shift);
 int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                    int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st);
 int dpa_x3_splits(int Kred, int splits);
@@ -656,14 +657,28 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
 }
 
 // ---------------- classifier head ----------------
+// bn_z [B,2,2,Cin] fp32 + bn_scale/bn_shift [Cin] (optional): the features x [B,Cin] are computed
+// from the last conv's output (BN + ReLU + 2x2 max-pool) inside the head kernel and written to x
 void fc_ce_train(Tensor x, Tensor w, Tensor b, Tensor target, Tensor loss_row, Tensor dlogits, Tensor dx, Tensor dw,
-                 Tensor db, Tensor loss_out, OptT loss_accum) {
+                 Tensor db, Tensor loss_out, OptT loss_accum, OptT bn_z, OptT bn_scale, OptT bn_shift) {
   need(x, "x");
   need(target, "target", at::kLong);
   const int B = x.size(0), Cin = x.size(1), J = w.size(0);
+  const float* zp = nullptr;
+  if (bn_z.has_value() && bn_z->defined()) {
+    need(*bn_z, "bn_z");
+    TORCH_CHECK(bn_z->dim() == 4 && bn_z->size(0) == B && bn_z->size(1) == 2 && bn_z->size(2) == 2 &&
+                    bn_z->size(3) == Cin,
+                "fc_ce_train: bn_z must be [B,2,2,Cin]");
+    TORCH_CHECK(bn_scale.has_value() && bn_shift.has_value() && bn_scale->numel() == Cin && bn_shift->numel() == Cin,
+                "fc_ce_train: bn_scale / bn_shift [Cin] needed with bn_z");
+    need(*bn_scale, "bn_scale");
+    need(*bn_shift, "bn_shift");
+    zp = fp(*bn_z);
+  }
   chk(dpa_fc_ce_train(fp(x), fp(w), fp(b), reinterpret_cast<const long long*>(target.data_ptr<int64_t>()),
                       fp(loss_row), fp(dlogits), fp(dx), fp(dw), fp(db), fp(loss_out), ofp(loss_accum), B, Cin, J,
-                      cur_stream()),
+                      cur_stream(), zp, zp ? fp(*bn_scale) : nullptr, zp ? fp(*bn_shift) : nullptr),
       "fc_ce_train");
 }
 
@@ -892,7 +907,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5);
   m.def("conv0_part_floats", [](int64_t N) { return dpa_conv0_part_floats((int)N); });
   m.def("wgrad0_part_floats", [](int64_t N) { return dpa_wgrad0_part_floats((int)N); });
-  m.def("fc_ce_train", &fc_ce_train);
+  m.def("fc_ce_train", &fc_ce_train, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("loss_row"),
+        py::arg("dlogits"), py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("loss_out"), py::arg("loss_accum"),
+        py::arg("bn_z") = py::none(), py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none());
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);
   m.def("maxpool_fwd", &maxpool_fwd);

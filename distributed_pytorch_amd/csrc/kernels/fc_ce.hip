@@ -17,13 +17,25 @@ constexpr int GEN_J = 16, GEN_CL = 16;
 // W [J][Cin] is staged once per block into LDS (one round of independent 16-B loads), the row
 // (Cin/64 values per lane) is held in registers, and the J wave reductions are interleaved: the
 // kernel pays ~two global-memory latencies instead of a chain of dependent L2 round trips.
-template <bool TRAIN, int MAXJ, int MAXCL>
+//
+// Bn: the last conv layer's BatchNorm + ReLU + 2x2 max-pool folded into the row load (VGG on 32x32:
+// the pool leaves one pixel, so a feature row is the max over the 4 pixels of z [B][4][Cin] of
+// relu(z*scale + shift), the same operations in the same order as bn_apply).  The features are
+// also stored to x (the weight-gradient kernel reads them), and the separate bn_apply launch goes.
+struct BnIn {
+  const float* z;
+  const float* scale;
+  const float* shift;
+};
+
+template <bool TRAIN, int MAXJ, int MAXCL, bool BNIN = false>
 __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias,
                                                          const long long* __restrict__ target,
                                                          float* __restrict__ loss_row, float* __restrict__ dlogits,
                                                          float* __restrict__ dx, int* __restrict__ correct_row,
-                                                         float* __restrict__ logits_out, int B, int Cin, int J) {
+                                                         float* __restrict__ logits_out, int B, int Cin, int J,
+                                                         BnIn bn = BnIn{nullptr, nullptr, nullptr}) {
   extern __shared__ float w_s[];  // [J][Cin]
   for (int i = threadIdx.x * 4; i < J * Cin; i += blockDim.x * 4)
     *reinterpret_cast<float4*>(w_s + i) = *reinterpret_cast<const float4*>(w + i);
@@ -33,10 +45,28 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
   if (row >= B) return;
   const float* xr = x + (long)row * Cin;
   float xv[MAXCL];
+  if constexpr (BNIN) {
+    const float* zr = bn.z + (long)row * 4 * Cin;
+    float* xo = const_cast<float*>(xr);
 #pragma unroll
-  for (int k = 0; k < MAXCL; ++k) {
-    const int c = lane + 64 * k;
-    xv[k] = c < Cin ? xr[c] : 0.f;
+    for (int k = 0; k < MAXCL; ++k) {
+      const int c = lane + 64 * k;
+      float v = 0.f;
+      if (c < Cin) {
+        const float sc = bn.scale[c], sh = bn.shift[c];
+        const float v00 = fmaxf(fmaf(zr[c], sc, sh), 0.f), v01 = fmaxf(fmaf(zr[Cin + c], sc, sh), 0.f);
+        const float v10 = fmaxf(fmaf(zr[2 * Cin + c], sc, sh), 0.f), v11 = fmaxf(fmaf(zr[3 * Cin + c], sc, sh), 0.f);
+        v = fmaxf(fmaxf(v00, v01), fmaxf(v10, v11));
+        xo[c] = v;
+      }
+      xv[k] = v;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < MAXCL; ++k) {
+      const int c = lane + 64 * k;
+      xv[k] = c < Cin ? xr[c] : 0.f;
+    }
   }
   float logit[MAXJ];
 #pragma unroll
@@ -220,10 +250,20 @@ __global__ __launch_bounds__(256) void eval_accum_kernel(const float* __restrict
 
 extern "C" {
 
+// bn_z / bn_scale / bn_shift (optional, VGG head): x is then OUTPUT -- the features are computed from
+// the last conv layer's z [B][2][2][Cin] (BN + ReLU + 2x2 max-pool, see BnIn) and stored there.
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
-                    int Cin, int J, hipStream_t st) {
+                    int Cin, int J, hipStream_t st, const float* bn_z, const float* bn_scale, const float* bn_shift) {
   if (J > GEN_J || Cin > 64 * GEN_CL || Cin % 4 || (long)B * J * 4 > 48 * 1024) return -2;
+  if (bn_z) {
+    if (!bn_scale || !bn_shift || J > 10 || Cin > 512) return -2;
+    fc_ce_rows_kernel<true, 10, 8, true><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(
+        x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin, J, BnIn{bn_z, bn_scale, bn_shift});
+    fc_ce_wgrad_kernel<10><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
+                                                                     loss_accum, B, Cin, J);
+    return (int)hipGetLastError();
+  }
   if (J <= 10 && Cin <= 512) {
     fc_ce_rows_kernel<true, 10, 8><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits, dx,
                                                                           nullptr, nullptr, B, Cin, J);

@@ -241,6 +241,11 @@ class VGGEngine:
                             and os.environ.get("DPA_FUSED_CONV0", "1") == "1"
                             and l0.hw == 32 and l0.cout == 64 and l0.cin <= 3)
         self.part0 = torch.empty(self.K.conv0_part_floats(N), **f32) if self.fused_conv0 else None
+        # Head: the last layer's BN + ReLU + 2x2 max-pool folded into the classifier kernel's row load
+        # (fc_ce.hip BnIn: one launch less on the critical path); DPA_FUSED_HEAD=0 runs bn_apply
+        lL = L[-1]
+        self.fused_head = (dev.type == "cuda" and os.environ.get("DPA_FUSED_HEAD", "1") == "1" and lL.pool
+                           and lL.hw == 2 and self.spec.fc_in == lL.cout and self.a[-1] is not None)
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -602,10 +607,14 @@ class VGGEngine:
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                            self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"], self.bn_momentum,
                            self.bn_eps)
+            if i == len(L) - 1 and self.fused_head:
+                continue  # applied inside the head kernel below
             K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
         feat = self.a[-1][:n].view(n, -1)
+        bn_in = (dict(bn_z=self.z[-1][:n], bn_scale=self.stats[-1]["scale"], bn_shift=self.stats[-1]["shift"])
+                 if self.fused_head else {})
         K.fc_ce_train(feat, P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n], self.dlogits[:n],
-                      self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
+                      self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum, **bn_in)
         if grad_ready is not None:
             grad_ready(["fc1.weight", "fc1.bias"])
         # Kernel-start signals (epoch > 0, signal.hip): each BN backward raises bsig[i] when it starts,

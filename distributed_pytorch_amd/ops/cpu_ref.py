@@ -180,8 +180,11 @@ def bn_bwd_wgrad0(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, c
 
 
 # ---------------------------------------------------------------- classifier head
-def fc_ce_train(x, w, b, target, loss_row, dlogits, dx, dw, db, loss_out, loss_accum):
+def fc_ce_train(x, w, b, target, loss_row, dlogits, dx, dw, db, loss_out, loss_accum, bn_z=None, bn_scale=None,
+                bn_shift=None):
     B = x.shape[0]
+    if bn_z is not None:  # features from the last conv's z: BN + ReLU + 2x2 max-pool, written to x
+        x.copy_(torch.relu(bn_z * bn_scale + bn_shift).reshape(B, 4, -1).amax(1))
     logits = x @ w.t() + b
     lse = torch.logsumexp(logits, 1)
     lr = lse - logits.gather(1, target.view(-1, 1)).squeeze(1)

@@ -613,3 +613,31 @@ def test_graphed_step_matches_eager(impl):
         outs.append((e.params.flat.clone(), e.mom.flat.clone(), torch.stack(losses)))
     for a_, b_ in zip(outs[0], outs[1]):
         assert torch.equal(a_, b_)
+
+
+def test_fused_head_matches_separate_bn_apply(monkeypatch):
+    """The last layer's BN + ReLU + 2x2 max-pool computed inside the classifier kernel (fc_ce.hip
+    BnIn) instead of by bn_apply: same operations in the same order, so training is bit-identical."""
+    from distributed_pytorch_amd.engine import VGGEngine
+
+    g = torch.Generator().manual_seed(13)
+    xs = [torch.randn(64, 32, 32, 4, generator=g) for _ in range(2)]
+    ts = [torch.randint(0, 10, (64,), generator=g) for _ in range(2)]
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DPA_FUSED_HEAD", fused)
+        e = VGGEngine("VGG11", "cuda", max_batch=64, impl="x3", lr=0.05)
+        assert e.fused_head == (fused == "1")
+        e.init_parameters(seed=6)
+        losses = []
+        for x, t in zip(xs, ts):
+            x = x.cuda()
+            x[..., 3] = 0
+            e.forward_backward(x, t.cuda())
+            e.sgd_step()
+            e.finish_step()
+            losses.append(e.loss.clone())
+        torch.cuda.synchronize()
+        outs.append((e.params.flat.clone(), e.a[-1].clone(), torch.cat(losses)))
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
