@@ -43,8 +43,6 @@ from distributed_pytorch_amd.utils.profiling import EventProbe, step_comm_report
 BASELINE_METRIC = "images/sec whole-node VGG-11 CIFAR-10 at 1/2/4/8 MI355X; scaling efficiency"  # BASELINE.json
 # BASELINE.md (reference harness measured on CPU — the only numbers the reference has)
 BASELINE_IMG_S = {1: 397.8, 2: 601.8}
-# stock PyTorch-ROCm eager fp32 on one MI355X (tools/torch_baseline.py, profiles/)
-TORCH_EAGER_IMG_S_PER_GPU = 68699.5
 
 
 def parse(argv=None):
@@ -81,6 +79,10 @@ def parse(argv=None):
                     help="re-run this command under rocprofv3 --kernel-trace --stats (prints the command)")
     ap.add_argument("--profile-dir", default="gpurun_out/prof")
     ap.add_argument("--launch-timeout", type=float, default=1800.0, help="wall-clock limit of a self-launched job")
+    ap.add_argument("--torch-baseline", type=int, default=0, metavar="STEPS",
+                    help="1 GPU: first time STEPS steps of stock PyTorch-ROCm eager fp32 training of the same model "
+                         "and batch (tools/torch_baseline.py, in a child process on this GPU) and report "
+                         "vs_torch_eager_fp32 from this same run (0 = off)")
     return ap.parse_args(argv)
 
 
@@ -247,6 +249,9 @@ def main(argv=None):
         raise SystemExit(f"--gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
     launcher = "spawn" if is_spawned_child() else ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or
                                                    "WORLD_SIZE" in os.environ else "single")
+    torch_ref = None
+    if a.torch_baseline > 0 and gpus == 1 and a.model == "VGG11":  # before this process touches the GPU
+        torch_ref = benchlib.torch_eager_baseline(a.torch_baseline, min(a.warmup, 10), a.batch)
     ctx = init_env(device=a.device, comm=a.comm)
     dev = ctx.device
     torch.manual_seed(1)
@@ -322,7 +327,9 @@ def main(argv=None):
             "replicas_identical": pdiff == 0.0,
             "replica_param_max_diff": pdiff,
             "comm_diag": diag,
-            "vs_torch_eager_fp32": round(img_s / (TORCH_EAGER_IMG_S_PER_GPU * ctx.world), 3),
+            # same-run stock-torch comparison (only with --torch-baseline; None otherwise)
+            "torch_eager_fp32_img_s": round(torch_ref["img_per_s"], 1) if torch_ref else None,
+            "vs_torch_eager_fp32": round(img_s / torch_ref["img_per_s"], 3) if torch_ref else None,
             "final_loss": round(loss, 4),
             "param_checksum": checksum,
         }

@@ -68,6 +68,18 @@ int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short*
                       int tile, int reduce, int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig,
                       int sig_val);
 int dpa_wait_signal(const int* sig, int val, long long timeout_us, int* tmo, hipStream_t st);
+int dpa_bn_fused_geo(int Mo, int C, int pool, int bwd, int rmax, long* part_floats, long* cnt_words, int* blocks);
+int dpa_bn_fused_fwd(const float* src, int nsplit, float* zw, int N, int H, int W, int C, int pool, int rmax,
+                     float* part, unsigned* cnt, const float* gamma, const float* beta, const float* bias,
+                     float* rmean, float* rvar, long long* nbt, float* mean, float* invstd, float* scale,
+                     float* shift, int apply, float* out, unsigned short* out3, int np, long ps, float momentum,
+                     float eps, int* tmo, long long timeout_us, hipStream_t st);
+int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H, int W, int C, int pool, int rmax,
+                     float* part, unsigned* cnt, const float* scale, const float* shift, const float* mean,
+                     const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dbias, float* out,
+                     unsigned short* out3, int np, long ps, int* tmo, long long timeout_us, hipStream_t st, int* sig,
+                     int sig_val);
+
 int dpa_set_signal(int* sig, int val, hipStream_t st);
 int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
                     int bf, hipStream_t st);
@@ -656,6 +668,97 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
       "bn_bwd");
 }
 
+// ---------------- one-launch BatchNorm (bn_fused.hip) ----------------
+// (part_floats, cnt_words, blocks) of the fused layer, or None when its geometry does not fit.
+py::object bn_fused_geo(int64_t Mo, int64_t C, bool pool, bool bwd, int64_t rmax) {
+  long pf = 0, cw = 0;
+  int nb = 0;
+  if (dpa_bn_fused_geo((int)Mo, (int)C, pool ? 1 : 0, bwd ? 1 : 0, (int)rmax, &pf, &cw, &nb) != 0) return py::none();
+  return py::make_tuple((int64_t)pf, (int64_t)cw, (int64_t)nb);
+}
+
+// out (optional): fp32 [N,Ho,Wo,C] or bf16 planes [NP,N,Ho,Wo,C]; fp32 only
+struct OutPtrs {
+  float* f = nullptr;
+  u16* b = nullptr;
+  int np = 0;
+  long ps = 0;
+};
+OutPtrs out_ptrs(const OptT& out, int64_t n, const char* what) {
+  OutPtrs o;
+  if (!out.has_value() || !out->defined()) return o;
+  const Tensor& t = *out;
+  if (t.scalar_type() == at::kBFloat16) {
+    if (t.numel() == n) {
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous(), what, ": out must be contiguous");
+      o.np = 1;
+    } else {
+      need_planes(t, what);
+      TORCH_CHECK(t.numel() == t.size(0) * n, what, ": planes shape");
+      o.np = t.size(0);
+    }
+    o.b = up(t);
+    o.ps = n;
+  } else {
+    need(t, what);
+    TORCH_CHECK(t.numel() == n, what, ": out shape");
+    o.f = fp(t);
+  }
+  return o;
+}
+
+void bn_fused_fwd(Tensor src, int64_t nsplit, Tensor z, bool pool, int64_t rmax, Tensor part, Tensor cnt,
+                  Tensor gamma, Tensor beta, OptT bias, OptT rmean, OptT rvar, OptT nbt, Tensor mean, Tensor invstd,
+                  Tensor scale, Tensor shift, OptT out, double momentum, double eps, Tensor tmo,
+                  int64_t timeout_us) {
+  need(src, "src");
+  need(z, "z");
+  need(part, "part");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32, "bn_fused_fwd: cnt must be int32");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
+  long pf = 0, cw = 0;
+  int nb = 0;
+  TORCH_CHECK(dpa_bn_fused_geo(Mo, C, pool ? 1 : 0, 0, (int)rmax, &pf, &cw, &nb) == 0, "bn_fused_fwd: no geometry");
+  TORCH_CHECK(part.numel() >= pf && cnt.numel() >= cw, "bn_fused_fwd: workspace too small");
+  TORCH_CHECK(src.numel() >= nsplit * z.numel(), "bn_fused_fwd: src too small");
+  long long* nb_p = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    need(*nbt, "nbt", at::kLong);
+    nb_p = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  const OutPtrs o = out_ptrs(out, (int64_t)Mo * C, "bn_fused_fwd");
+  chk(dpa_bn_fused_fwd(fp(src), (int)nsplit, fp(z), N, H, W, C, pool ? 1 : 0, (int)rmax, fp(part),
+                       reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), fp(gamma), fp(beta), ofp(bias), ofp(rmean),
+                       ofp(rvar), nb_p, fp(mean), fp(invstd), fp(scale), fp(shift), (o.f || o.b) ? 1 : 0, o.f, o.b,
+                       o.np, o.ps, (float)momentum, (float)eps, signal_ptr(tmo, "bn_fused_fwd"), timeout_us,
+                       cur_stream()),
+      "bn_fused_fwd");
+}
+
+void bn_fused_bwd(Tensor gsrc, int64_t nsplit, Tensor z, bool pool, int64_t rmax, Tensor part, Tensor cnt,
+                  Tensor scale, Tensor shift, Tensor mean, Tensor invstd, Tensor gamma, Tensor dgamma, Tensor dbeta,
+                  OptT dbias, Tensor dz, Tensor tmo, int64_t timeout_us, OptT sig, int64_t sig_val) {
+  need(gsrc, "gsrc");
+  need(z, "z");
+  need(part, "part");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32, "bn_fused_bwd: cnt must be int32");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
+  long pf = 0, cw = 0;
+  int nb = 0;
+  TORCH_CHECK(dpa_bn_fused_geo(Mo, C, pool ? 1 : 0, 1, (int)rmax, &pf, &cw, &nb) == 0, "bn_fused_bwd: no geometry");
+  TORCH_CHECK(part.numel() >= pf && cnt.numel() >= cw, "bn_fused_bwd: workspace too small");
+  TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_fused_bwd: gsrc too small");
+  const OutPtrs o = out_ptrs(dz, z.numel(), "bn_fused_bwd");
+  chk(dpa_bn_fused_bwd(fp(gsrc), (int)nsplit, fp(z), N, H, W, C, pool ? 1 : 0, (int)rmax, fp(part),
+                       reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), fp(scale), fp(shift), fp(mean), fp(invstd),
+                       fp(gamma), fp(dgamma), fp(dbeta), ofp(dbias), o.f, o.b, o.np, o.ps,
+                       signal_ptr(tmo, "bn_fused_bwd"), timeout_us, cur_stream(), opt_signal(sig, "bn_fused_bwd"),
+                       (int)sig_val),
+      "bn_fused_bwd");
+}
+
 // ---------------- classifier head ----------------
 // bn_z [B,2,2,Cin] fp32 + bn_scale/bn_shift [Cin] (optional): the features x [B,Cin] are computed
 // from the last conv's output (BN + ReLU + 2x2 max-pool) inside the head kernel and written to x
@@ -890,6 +993,17 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
         py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none());
+  m.def("bn_fused_geo", &bn_fused_geo, py::arg("Mo"), py::arg("C"), py::arg("pool"), py::arg("bwd"),
+        py::arg("rmax"));
+  m.def("bn_fused_fwd", &bn_fused_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
+        py::arg("rmax"), py::arg("part"), py::arg("cnt"), py::arg("gamma"), py::arg("beta"), py::arg("bias"),
+        py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("mean"), py::arg("invstd"), py::arg("scale"),
+        py::arg("shift"), py::arg("out"), py::arg("momentum"), py::arg("eps"), py::arg("tmo"),
+        py::arg("timeout_us"));
+  m.def("bn_fused_bwd", &bn_fused_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
+        py::arg("rmax"), py::arg("part"), py::arg("cnt"), py::arg("scale"), py::arg("shift"), py::arg("mean"),
+        py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"),
+        py::arg("tmo"), py::arg("timeout_us"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
   m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
         py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("x"), py::arg("wpart"),
@@ -951,16 +1065,19 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         c.set(k, sv);
       })
-      .def("get", [](dpa::TcpStoreClient& c, const std::string& k) {
+      .def("get", [](dpa::TcpStoreClient& c, const std::string& k, double timeout_s) {
         std::string v;
         {
           py::gil_scoped_release nogil;
-          v = c.get(k);
+          v = c.get(k, timeout_s);
         }
         return py::bytes(v);
-      })
+      }, py::arg("key"), py::arg("timeout_s") = -1.0)
       .def("add", &dpa::TcpStoreClient::add, py::call_guard<py::gil_scoped_release>())
-      .def("wait", &dpa::TcpStoreClient::wait, py::call_guard<py::gil_scoped_release>())
+      .def("delete", &dpa::TcpStoreClient::del, py::call_guard<py::gil_scoped_release>())
+      .def("num_keys", &dpa::TcpStoreClient::num_keys, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &dpa::TcpStoreClient::wait, py::arg("keys"), py::arg("timeout_s") = -1.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("barrier", &dpa::TcpStoreClient::barrier, py::call_guard<py::gil_scoped_release>());
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool>(), py::arg("rank"),

@@ -52,9 +52,35 @@ RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipS
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
   check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  comm_raw_ = comm_;
   hip_check(hipEventCreateWithFlags(&ev_in_, event_flags()), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_out_, event_flags()), "hipEventCreate");
+  const char* w = std::getenv("DPA_RCCL_WARMUP");
+  if (world_ > 1 && !(w && std::string(w) == "0")) warmup_connections();
   if (wd_.enabled) watchdog_ = std::thread([this] { watchdog_loop(); });
+}
+
+// RCCL connects peers lazily, inside the first collective / send-recv group that needs them, and
+// that enqueue call can block on a dead peer while it holds comm_mu_.  One tiny round of every
+// pattern the sync modes issue (all-reduce, broadcast, the gather's grouped send/recv to rank 0)
+// at start-up makes every later enqueue a pure queue operation.
+void RcclComm::warmup_connections() {
+  void* buf = nullptr;
+  const size_t n = 64;  // floats per rank
+  hip_check(hipMalloc(&buf, n * sizeof(float) * (size_t)(world_ + 1)), "hipMalloc");
+  hip_check(hipMemsetAsync(buf, 0, n * sizeof(float) * (size_t)(world_ + 1), stream_), "hipMemsetAsync");
+  float* b = static_cast<float*>(buf);
+  check(ncclAllReduce(b, b, n, ncclFloat32, ncclSum, comm_, stream_), "ncclAllReduce(warmup)");
+  check(ncclBroadcast(b, b, n, ncclFloat32, 0, comm_, stream_), "ncclBroadcast(warmup)");
+  check(ncclGroupStart(), "ncclGroupStart");
+  if (rank_ == 0) {
+    for (int p = 1; p < world_; ++p) check(ncclRecv(b + (size_t)p * n, n, ncclFloat32, p, comm_, stream_), "ncclRecv");
+  } else {
+    check(ncclSend(b + (size_t)world_ * n, n, ncclFloat32, 0, comm_, stream_), "ncclSend");
+  }
+  check(ncclGroupEnd(), "ncclGroupEnd");
+  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(warmup)");
+  hip_check(hipFree(buf), "hipFree");
 }
 
 RcclComm::~RcclComm() {
@@ -75,7 +101,9 @@ RcclComm::~RcclComm() {
 
 void RcclComm::release_locked(bool abort) {
   if (comm_) {
-    if (abort)
+    if (aborted_unlocked_.load())
+      ;  // already aborted by the watchdog while an issuer was stuck in RCCL: only drop the handle
+    else if (abort)
       ncclCommAbort(comm_);
     else
       ncclCommDestroy(comm_);
@@ -146,12 +174,23 @@ void RcclComm::fail(const std::string& msg) {
     std::_Exit(70);
   }
   // Abort under comm_mu_: an issue that is in flight finishes first (enqueue calls return without
-  // waiting on peers), and no issuer can ever see the handle after it is released.
+  // waiting on peers), and no issuer can ever see the handle after it is released.  An issuer that
+  // holds the lock longer than the timeout is itself stuck inside RCCL: abort the communicator
+  // from here without the lock (unblocking it), then drop the handle once it lets go.
+  const auto t0 = std::chrono::steady_clock::now();
   while (!stop_) {
     Lock g(comm_mu_, std::defer_lock);
     if (g.try_lock_for(std::chrono::milliseconds(500))) {
       release_locked(true);
       return;
+    }
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!aborted_unlocked_.load() && waited > wd_.timeout_s && comm_raw_) {
+      std::fprintf(stderr, "[dpa rank %d] RCCL watchdog: an enqueue is stuck inside RCCL; aborting the communicator\n",
+                   rank_);
+      std::fflush(stderr);
+      ncclCommAbort(comm_raw_);
+      aborted_unlocked_ = true;
     }
   }
 }

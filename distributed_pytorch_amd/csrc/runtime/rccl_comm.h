@@ -89,9 +89,15 @@ class RcclComm {
   void watchdog_loop();
   void fail(const std::string& msg);  // watchdog thread only
   void release_locked(bool abort);    // caller holds comm_mu_
+  void warmup_connections();          // constructor only
 
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;  // guarded by comm_mu_
+  // The handle as created, for the one abort the watchdog may issue WITHOUT comm_mu_: when an
+  // issuer has held the lock past the timeout it is stuck inside RCCL (ncclCommAbort is callable
+  // from another thread and unblocks it); the handle is then only cleared, never released again.
+  ncclComm_t comm_raw_ = nullptr;
+  std::atomic<bool> aborted_unlocked_{false};
   std::timed_mutex comm_mu_;
   hipStream_t stream_;
   hipEvent_t ev_in_, ev_out_;

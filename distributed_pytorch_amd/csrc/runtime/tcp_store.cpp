@@ -15,7 +15,7 @@ namespace dpa {
 
 namespace {
 
-enum : char { OP_SET = 'S', OP_GET = 'G', OP_ADD = 'A' };
+enum : char { OP_SET = 'S', OP_GET = 'G', OP_ADD = 'A', OP_DEL = 'D', OP_NKEYS = 'N' };
 enum : char { ST_OK = 0, ST_TIMEOUT = 1 };
 
 bool send_all(int fd, const void* p, size_t n) {
@@ -146,6 +146,12 @@ void TcpStoreServer::serve(int fd) {
       } else {
         st = ST_TIMEOUT;
       }
+    } else if (op == OP_DEL) {
+      std::lock_guard<std::mutex> g(mu_);
+      out = i64(kv_.erase(key) ? 1 : 0);
+    } else if (op == OP_NKEYS) {
+      std::lock_guard<std::mutex> g(mu_);
+      out = i64((long long)kv_.size());
     } else {
       return;  // protocol error: drop the connection
     }
@@ -195,20 +201,40 @@ std::string TcpStoreClient::request(char op, const std::string& key, const std::
 
 void TcpStoreClient::set(const std::string& key, const std::string& value) { request(OP_SET, key, value); }
 
-std::string TcpStoreClient::get(const std::string& key) {
-  return request(OP_GET, key, std::to_string((long)(timeout_s_ * 1000.0)));
+std::string TcpStoreClient::get(const std::string& key, double timeout_s) {
+  const double t = timeout_s >= 0 ? timeout_s : timeout_s_;
+  return request(OP_GET, key, std::to_string((long)(t * 1000.0)));
 }
 
 long long TcpStoreClient::add(const std::string& key, long long delta) { return i64of(request(OP_ADD, key, i64(delta))); }
 
-void TcpStoreClient::wait(const std::vector<std::string>& keys) {
-  for (const auto& k : keys) get(k);
+bool TcpStoreClient::del(const std::string& key) { return i64of(request(OP_DEL, key, "")) != 0; }
+
+long long TcpStoreClient::num_keys() { return i64of(request(OP_NKEYS, "", "")); }
+
+// every key within ONE overall deadline (not timeout_s per key)
+void TcpStoreClient::wait(const std::vector<std::string>& keys, double timeout_s) {
+  const double t = timeout_s >= 0 ? timeout_s : timeout_s_;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(t);
+  for (const auto& k : keys) {
+    const double left = std::chrono::duration<double>(deadline - std::chrono::steady_clock::now()).count();
+    get(k, left > 0 ? left : 0.0);
+  }
 }
 
+// Counter barrier that leaves nothing behind: arrivals count up, the last arrival publishes
+// "done", every rank then checks out, and the last to check out deletes the three keys (nobody
+// reads them any more).
 void TcpStoreClient::barrier(const std::string& tag, int world) {
-  const long long n = add("__barrier_cnt/" + tag, 1);
-  if (n == world) set("__barrier_done/" + tag, "1");
-  get("__barrier_done/" + tag);
+  const std::string cnt = "__barrier_cnt/" + tag, done = "__barrier_done/" + tag, out = "__barrier_out/" + tag;
+  const long long n = add(cnt, 1);
+  if (n == world) set(done, "1");
+  get(done);
+  if (add(out, 1) == world) {
+    del(cnt);
+    del(done);
+    del(out);
+  }
 }
 
 }  // namespace dpa

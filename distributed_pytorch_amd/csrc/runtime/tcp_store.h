@@ -3,8 +3,8 @@
 //
 // Rank 0 runs the server thread; every rank (including 0) talks to it through a client socket.
 // Operations: set(key, bytes), get(key) -> bytes (blocks until present or timeout), add(key, n) ->
-// new value (atomic counter), wait(keys), and a counter barrier built on add+wait.  Keys live for
-// the lifetime of the server.  Length-prefixed binary protocol; one request in flight per client.
+// new value (atomic counter), wait(keys), delete(key), and a counter barrier built on add+wait that
+// removes its keys when the last participant leaves.  Length-prefixed binary protocol; one request in flight per client.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -42,10 +42,14 @@ class TcpStoreClient {
   TcpStoreClient(const std::string& host, int port, double timeout_s);
   ~TcpStoreClient();
   void set(const std::string& key, const std::string& value);
-  std::string get(const std::string& key);  // blocks until the key exists (bounded by timeout)
+  // blocks until the key exists, at most timeout_s (< 0: the client's default timeout)
+  std::string get(const std::string& key, double timeout_s = -1.0);
   long long add(const std::string& key, long long delta);
-  void wait(const std::vector<std::string>& keys);
-  // all `world` participants call with the same tag; returns once all arrived
+  bool del(const std::string& key);  // true if the key existed
+  long long num_keys();
+  void wait(const std::vector<std::string>& keys, double timeout_s = -1.0);
+  // all `world` participants call with the same tag; returns once all arrived; its keys are
+  // deleted by the last participant to leave
   void barrier(const std::string& tag, int world);
 
  private:

@@ -217,7 +217,11 @@ class VGGEngine:
         self.bsig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None  # BN bwd starts
         self.ksig_tmo = torch.zeros(1, dtype=torch.int32, device=dev) if self.ksignal else None
         self._sig_epoch = 0
-        self.ksig_timeout_us = int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "60000000"))
+        # A wait may legitimately last as long as the main stream is held behind the previous step's
+        # collectives (a slow peer: up to the communicator's DPA_COMM_TIMEOUT, after which the RCCL
+        # watchdog aborts), so the bound is never shorter than that plus a minute.
+        comm_us = int(float(os.environ.get("DPA_COMM_TIMEOUT", "600")) * 1e6)
+        self.ksig_timeout_us = max(int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "0")), comm_us + 60_000_000)
         # params_free hands the sync a later kernel's signal instead of recording an event (A/B: 0)
         self.free_signal = os.environ.get("DPA_FREE_SIGNAL", "1") == "1"
         self.slab = torch.empty(1, **f32)
@@ -246,6 +250,24 @@ class VGGEngine:
         lL = L[-1]
         self.fused_head = (dev.type == "cuda" and os.environ.get("DPA_FUSED_HEAD", "1") == "1" and lL.pool
                            and lL.hw == 2 and self.spec.fc_in == lL.cout and self.a[-1] is not None)
+        # One-launch BatchNorm (bn_fused.hip) for the small layers: statistics, finalize and apply
+        # (forward) / reduce, finalize and apply (backward) in one kernel whose blocks meet per
+        # channel slice.  Used where z has at most DPA_BN_FUSED_MAX elements (0: never) and the tile
+        # geometry fits (<= DPA_BN_FUSED_RMAX row blocks per slice).  Counters self-reset; the
+        # workspace is zeroed once here.
+        self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", str(2200000))) if dev.type == "cuda" else 0
+        self.bn_fused_rmax = int(os.environ.get("DPA_BN_FUSED_RMAX", "64"))
+        self._fgeo: Dict[tuple, bool] = {}
+        fpart, fcnt = 0, 0
+        if self.bn_fused_max > 0 and hasattr(self.K, "bn_fused_geo"):
+            for i, l in enumerate(L):
+                for bwd in (False, True):
+                    gq = self._fused_geo(i, N, bwd)
+                    if gq is not None:
+                        fpart, fcnt = max(fpart, gq[0]), max(fcnt, gq[1])
+        self.fpart = torch.zeros(max(fpart, 1), **f32)
+        self.fcnt = torch.zeros(max(fcnt, 32), dtype=torch.int32, device=dev)
+        self.bn_tmo = torch.zeros(1, dtype=torch.int32, device=dev)
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -379,6 +401,23 @@ class VGGEngine:
     def num_parameters(self) -> int:
         return sum(p.numel() for p in self.state_dict().values() if p.dtype == torch.float32) - sum(
             self.buffers.numels.values())
+
+    def _fused_geo(self, i: int, n: int, bwd: bool):
+        """(part_floats, cnt_words, blocks) when layer i's BN runs as one launch at batch n, else None."""
+        if self.bn_fused_max <= 0 or not hasattr(self.K, "bn_fused_geo"):
+            return None
+        l = self.spec.convs[i]
+        if i == 0 or n * l.hw * l.hw * l.cout > self.bn_fused_max:
+            return None  # layer 0: conv0_fwd / bn_bwd_wgrad0 fuse its BN with the convolution instead
+        ho = l.hw // 2 if l.pool else l.hw
+        return self.K.bn_fused_geo(n * ho * ho, l.cout, l.pool, bwd, self.bn_fused_rmax)
+
+    def _fused(self, i: int, n: int, bwd: bool) -> bool:
+        key = (i, n, bwd)
+        v = self._fgeo.get(key)
+        if v is None:
+            v = self._fgeo[key] = self._fused_geo(i, n, bwd) is not None
+        return v
 
     # ------------------------------------------------------------------ kernel configs
     def _layer_impl(self, i: int) -> str:
@@ -602,6 +641,15 @@ class VGGEngine:
             if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
                 buffers_wait()
                 buffers_wait = None
+            if self._fused(i, n, False):
+                head = i == len(L) - 1 and self.fused_head  # the head kernel applies it
+                K.bn_fused_fwd(self.slab if ns > 1 else z, ns, z, l.pool, self.bn_fused_rmax, self.fpart, self.fcnt,
+                               P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
+                               self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
+                               self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
+                               None if head else self._act_out(i, n), self.bn_momentum, self.bn_eps, self.bn_tmo,
+                               self.ksig_timeout_us)
+                continue
             K.bn_fwd_stats(self.slab if ns > 1 else z, ns, z, self.part, P[f"{l.bn_key}.weight"],
                            P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
@@ -690,9 +738,15 @@ class VGGEngine:
                 if params_free is not None:
                     params_free(names)
                 continue
-            K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
-                     st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                     G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig)
+            if self._fused(i, n, True):
+                K.bn_fused_bwd(self.slab if gsplit > 1 else g, gsplit, z, l.pool, self.bn_fused_rmax, self.fpart,
+                               self.fcnt, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
+                               G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf,
+                               self.bn_tmo, self.ksig_timeout_us, **bsig)
+            else:
+                K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
+                         st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
+                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig)
             after_bn(i)
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
@@ -766,6 +820,9 @@ class VGGEngine:
         if self.ksig_tmo is not None and int(self.ksig_tmo.item()) != 0:
             raise RuntimeError("VGGEngine: a wgrad-stream signal wait timed out "
                                f"(DPA_KSIGNAL_TIMEOUT_US={self.ksig_timeout_us}); weight gradients are invalid")
+        if int(self.bn_tmo.item()) != 0:
+            raise RuntimeError("VGGEngine: a one-launch BatchNorm slice rendezvous timed out; this step's "
+                               "activations / gradients are invalid")
 
     def finish_step(self):
         self.steps_taken += 1

@@ -15,14 +15,21 @@ path as under torchrun), and supervises them:
 
 Each child runs in its own process group so that the teardown reaches any helper processes it
 started; only the exact process groups started here are signalled.
+
+The teardown also runs when the launcher itself is told to stop: SIGTERM / SIGHUP / SIGINT raise
+into it (exit code 128 + signal).  And if the launcher dies without running it (SIGKILL, a crashed
+interpreter), every child gets SIGTERM from the kernel (``PR_SET_PDEATHSIG``), so no rank is left
+holding a GPU while its peers hang in a collective until the watchdog.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -54,6 +61,23 @@ def rank_env(rank: int, world: int, port: int, store_port: int, base: Optional[D
     return env
 
 
+class _Stopped(Exception):
+    def __init__(self, signum: int):
+        super().__init__(signum)
+        self.signum = signum
+
+
+def _die_with_parent(parent: int):
+    """preexec_fn of every rank (runs in the child between fork and exec): SIGTERM when the launcher
+    dies; exit at once if it is already gone."""
+    try:
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+    if os.getppid() != parent:
+        os._exit(1)
+
+
 def _kill_group(p: subprocess.Popen, sig: int):
     try:
         os.killpg(p.pid, sig)
@@ -70,15 +94,24 @@ def launch(script: str, argv: Sequence[str], nprocs: int, timeout_s: float = 180
     port, store_port = free_port_pair()
     procs: List[subprocess.Popen] = []
     py = python or sys.executable
-    for r in range(nprocs):
-        env = rank_env(r, nprocs, port, store_port)
-        if extra_env:
-            env.update(extra_env)
-        procs.append(subprocess.Popen([py, script, *argv], env=env, start_new_session=True))
-    deadline = time.monotonic() + timeout_s
+    parent = os.getpid()
+    old_handlers = {}
+    if threading.current_thread() is threading.main_thread():
+        def _on_signal(signum, _frame):
+            raise _Stopped(signum)
+
+        for sg in (signal.SIGTERM, signal.SIGHUP, signal.SIGINT):
+            old_handlers[sg] = signal.signal(sg, _on_signal)
     code = 0
     failed: Optional[int] = None
     try:
+        for r in range(nprocs):
+            env = rank_env(r, nprocs, port, store_port)
+            if extra_env:
+                env.update(extra_env)
+            procs.append(subprocess.Popen([py, script, *argv], env=env, start_new_session=True,
+                                          preexec_fn=lambda: _die_with_parent(parent)))
+        deadline = time.monotonic() + timeout_s
         while True:
             alive = 0
             for r, p in enumerate(procs):
@@ -97,9 +130,15 @@ def launch(script: str, argv: Sequence[str], nprocs: int, timeout_s: float = 180
                 code = 124
                 break
             time.sleep(0.05)
+    except _Stopped as e:
+        print(f"[launch] launcher received signal {e.signum}; stopping all ranks", file=sys.stderr, flush=True)
+        code = 128 + e.signum
     except KeyboardInterrupt:
         code = 130
     finally:
+        # a second signal during the teardown must not abort it half-way
+        for sg in old_handlers:
+            signal.signal(sg, signal.SIG_IGN)
         live = [p for p in procs if p.poll() is None]
         for p in live:
             _kill_group(p, signal.SIGTERM)
@@ -110,6 +149,8 @@ def launch(script: str, argv: Sequence[str], nprocs: int, timeout_s: float = 180
             except subprocess.TimeoutExpired:
                 _kill_group(p, signal.SIGKILL)
                 p.wait()
+        for sg, h in old_handlers.items():
+            signal.signal(sg, h)
     return code
 
 

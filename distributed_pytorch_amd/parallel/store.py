@@ -30,7 +30,14 @@ class NativeStore:
         return self._c.get(key)
 
     def wait(self, keys: List[str], timeout: Optional[datetime.timedelta] = None) -> None:
-        self._c.wait(list(keys))
+        """Block until every key exists; ``timeout`` bounds the whole wait (default: the store's)."""
+        self._c.wait(list(keys), timeout.total_seconds() if timeout is not None else -1.0)
+
+    def delete_key(self, key: str) -> bool:
+        return bool(self._c.delete(key))
+
+    def num_keys(self) -> int:
+        return int(self._c.num_keys())
 
     def add(self, key: str, delta: int) -> int:
         return self._c.add(key, int(delta))
@@ -53,6 +60,12 @@ class NativeStore:
         self._server = None
 
     def all_max(self, tag: str, value: float) -> float:
-        """Max of one float over all ranks (every rank gets it)."""
+        """Max of one float over all ranks (every rank gets it).  The last rank to finish reading
+        deletes the tag's keys, so repeated calls leave nothing behind in the store."""
         self.set(f"{tag}/{self.rank}", struct.pack("<d", float(value)))
-        return max(struct.unpack("<d", self.get(f"{tag}/{r}"))[0] for r in range(self.world))
+        m = max(struct.unpack("<d", self.get(f"{tag}/{r}"))[0] for r in range(self.world))
+        if self.add(f"{tag}/out", 1) == self.world:
+            for r in range(self.world):
+                self._c.delete(f"{tag}/{r}")
+            self._c.delete(f"{tag}/out")
+        return m

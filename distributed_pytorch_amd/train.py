@@ -114,6 +114,7 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
             t_win = now
             ctx.comm.check()
         if ck_every and args.checkpoint_dir and (batch_idx + 1) % ck_every == 0:
+            engine.check_signals()  # never save weights built from a step whose cross-stream wait gave up
             sync.prepare_checkpoint()
             checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch, batch_idx + 1, args.sampler_seed, ctx.world,
                             sync.mode, ddp_prefix=sync.mode == "ddp")

@@ -87,7 +87,32 @@ def replicas_max_diff(comm, flat: torch.Tensor) -> float:
     return float((mx - mn).abs().max().item())
 
 
-def comm_world(comm) -> int:
-    """Ranks the communicator itself reports (RCCL: ncclCommCount)."""
+def comm_world(comm) -> Optional[int]:
+    """Ranks an RCCL communicator itself reports (ncclCommCount); None when the run has no RCCL
+    communicator (null comm of a 1-GPU run, torch/gloo process groups)."""
     f = getattr(comm, "comm_count", None)
-    return int(f()) if f is not None else int(comm.world)
+    return int(f()) if f is not None else None
+
+
+def torch_eager_baseline(steps: int, warmup: int, batch: int, timeout_s: float = 300.0) -> Optional[dict]:
+    """Stock PyTorch-ROCm eager fp32 VGG-11 step (tools/torch_baseline.py: MIOpen convs, torch SGD)
+    timed in a CHILD process on this run's GPU, before this process touches the device.  Returns
+    its JSON record, or None if it failed."""
+    import json
+
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tools",
+                        "torch_baseline.py")
+    cmd = [sys.executable, tool, "--steps", str(steps), "--warmup", str(warmup), "--batch", str(batch),
+           "--modes", "fp32"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return None
+    if r.returncode != 0:
+        return None
+    for line in reversed(r.stdout.strip().splitlines()):
+        try:
+            return json.loads(line)
+        except ValueError:
+            continue
+    return None

@@ -14,7 +14,9 @@ Loading uses ``torch.load(weights_only=True)`` — nothing in the file is execut
 Resume safety:
 * a checkpoint written by a run with a different world size or sync mode is refused (its
   ``batch_idx`` indexes a different shard); ``reshard=True`` (``--resume-reshard``) loads the
-  weights and optimizer state anyway and restarts the saved epoch at batch 0;
+  weights and optimizer state anyway and restarts the saved epoch at batch 0.  A rank with no file
+  of its own (the world grew: ranks >= the old world size) then loads the lowest-numbered rank's
+  file — after ``prepare_checkpoint`` every rank saved identical parameters and full momentum;
 * ``agree`` (after every rank loaded) checks that all ranks resume from the same
   (epoch, batch_idx, steps_taken) — ranks holding checkpoints of different iterations (a crash
   between two ``--checkpoint-every`` writes) or a rank without one would otherwise pair gradients
@@ -65,8 +67,17 @@ def load(ckpt_dir: str, rank: int, engine, map_location="cpu", world: Optional[i
     validated against the saved ones."""
     p = path_for(ckpt_dir, rank)
     if not os.path.exists(p):
-        return None
-    obj = torch.load(p, map_location=map_location, weights_only=True)
+        if not reshard:
+            return None
+        p = _donor(ckpt_dir)
+        if p is None:
+            return None
+        obj = torch.load(p, map_location=map_location, weights_only=True)
+        if (world is None or obj.get("world") is None or int(obj["world"]) == int(world)) and (
+                mode is None or obj.get("mode") in (None, mode)):
+            return None  # same topology: this rank's own checkpoint is genuinely missing (agree refuses)
+    else:
+        obj = torch.load(p, map_location=map_location, weights_only=True)
     saved_w, saved_m = obj.get("world"), obj.get("mode")
     mismatch = []
     if world is not None and saved_w is not None and int(saved_w) != int(world):
@@ -90,6 +101,15 @@ def load(ckpt_dir: str, rank: int, engine, map_location="cpu", world: Optional[i
     return obj
 
 
+def _donor(ckpt_dir: str) -> Optional[str]:
+    """Lowest-numbered rank file in ckpt_dir (the checkpoint a new rank of a grown world loads)."""
+    if not os.path.isdir(ckpt_dir):
+        return None
+    ranks = sorted(int(f[4:-3]) for f in os.listdir(ckpt_dir)
+                   if f.startswith("rank") and f.endswith(".pt") and f[4:-3].isdigit())
+    return path_for(ckpt_dir, ranks[0]) if ranks else None
+
+
 def resume_point(obj: Optional[dict]) -> Tuple[int, int, int, int]:
     """(has_checkpoint, epoch, batch_idx, steps_taken) of a loaded checkpoint (zeros if none)."""
     if obj is None:
@@ -97,19 +117,36 @@ def resume_point(obj: Optional[dict]) -> Tuple[int, int, int, int]:
     return 1, int(obj["epoch"]), int(obj["batch_idx"]), int(obj.get("steps_taken", 0))
 
 
+def _pieces(point) -> list:
+    """Each value (>= -1, < 2^48 - 1) as three exact 16-bit pieces of value + 1: a float32 all-reduce
+    then compares them exactly (a float32 of a large step count would round)."""
+    out = []
+    for x in point:
+        v = int(x) + 1
+        if v < 0 or v >= 1 << 48:
+            raise ValueError(f"resume point value out of range: {x}")
+        out += [(v >> 32) & 0xFFFF, (v >> 16) & 0xFFFF, v & 0xFFFF]
+    return out
+
+
+def _unpieces(p) -> list:
+    return [(int(p[i]) << 32 | int(p[i + 1]) << 16 | int(p[i + 2])) - 1 for i in range(0, len(p), 3)]
+
+
 def agree(comm, point: Tuple[int, int, int, int], device) -> None:
-    """Raise ResumeMismatch on EVERY rank unless all ranks hold the same resume point.  One
-    all-reduce of (x, -x): max(x) == -max(-x) == min(x) iff all ranks agree."""
+    """Raise ResumeMismatch on EVERY rank unless all ranks hold the same resume point.  One max
+    all-reduce of (x, -x) over exact 16-bit pieces: max(x) == -max(-x) == min(x) iff all agree."""
     if comm.world <= 1:
         return
-    v = torch.tensor(list(point), dtype=torch.float64)
+    v = torch.tensor(_pieces(point), dtype=torch.float64)
     t = torch.cat([v, -v]).to(device=device, dtype=torch.float32 if device.type == "cuda" else torch.float64)
     with comm.region():
         comm.all_reduce(t, "max")
     comm.wait()
     t = t.double().cpu()
-    mx, mn = t[:4], -t[4:]
+    k = v.numel()
+    mx, mn = t[:k], -t[k:]
     if not torch.equal(mx, mn):
         raise ResumeMismatch(f"ranks disagree on the resume point (has_ckpt, epoch, batch_idx, steps_taken): "
-                             f"max {mx.long().tolist()} vs min {mn.long().tolist()}, this rank "
+                             f"max {_unpieces(mx.tolist())} vs min {_unpieces(mn.tolist())}, this rank "
                              f"{list(point)}; refusing to pair gradients of different steps")

@@ -172,18 +172,35 @@ def run_native_store(rank, world, port, outdir):
     from distributed_pytorch_amd.parallel.comm import exchange_unique_id
     from distributed_pytorch_amd.parallel.store import NativeStore
 
+    import datetime
+    import time
+
     st = NativeStore("127.0.0.1", port, rank, world, timeout_s=60)
     uid = exchange_unique_id(st, rank, lambda: bytes(range(128)), tag="uid")
     st.barrier("b1")
     mx = st.all_max("m", 1.5 * rank + 0.25)
     cnt = st.add("c", 1)
     st.barrier("b2")
+    n0 = st.num_keys()
+    for i in range(10):  # barriers and max-reduces clean up after themselves
+        st.barrier(f"loop{i}")
+        st.all_max(f"lm{i}", float(i + rank))
+    st.barrier("b3")
+    n1 = st.num_keys()
+    t0 = time.monotonic()
+    try:
+        st.wait(["never-set"], datetime.timedelta(seconds=0.5))
+        waited = None
+    except RuntimeError:
+        waited = time.monotonic() - t0
+    st.barrier("b4")
     with open(os.path.join(outdir, f"ns_{rank}.json"), "w") as f:
-        json.dump({"uid": list(uid), "max": mx, "cnt": cnt}, f)
+        json.dump({"uid": list(uid), "max": mx, "cnt": cnt, "keys_before": n0, "keys_after": n1,
+                   "bounded_wait_s": waited}, f)
     st.close()  # rank 0 keeps serving until every client checked out
 
 
-def run_resume_agree(rank, world, port, ckdir, outdir, batch_idx_by_rank, world_saved=None):
+def run_resume_agree(rank, world, port, ckdir, outdir, batch_idx_by_rank, world_saved=None, reshard=False):
     """Each rank writes a checkpoint (its own batch index, or none if None), then resumes through
     train.resume exactly like a training run; records what happened."""
     import argparse
@@ -198,13 +215,17 @@ def run_resume_agree(rank, world, port, ckdir, outdir, batch_idx_by_rank, world_
     comm = TorchComm(device=torch.device("cpu"))
     ctx = DistContext(rank, world, rank, torch.device("cpu"), comm, True)
     e = VGGEngine("VGG11", "cpu", max_batch=4)
-    bi = batch_idx_by_rank[rank]
+    bi = batch_idx_by_rank[rank] if rank < len(batch_idx_by_rank) else None
     if bi is not None:
+        e.init_parameters(seed=11)
+        e.steps_taken = 7
         checkpoint.save(ckdir, rank, e, 0, bi, 0, world_saved or world, "ddp", ddp_prefix=True)
     dist.barrier()
-    args = argparse.Namespace(resume=True, checkpoint_dir=ckdir, resume_reshard=False)
+    e = VGGEngine("VGG11", "cpu", max_batch=4)
+    args = argparse.Namespace(resume=True, checkpoint_dir=ckdir, resume_reshard=reshard)
     try:
-        out = {"ok": list(resume(ctx, e, "ddp", args, 100))}
+        out = {"ok": list(resume(ctx, e, "ddp", args, 100)), "steps_taken": e.steps_taken,
+               "param_sum": float(e.params.flat.double().sum())}
     except checkpoint.ResumeMismatch as ex:
         out = {"error": str(ex)}
     with open(os.path.join(outdir, f"resume_{rank}.json"), "w") as f:

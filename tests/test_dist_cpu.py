@@ -153,6 +153,9 @@ def test_native_tcp_store(tmp_path):
         assert r["uid"] == list(range(128))
         assert r["max"] == 1.5 * (WORLD - 1) + 0.25
     assert sorted(r["cnt"] for r in res) == list(range(1, WORLD + 1))
+    for r in res:  # 10 barriers + 10 max-reduces leave at most one barrier's 3 keys in flight
+        assert r["keys_after"] <= r["keys_before"] + 3, r
+        assert r["bounded_wait_s"] is not None and 0.3 < r["bounded_wait_s"] < 5.0, r
 
 
 def _run_ranks(script, args, outdir, world):

@@ -3,6 +3,7 @@ round-end driver runs as ``python bench.py --gpus N`` must start N ranks, report
 and turn a failed or hung rank into a non-zero exit instead of a hang."""
 import json
 import os
+import signal
 import subprocess
 import sys
 import textwrap
@@ -97,7 +98,8 @@ def test_bench_self_launch_two_ranks_cpu():
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["launcher"] == "spawn"
     assert rec["config"]["global_batch"] == 8
-    assert rec["replicas_identical"] is True and rec["rccl_world"] == 2
+    assert rec["replicas_identical"] is True
+    assert rec["rccl_world"] is None  # gloo process group: no RCCL communicator exists
     assert rec["scaling_efficiency"] is not None and rec["value"] > 0
     # the warmup-time gradient-sync plan choice: every candidate timed, one chosen, reported
     tune = rec["config"]["comm_tune"]
@@ -115,6 +117,76 @@ def test_bench_self_launch_two_ranks_cpu():
     rec2 = json.loads([l for l in r2.stdout.splitlines() if l.startswith("{")][-1])
     assert rec2["config"]["comm_tune"] is None
     assert rec2["param_checksum"] == rec["param_checksum"] and rec2["final_loss"] == rec["final_loss"]
+
+
+def test_bench_single_rank_reports_no_rccl_world():
+    """A 1-GPU-style run has a null communicator: ``rccl_world`` must be None (not 1), and without
+    --torch-baseline the stock-torch comparison fields are None (never a stale constant)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", spawn.SPAWNED_ENV)}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--batch", "4",
+                        "--steps", "1", "--warmup", "1", "--diag-steps", "0"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 1 and rec["config"]["comm"] == "null"
+    assert rec["rccl_world"] is None
+    assert rec["vs_torch_eager_fp32"] is None and rec["torch_eager_fp32_img_s"] is None
+
+
+def test_comm_world_only_for_rccl():
+    from distributed_pytorch_amd.parallel import NullComm
+    from distributed_pytorch_amd.utils.benchlib import comm_world
+
+    class FakeRccl:
+        world = 4
+
+        def comm_count(self):
+            return 4
+
+    assert comm_world(NullComm()) is None
+    assert comm_world(FakeRccl()) == 4
+
+
+def _alive(pid: int) -> bool:
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except FileNotFoundError:
+        return False
+
+
+@pytest.mark.parametrize("sig", [signal.SIGTERM, signal.SIGKILL])
+def test_launcher_stop_takes_ranks_down(tmp_path, sig):
+    """Stopping the self-launcher (SIGTERM: its handler runs the teardown; SIGKILL: the ranks'
+    parent-death signal) leaves no rank running."""
+    child = tmp_path / "child.py"
+    child.write_text("import os, sys, time\n"
+                     "open(os.path.join(sys.argv[1], 'pid' + os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                     "time.sleep(120)\n")
+    launcher = tmp_path / "launcher.py"
+    launcher.write_text(f"import sys\nsys.path.insert(0, {ROOT!r})\n"
+                        "from distributed_pytorch_amd.parallel import spawn\n"
+                        f"sys.exit(spawn.launch({str(child)!r}, [{str(tmp_path)!r}], 2, timeout_s=300))\n")
+    p = subprocess.Popen([sys.executable, str(launcher)], start_new_session=True)
+    try:
+        t_end = time.time() + 60
+        files = [tmp_path / "pid0", tmp_path / "pid1"]
+        while not all(f.exists() and f.read_text() for f in files):
+            assert time.time() < t_end and p.poll() is None, "ranks did not start"
+            time.sleep(0.1)
+        pids = [int(f.read_text()) for f in files]
+        assert all(_alive(q) for q in pids)
+        os.kill(p.pid, sig)
+        rc = p.wait(30)
+        if sig == signal.SIGTERM:
+            assert rc == 128 + signal.SIGTERM
+        t_end = time.time() + 30
+        while any(_alive(q) for q in pids):
+            assert time.time() < t_end, "a rank outlived its launcher"
+            time.sleep(0.1)
+    finally:
+        if p.poll() is None:
+            p.kill()
 
 
 def test_native_store_port_via_torchrun_agent_store(tmp_path):

@@ -1,6 +1,7 @@
-"""HIP kernels (BN/ReLU/pool, classifier head, SGD, augmentation) vs the plain-PyTorch fp32
-reference of the same op (distributed_pytorch_amd.ops.cpu_ref mirrors the native API), and one
-whole VGG-11 training step of the GPU engine vs stock torch autograd on model.VGG11."""
+"""HIP kernels (BN activation variants, classifier head, SGD, augmentation) vs the plain-PyTorch
+fp32 reference of the same op (distributed_pytorch_amd.ops.cpu_ref mirrors the native API), and one
+whole VGG-11 training step of the GPU engine vs stock torch autograd on model.VGG11.  The VGG
+BatchNorm+ReLU+max-pool kernels are checked against torch autograd in fp64 in test_bn_gpu.py."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -21,89 +22,6 @@ def close(a, b, tol):
     d = (a - b).abs().max().item()
     s = b.abs().max().clamp_min(1e-6).item()
     assert d <= tol * s, f"max abs diff {d} vs scale {s}"
-
-
-BN_SHAPES = [(4, 32, 32, 64, True), (4, 16, 16, 128, True), (8, 8, 8, 256, False), (16, 2, 2, 512, True),
-             (3, 6, 6, 16, False), (2, 4, 4, 1024 // 4, True)]
-
-
-@pytest.mark.parametrize("shape", BN_SHAPES)
-def test_bn_forward(shape):
-    C_ = _C()
-    N, H, W, C, pool = shape
-    g = torch.Generator().manual_seed(0)
-    z = torch.randn(N, H, W, C, generator=g) * 3 + 1.5
-    gamma, beta, bias = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g), torch.randn(C, generator=g)
-    rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
-    nbt = torch.zeros(1, dtype=torch.int64)
-    outs_ref = [torch.zeros(C) for _ in range(4)]
-    Ho = H // 2 if pool else H
-    a_ref = torch.empty(N, Ho, Ho if pool else W, C)
-    rm_r, rv_r = rm.clone(), rv.clone()
-    cpu_ref.bn_fwd_stats(z, 1, z, None, gamma, beta, bias, rm_r, rv_r, nbt, *outs_ref, 0.1, 1e-5)
-    cpu_ref.bn_apply(z, a_ref, outs_ref[2], outs_ref[3], pool)
-    d = lambda t: t.cuda()
-    # exercise the fused split-K path: z arrives as 3 slabs that sum to it
-    sl = torch.randn(3, *z.shape, generator=g)
-    sl[2] = z - sl[0] - sl[1]
-    zd = torch.empty(z.shape, device="cuda")
-    part = torch.zeros(C_.bn_part_floats(N * H * W, C, False), device="cuda")
-    outs = [torch.zeros(C, device="cuda") for _ in range(4)]
-    rm_d, rv_d, nbt_d = d(rm), d(rv), torch.zeros(1, dtype=torch.int64, device="cuda")
-    C_.bn_fwd_stats(d(sl.reshape(-1)), 3, zd, part, d(gamma), d(beta), d(bias), rm_d, rv_d, nbt_d, *outs, 0.1, 1e-5)
-    close(zd, z, 1e-5)
-    a = torch.empty(a_ref.shape, device="cuda")
-    C_.bn_apply(zd, a, outs[2], outs[3], pool)
-    torch.cuda.synchronize()
-    for o, r in zip(outs, outs_ref):
-        close(o, r, 1e-5)
-    close(rm_d, rm_r, 1e-5)
-    close(rv_d, rv_r, 1e-5)
-    assert int(nbt_d.item()) == 1
-    close(a, a_ref, 1e-5)
-
-
-@pytest.mark.parametrize("shape", BN_SHAPES)
-def test_bn_backward(shape):
-    C_ = _C()
-    N, H, W, C, pool = shape
-    g = torch.Generator().manual_seed(1)
-    z = torch.randn(N, H, W, C, generator=g) * 2 - 0.3
-    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.5
-    mean, invstd = z.reshape(-1, C).mean(0), torch.rsqrt(z.reshape(-1, C).var(0, unbiased=False) + 1e-5)
-    scale, shift = gamma * invstd, beta - mean * gamma * invstd
-    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
-    gout = torch.randn(N, Ho, Wo, C, generator=g)
-    ref = [torch.zeros(C) for _ in range(3)]
-    dz_ref = torch.empty_like(z)
-    cpu_ref.bn_bwd(gout, 1, gout, z, scale, shift, mean, invstd, gamma, None, None, ref[0], ref[1], ref[2], dz_ref,
-                   pool)
-    d = lambda t: t.cuda()
-    part = torch.zeros(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
-    coef = torch.empty(3 * C, device="cuda")
-    for nsplit in (1, 2):
-        out = [torch.zeros(C, device="cuda") for _ in range(3)]
-        dz = torch.empty(z.shape, device="cuda")
-        gbuf = torch.empty(gout.shape, device="cuda")
-        if nsplit == 1:
-            src = d(gout)
-            gbuf = src
-        else:
-            half = torch.randn(gout.shape, generator=g)
-            src = d(torch.stack([half, gout - half]).reshape(-1))
-        C_.bn_bwd(src, nsplit, gbuf, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, out[0],
-                  out[1], out[2], dz, pool)
-        torch.cuda.synchronize()
-        close(gbuf, gout, 1e-5)
-        close(dz, dz_ref, 2e-5)
-        close(out[0], ref[0], 2e-5)
-        close(out[1], ref[1], 2e-5)
-        assert out[2].abs().max().item() < 1e-3 * ref[0].abs().max().item() + 1e-4  # dbias ~ 0
-    return
-    close(dz, dz_ref, 2e-5)
-    close(out[0], ref[0], 2e-5)
-    close(out[1], ref[1], 2e-5)
-    assert out[2].abs().max().item() < 1e-3 * ref[0].abs().max().item() + 1e-4  # dbias ~ 0
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])

@@ -48,7 +48,7 @@ def test_resume_point_must_agree_across_ranks(tmp_path, case):
     _spawn(H.run_resume_agree, 2, ck, out, by_rank)
     res = [json.load(open(os.path.join(out, f"resume_{r}.json"))) for r in range(2)]
     if case == "agree":
-        assert res[0] == res[1] == {"ok": [0, 40]}
+        assert res[0]["ok"] == res[1]["ok"] == [0, 40]
     else:  # every rank refuses (none is left waiting in a collective the others never issue)
         assert all("error" in r and "disagree" in r["error"] for r in res), res
 
@@ -58,6 +58,25 @@ def test_resume_topology_change_fails_on_every_rank(tmp_path):
     _spawn(H.run_resume_agree, 2, ck, out, [40, 40], 4)
     res = [json.load(open(os.path.join(out, f"resume_{r}.json"))) for r in range(2)]
     assert all("error" in r and "world size 4 -> 2" in r["error"] for r in res), res
+
+
+def test_resume_reshard_onto_a_larger_world(tmp_path):
+    """2 -> 4 ranks with --resume-reshard: ranks 2 and 3 have no file of their own and load rank 0's;
+    every rank restarts the saved epoch at batch 0 with the same weights and step count."""
+    ck, out = str(tmp_path / "ck"), str(tmp_path)
+    _spawn(H.run_resume_agree, 4, ck, out, [40, 40], 2, True)
+    res = [json.load(open(os.path.join(out, f"resume_{r}.json"))) for r in range(4)]
+    assert all("ok" in r for r in res), res
+    assert all(r["ok"] == [0, 0] and r["steps_taken"] == 7 for r in res), res
+    assert len({r["param_sum"] for r in res}) == 1
+
+
+def test_agree_pieces_are_exact():
+    big = (1, 3, (1 << 40) + 1, (1 << 24) + 1)
+    assert checkpoint._unpieces(checkpoint._pieces(big)) == list(big)
+    assert checkpoint._unpieces(checkpoint._pieces((-1, -1, -1, -1))) == [-1, -1, -1, -1]
+    p1, p2 = checkpoint._pieces((1, 0, 0, 1 << 24)), checkpoint._pieces((1, 0, 0, (1 << 24) + 1))
+    assert torch.tensor(p1, dtype=torch.float32).tolist() != torch.tensor(p2, dtype=torch.float32).tolist()
 
 
 def _write_py_release(root, payload_train, payload_test):
