@@ -1,4 +1,4 @@
-"""Per-dispatch PMC table for one training step from rocprofv3 --pmc CSVs (scripts/pmc_conv.sh).
+"""Per-dispatch PMC table for one training step from rocprofv3 --pmc CSVs (scripts/gpu_profile.sh (PMC=1)).
 
     python tools/pmc_summary.py gpurun_out/pmcA/run_counter_collection.csv \
         [gpurun_out/pmcB/run_counter_collection.csv] [--step -1] [--marker sgd_flat]
