@@ -40,6 +40,10 @@ def main(argv=None):
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"])
     ap.add_argument("--autotune", action="store_true",
                     help="time every conv kernel config during warmup and save tuning/generic_mi355x.json")
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
+                    help="1 GPU: capture the whole training step (forward, backward through autograd, fused SGD) "
+                         "as one HIP graph after the warmup and replay it (removes the host/autograd gaps "
+                         "between kernels)")
     ap.add_argument("--profile", action="store_true", help="re-run under rocprofv3 --kernel-trace --stats")
     ap.add_argument("--profile-dir", default="gpurun_out/prof_resnet")
     ap.add_argument("--launch-timeout", type=float, default=1800.0)
@@ -81,6 +85,27 @@ def main(argv=None):
     def timed_step():
         last["loss"] = step()
 
+    graphed = False
+    if a.graph == "on" and ctx.world == 1 and dev.type == "cuda":
+        # torch.cuda.graph recipe: eager warmup on a side stream, then capture one whole step.  The
+        # replays run the identical kernels on the same static input / parameter / gradient
+        # buffers; only the Python host work (autograd graph walk, launches) disappears.
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(3, a.warmup)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = step()
+        graphed = True
+
+        def timed_step():
+            graph.replay()
+            last["loss"] = static_loss
+
     el = benchlib.timed_steps(timed_step, a.steps, a.warmup, ctx, dev)  # max over ranks
     loss = last["loss"]
     pdiff = benchlib.replicas_max_diff(ctx.comm, ddp.flat_params)
@@ -94,6 +119,7 @@ def main(argv=None):
             "data": "synthetic (ImageNet-shaped 224x224x3 on device, random labels)",
             "config": {"model": "resnet50", "global_batch": a.batch * ctx.world, "seq_len": None,
                        "image_size": a.image, "parallelism": f"dp{ctx.world}", "buckets": ddp.num_buckets(),
+                       "hip_graph": graphed,
                        "comm": ctx.comm.name, "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
             "rccl_world": benchlib.comm_world(ctx.comm), "replicas_identical": pdiff == 0.0,
             "final_loss": round(float(loss.item()), 4),

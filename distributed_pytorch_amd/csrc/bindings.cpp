@@ -41,6 +41,18 @@ int dpa_ce(const float* logits, const long long* target, float* loss_row, float*
 int dpa_head_bwd_prep(const float* dlogits, const float* gout, float* dl, float* db, int N, int J, hipStream_t st);
 int dpa_gap_bwd(const float* dfeat, void* dx, int N, int HW, int C, int xbf, hipStream_t st);
 long dpa_conv0_part_floats(int N);
+int dpa_gemm_f32(const float* A, int lda, int ak, const float* B, int ldb, int bk, float* C, int M, int N, int K,
+                 const float* bias, float* slab, int splits, hipStream_t st);
+int dpa_conv0_stats(const float* x, const float* w, int CP, float* part, int N, const float* gamma, const float* beta,
+                    const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
+                    float* scale, float* shift, float momentum, float eps, hipStream_t st);
+int dpa_conv0_bn_pool(const float* x, const float* w, int CP, const float* scale, const float* shift, float* a,
+                      unsigned short* a3, int np, long ps, int N, hipStream_t st);
+long dpa_bn_bwd_l0_part_floats(int N);
+int dpa_bn_bwd_l0(const float* gsrc, int nsplit, long slab, const float* x, const float* w, int CP,
+                  const float* scale, const float* shift, const float* mean, const float* invstd, const float* gamma,
+                  float* wpart, float* dgamma, float* dbeta, float* dbias, float* dw, int N, hipStream_t st, int* sig,
+                  int sig_val);
 int dpa_conv0_fwd(const float* x, const float* w, int CP, float* z, float* part, int N, const float* gamma,
                   const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
                   float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st);
@@ -561,6 +573,97 @@ void conv0_fwd(Tensor x, Tensor w, Tensor z, OptT part, OptT gamma, OptT beta, O
       "conv0_fwd");
 }
 
+// ---- layer 0 without a stored z (first_layer.hip): statistics pass, recomputing apply, one-pass
+// backward from (g, x) ----
+void conv0_check(const Tensor& x, const Tensor& w, const char* what) {
+  need(x, "x");
+  need(w, "w");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4, what, ": x [N,32,32,4]");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) >= 3,
+              what, ": w [64,3,3,CP]");
+}
+
+void conv0_stats(Tensor x, Tensor w, Tensor part, Tensor gamma, Tensor beta, OptT bias, OptT rmean, OptT rvar,
+                 OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum, double eps) {
+  conv0_check(x, w, "conv0_stats");
+  const int N = x.size(0);
+  need(part, "part");
+  TORCH_CHECK(part.numel() >= dpa_conv0_part_floats(N), "conv0_stats: part too small");
+  for (const Tensor* o : {&gamma, &beta, &mean, &invstd, &scale, &shift})
+    TORCH_CHECK(o->numel() == 64, "conv0_stats: channel vectors [64]");
+  long long* nb = nbt.has_value() && nbt->defined() ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr;
+  chk(dpa_conv0_stats(fp(x), fp(w), (int)w.size(3), fp(part), N, fp(gamma), fp(beta), ofp(bias), ofp(rmean),
+                      ofp(rvar), nb, fp(mean), fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps,
+                      cur_stream()),
+      "conv0_stats");
+}
+
+// out: fp32 [N,16,16,64] or bf16 planes [NP,N,16,16,64]
+void conv0_bn_pool(Tensor x, Tensor w, Tensor scale, Tensor shift, Tensor out) {
+  conv0_check(x, w, "conv0_bn_pool");
+  const int N = x.size(0);
+  const int64_t n = (int64_t)N * 16 * 16 * 64;
+  TORCH_CHECK(scale.numel() == 64 && shift.numel() == 64, "conv0_bn_pool: scale/shift [64]");
+  if (out.scalar_type() == at::kBFloat16) {
+    int np = 1;
+    if (out.numel() != n) {
+      need_planes(out, "out");
+      TORCH_CHECK(out.numel() == out.size(0) * n, "conv0_bn_pool: planes shape");
+      np = out.size(0);
+    }
+    chk(dpa_conv0_bn_pool(fp(x), fp(w), (int)w.size(3), fp(scale), fp(shift), nullptr, up(out), np, n, N,
+                          cur_stream()),
+        "conv0_bn_pool");
+  } else {
+    need(out, "out");
+    TORCH_CHECK(out.numel() == n, "conv0_bn_pool: out [N,16,16,64]");
+    chk(dpa_conv0_bn_pool(fp(x), fp(w), (int)w.size(3), fp(scale), fp(shift), fp(out), nullptr, 0, 0, N,
+                          cur_stream()),
+        "conv0_bn_pool");
+  }
+}
+
+void bn_bwd_l0(Tensor gsrc, int64_t nsplit, Tensor x, Tensor w, Tensor scale, Tensor shift, Tensor mean,
+               Tensor invstd, Tensor gamma, Tensor wpart, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dw, OptT sig,
+               int64_t sig_val) {
+  conv0_check(x, w, "bn_bwd_l0");
+  for (auto* t : {&gsrc, &scale, &shift, &mean, &invstd, &gamma, &wpart, &dgamma, &dbeta, &dw})
+    need(*t, "bn_bwd_l0 operand");
+  const int N = x.size(0);
+  const int64_t gn = (int64_t)N * 16 * 16 * 64;
+  TORCH_CHECK(gsrc.numel() >= nsplit * gn, "bn_bwd_l0: gsrc too small");
+  TORCH_CHECK(wpart.numel() >= dpa_bn_bwd_l0_part_floats(N), "bn_bwd_l0: wpart too small");
+  TORCH_CHECK(dw.numel() == 64 * 9 * w.size(3) && dw.size(-1) == w.size(3), "bn_bwd_l0: dw like w");
+  chk(dpa_bn_bwd_l0(fp(gsrc), (int)nsplit, gn, fp(x), fp(w), (int)w.size(3), fp(scale), fp(shift), fp(mean),
+                    fp(invstd), fp(gamma), fp(wpart), fp(dgamma), fp(dbeta), ofp(dbias), fp(dw), N, cur_stream(),
+                    opt_signal(sig, "bn_bwd_l0"), (int)sig_val),
+      "bn_bwd_l0");
+}
+
+// C = opA(A) @ opB(B) (+ bias), fp32 on the fp32 matrix cores (gemm_f32.hip).  opA(A) = A [M,K] or,
+// trans_a, A^T of A [K,M]; opB(B) = B [K,N] or, trans_b, B^T of B [N,K].  splits > 1: split-K
+// through slab (>= splits * M * N floats), fixed-order reduction.
+void gemm_f32(Tensor A, Tensor B, Tensor C, bool trans_a, bool trans_b, OptT bias, int64_t splits, OptT slab) {
+  need(A, "A");
+  need(B, "B");
+  need(C, "C");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_f32: 2-D operands");
+  const int M = trans_a ? A.size(1) : A.size(0), K = trans_a ? A.size(0) : A.size(1);
+  const int N = trans_b ? B.size(0) : B.size(1), KB = trans_b ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB && C.size(0) == M && C.size(1) == N, "gemm_f32: shapes");
+  float* sp = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined() && slab->numel() >= splits * (int64_t)M * N,
+                "gemm_f32: split-K needs a slab of splits * M * N floats");
+    need(*slab, "slab");
+    sp = fp(*slab);
+  }
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N, "gemm_f32: bias [N]");
+  chk(dpa_gemm_f32(fp(A), A.size(1), trans_a ? 0 : 1, fp(B), B.size(1), trans_b ? 1 : 0, fp(C), M, N, K, ofp(bias), sp,
+                   (int)splits, cur_stream()),
+      "gemm_f32");
+}
+
 // ---------------- generic classifier head (head.hip) ----------------
 // x [N,H,W,C] (bf16 or fp32) -> feat [N,C] fp32 (spatial mean)
 void gap(Tensor x, Tensor feat) {
@@ -1009,6 +1112,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("x"), py::arg("wpart"),
         py::arg("dw"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
   m.def("gap", &gap);
+  m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("trans_a") = false,
+        py::arg("trans_b") = false, py::arg("bias") = py::none(), py::arg("splits") = 1, py::arg("slab") = py::none());
   m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("target"), py::arg("loss_row"),
         py::arg("dlogits") = py::none(), py::arg("correct_row") = py::none(), py::arg("loss") = py::none(),
         py::arg("acc") = py::none());
@@ -1020,6 +1125,15 @@ PYBIND11_MODULE(_C, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("scale") = py::none(),
         py::arg("shift") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5);
   m.def("conv0_part_floats", [](int64_t N) { return dpa_conv0_part_floats((int)N); });
+  m.def("conv0_stats", &conv0_stats, py::arg("x"), py::arg("w"), py::arg("part"), py::arg("gamma"), py::arg("beta"),
+        py::arg("bias"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("mean"), py::arg("invstd"),
+        py::arg("scale"), py::arg("shift"), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5);
+  m.def("conv0_bn_pool", &conv0_bn_pool, py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
+        py::arg("out"));
+  m.def("bn_bwd_l0", &bn_bwd_l0, py::arg("gsrc"), py::arg("nsplit"), py::arg("x"), py::arg("w"), py::arg("scale"),
+        py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("wpart"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("dbias"), py::arg("dw"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
+  m.def("bn_bwd_l0_part_floats", [](int64_t N) { return dpa_bn_bwd_l0_part_floats((int)N); });
   m.def("wgrad0_part_floats", [](int64_t N) { return dpa_wgrad0_part_floats((int)N); });
   m.def("fc_ce_train", &fc_ce_train, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("loss_row"),
         py::arg("dlogits"), py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("loss_out"), py::arg("loss_accum"),

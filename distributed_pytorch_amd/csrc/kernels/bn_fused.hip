@@ -231,12 +231,26 @@ __global__ __launch_bounds__(FT) void bn_fused_fwd_kernel(FArgs a) {
     const float* ps0 = a.part + (long)slice * a.R * 2 * CS;
     float n = 0.f, mu = 0.f, M2 = 0.f;
     const float nb = (float)(RB * Q);
-    for (int k = grp; k < a.R; k += G) {
-      const float pm = ps0[(long)k * 2 * CS + ch], pq = ps0[(long)k * 2 * CS + CS + ch];
-      const float nn = n + nb, d = pm - mu, f = nb / nn;
-      mu += d * f;
-      M2 += pq + d * d * n * f;
-      n = nn;
+    // MB partials' loads in flight at once, then their merges (a dependent L2 round trip per
+    // partial would dominate the kernel)
+    constexpr int MB = 8;
+    for (int k0 = grp; k0 < a.R; k0 += MB * G) {
+      float pm[MB], pq[MB];
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        const int k = k0 + u * G;
+        pm[u] = k < a.R ? ps0[(long)k * 2 * CS + ch] : 0.f;
+        pq[u] = k < a.R ? ps0[(long)k * 2 * CS + CS + ch] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        if (k0 + u * G < a.R) {
+          const float nn = n + nb, d = pm[u] - mu, f = nb / nn;
+          mu += d * f;
+          M2 += pq[u] + d * d * n * f;
+          n = nn;
+        }
+      }
     }
     mrg[grp][ch] = make_float2(mu, M2);
     __syncthreads();
@@ -393,11 +407,24 @@ __global__ __launch_bounds__(FT) void bn_fused_bwd_kernel(FArgs a) {
     const int ch = t % CS, grp = t / CS;
     const float* ps0 = a.part + (long)slice * a.R * 3 * CS;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int k = grp; k < a.R; k += G) {
-      const float* p = ps0 + (long)k * 3 * CS + ch;
-      s0 += p[0];
-      s1 += p[CS];
-      s2 += p[2 * CS];
+    constexpr int MB = 8;
+    for (int k0 = grp; k0 < a.R; k0 += MB * G) {
+      float p0[MB], p1[MB], p2[MB];
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        const int k = k0 + u * G;
+        const float* p = ps0 + (long)k * 3 * CS + ch;
+        const bool ok = k < a.R;
+        p0[u] = ok ? p[0] : 0.f;
+        p1[u] = ok ? p[CS] : 0.f;
+        p2[u] = ok ? p[2 * CS] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        s0 += p0[u];
+        s1 += p1[u];
+        s2 += p2[u];
+      }
     }
     mrg[grp][0][ch] = s0;
     mrg[grp][1][ch] = s1;
@@ -450,20 +477,27 @@ struct Geo {
 
 // Largest tile per thread (U units) whose grid is <= rmax row blocks per slice; units of 4 pixels
 // (pool) hold 4x the registers, and the backward holds g too.
+// Row blocks per slice: as few as possible (every block merges all R partials of its slice, and
+// all R must be resident together) but at least RMIN while a smaller tile allows it (bandwidth
+// of the load / store phases); at most rmax.
+constexpr int RMIN = 16;
 bool pick_geo(int Mo, int C, bool pool, bool bwd, int rmax, Geo& g) {
   g.CL = (C % 64 == 0) ? 16 : (C % 32 == 0 ? 8 : 0);
   if (!g.CL) return false;
   g.slices = C / (4 * g.CL);
   const int RL = FT / g.CL;
   const int umax = pool ? (bwd ? UMAX_BWD_POOL : UMAX_FWD_POOL) : (bwd ? UMAX_BWD : UMAX_FWD);
+  bool found = false;
   for (int u = 1; u <= umax; u *= 2) {
     if (Mo % (RL * u)) break;
     const int R = Mo / (RL * u);
+    if (R > rmax) continue;
+    if (found && R < RMIN) break;
     g.U = u;
     g.R = R;
-    if (R <= rmax) return true;
+    found = true;
   }
-  return false;
+  return found;
 }
 
 template <int U, int CL>

@@ -1,7 +1,7 @@
 // Classifier head of the generic (ResNet) path: global average pool + Linear + softmax
-// cross-entropy (mean), forward and backward.  The two GEMMs (logits = feat @ W^T + b, and the
-// backward's dfeat / dW) are plain library GEMMs (hipBLASLt through torch.mm); everything around
-// them is here so no elementwise/reduction pass of the step runs outside the framework's kernels:
+// cross-entropy (mean), forward and backward.  The GEMMs (logits = feat @ W^T + b, and the
+// backward's dfeat / dW) run on gemm_f32.hip; everything around them is here, so no GEMM,
+// elementwise or reduction pass of the step runs outside the framework's kernels:
 //
 //   gap        feat[n][c] = mean_hw x[n][hw][c]            (x bf16 or fp32 NHWC, feat fp32)
 //   ce_rows    per row: log-sum-exp, loss_row, dlogits = (softmax - onehot(target)) / N

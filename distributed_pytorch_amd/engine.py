@@ -245,6 +245,14 @@ class VGGEngine:
                             and os.environ.get("DPA_FUSED_CONV0", "1") == "1"
                             and l0.hw == 32 and l0.cout == 64 and l0.cin <= 3)
         self.part0 = torch.empty(self.K.conv0_part_floats(N), **f32) if self.fused_conv0 else None
+        # Layer 0 without a stored z (DPA_L0_RECOMPUTE=1, needs both fused layer-0 paths): the
+        # 27-MAC conv is recomputed by each consumer instead of writing and re-reading 67 MB of z —
+        # a statistics pass, an apply pass writing the pooled planes (first_layer.hip
+        # conv0_bn_pool_kernel), and ONE backward pass over (g, x) that accumulates the BN sums and
+        # the coefficient-free parts of the weight gradient (bn_bwd_l0_kernel).
+        self.l0_recompute = (self.fused_conv0 and self.fused_wgrad0 and hasattr(self.K, "bn_bwd_l0")
+                             and os.environ.get("DPA_L0_RECOMPUTE", "1") == "1")
+        self.l0part = torch.empty(self.K.bn_bwd_l0_part_floats(N), **f32) if self.l0_recompute else None
         # Head: the last layer's BN + ReLU + 2x2 max-pool folded into the classifier kernel's row load
         # (fc_ce.hip BnIn: one launch less on the critical path); DPA_FUSED_HEAD=0 runs bn_apply
         lL = L[-1]
@@ -256,10 +264,12 @@ class VGGEngine:
         # geometry fits (<= DPA_BN_FUSED_RMAX row blocks per slice).  Counters self-reset; the
         # workspace is zeroed once here.
         self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", str(2200000))) if dev.type == "cuda" else 0
+        self.bn_fused_bwd_max = (int(os.environ.get("DPA_BN_FUSED_BWD_MAX", str(self.bn_fused_max)))
+                                 if dev.type == "cuda" else 0)
         self.bn_fused_rmax = int(os.environ.get("DPA_BN_FUSED_RMAX", "64"))
         self._fgeo: Dict[tuple, bool] = {}
         fpart, fcnt = 0, 0
-        if self.bn_fused_max > 0 and hasattr(self.K, "bn_fused_geo"):
+        if max(self.bn_fused_max, self.bn_fused_bwd_max) > 0 and hasattr(self.K, "bn_fused_geo"):
             for i, l in enumerate(L):
                 for bwd in (False, True):
                     gq = self._fused_geo(i, N, bwd)
@@ -404,10 +414,11 @@ class VGGEngine:
 
     def _fused_geo(self, i: int, n: int, bwd: bool):
         """(part_floats, cnt_words, blocks) when layer i's BN runs as one launch at batch n, else None."""
-        if self.bn_fused_max <= 0 or not hasattr(self.K, "bn_fused_geo"):
+        lim = self.bn_fused_bwd_max if bwd else self.bn_fused_max
+        if lim <= 0 or not hasattr(self.K, "bn_fused_geo"):
             return None
         l = self.spec.convs[i]
-        if i == 0 or n * l.hw * l.hw * l.cout > self.bn_fused_max:
+        if i == 0 or n * l.hw * l.hw * l.cout > lim:
             return None  # layer 0: conv0_fwd / bn_bwd_wgrad0 fuse its BN with the convolution instead
         ho = l.hw // 2 if l.pool else l.hw
         return self.K.bn_fused_geo(n * ho * ho, l.cout, l.pool, bwd, self.bn_fused_rmax)
@@ -627,6 +638,17 @@ class VGGEngine:
             K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(L):
             z, st = self.z[i][:n], self.stats[i]
+            if i == 0 and self.l0_recompute:
+                if buffers_wait is not None:
+                    buffers_wait()
+                    buffers_wait = None
+                w0 = P[f"{l.conv_key}.weight"]
+                K.conv0_stats(x, w0, self.part0, P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"],
+                              P[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
+                              self.buffers[f"{l.bn_key}.running_var"], self.nbt[i:i + 1], st["mean"], st["invstd"],
+                              st["scale"], st["shift"], self.bn_momentum, self.bn_eps)
+                K.conv0_bn_pool(x, w0, st["scale"], st["shift"], self._act_out(i, n))
+                continue
             if i == 0 and self.fused_conv0:
                 if buffers_wait is not None:
                     buffers_wait()
@@ -726,6 +748,18 @@ class VGGEngine:
             dzbuf = self.dz3[i][:, :n] if self.planes[i] else self.dz[i][:n]
             names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
             bsig = dict(sig=self.bsig[i:i + 1], sig_val=epoch) if epoch else {}
+            if i == 0 and self.l0_recompute:
+                K.bn_bwd_l0(self.slab if gsplit > 1 else g, gsplit, x, P[f"{l.conv_key}.weight"], st["scale"],
+                            st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"], self.l0part,
+                            G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"],
+                            G[f"{l.conv_key}.weight"], **bsig)
+                after_bn(i)
+                drain_side()
+                if grad_ready is not None:
+                    grad_ready(names)
+                if params_free is not None:
+                    params_free(names)
+                continue
             if i == 0 and self.fused_wgrad0:
                 K.bn_bwd_wgrad0(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                                 st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
@@ -848,6 +882,10 @@ class VGGEngine:
         if self.x0p is not None and not self.fused_conv0:
             self.K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(self.spec.convs):
+            if i == 0 and self.l0_recompute:
+                self.K.conv0_bn_pool(x, P[f"{l.conv_key}.weight"], self.eval_ss[0]["scale"], self.eval_ss[0]["shift"],
+                                     self._act_out(0, n))
+                continue
             if i == 0 and self.fused_conv0:
                 self.K.conv0_fwd(x, P[f"{l.conv_key}.weight"], self.z[0][:n])
             else:

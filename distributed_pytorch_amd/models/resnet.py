@@ -4,7 +4,7 @@
 ``ResNet`` is built from the NHWC kernel layers (ops/layers.py): every conv runs the gfx950
 implicit-GEMM kernels (bf16 MFMA, or x3 fp32-grade), every BatchNorm is fused with its ReLU /
 residual-add+ReLU, the stem max-pool is the native NHWC pool, and the head (global average pool +
-Linear + softmax-CE) is one autograd node over head.hip + two hipBLASLt GEMMs
+Linear + softmax-CE) is one autograd node over head.hip + gemm_f32.hip (fp32 matrix cores)
 (``model(x, target)`` returns the loss; ``model(x)`` the logits).
 Parameter / buffer names and shapes (state_dict) match torchvision's ``resnet50`` so checkpoints
 interchange.  ``ResNetRef`` is the same network from stock torch NCHW modules: the numerics

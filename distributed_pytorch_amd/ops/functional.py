@@ -567,14 +567,45 @@ def kaiming_uniform_krsc(K: int, R: int, S: int, C: int, c_true: Optional[int] =
 
 
 # ------------------------------------------------------------------ classifier head
+def _gemm_splits(M: int, N: int, K: int) -> int:
+    """Split-K count for gemm_f32.hip's 64x64 tiles: ~256 blocks, K chunks of at least 128."""
+    tiles = -(-M // 64) * -(-N // 64)
+    s = 1
+    while tiles * s * 2 <= 256 and K // (s * 2) >= 128:
+        s *= 2
+    return s
+
+
+_GEMM_SLAB = {}
+
+
+def gemm_f32(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+             bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = op(a) @ op(b) (+ bias) in exact fp32 on the matrix cores (gemm_f32.hip); op = transpose
+    when the flag is set.  Split-K workspace cached per device."""
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    s = _gemm_splits(M, N, K) if (M * N) % 4 == 0 else 1
+    slab = None
+    if s > 1:
+        slab = _GEMM_SLAB.get(a.device)
+        if slab is None or slab.numel() < s * M * N:
+            slab = _GEMM_SLAB[a.device] = torch.empty(s * M * N, device=a.device, dtype=torch.float32)
+    _ext.require().gemm_f32(a, b, out, trans_a, trans_b, bias, s, slab)
+    return out
+
+
 def _head_fwd(x, weight, bias):
-    """feat = GAP(x) fp32 [N,C] (head.hip), logits = feat @ W^T + b (hipBLASLt)."""
-    if not _native(x):
+    """feat = GAP(x) fp32 [N,C] (head.hip), logits = feat @ W^T + b (gemm_f32.hip)."""
+    if not _native(x):  # CPU oracle path
         feat = x.to(weight.dtype).mean(dim=(1, 2))
-    else:
-        feat = torch.empty(x.shape[0], x.shape[-1], device=x.device, dtype=torch.float32)
-        _ext.require().gap(x, feat)
-    return feat, torch.addmm(bias, feat, weight.t())
+        return feat, torch.addmm(bias, feat, weight.t())
+    feat = torch.empty(x.shape[0], x.shape[-1], device=x.device, dtype=torch.float32)
+    _ext.require().gap(x, feat)
+    return feat, gemm_f32(feat, weight, trans_b=True, bias=bias)
 
 
 def _head_bwd(dlogits, gscale, feat, weight, wparam, bparam, shape, dtype):
@@ -599,18 +630,19 @@ def _head_bwd(dlogits, gscale, feat, weight, wparam, bparam, shape, dtype):
     if db is None:
         db = torch.empty(weight.shape[0], device=dev, dtype=torch.float32)
     K.head_bwd_prep(dlogits, gscale, dl, db)  # dl = dlogits * g, db = column sums (fixed order)
-    dfeat = torch.mm(dl, weight)
+    dfeat = gemm_f32(dl, weight)
     dw = grad_slot(wparam)
     if dw is None:
         dw = torch.empty_like(weight)
-    torch.mm(dl.t(), feat, out=dw)
+    gemm_f32(dl, feat, trans_a=True, out=dw)
     dx = torch.empty(shape, device=dev, dtype=dtype)
     K.gap_bwd(dfeat, dx)
     return dx, dw, db
 
 
 class HeadLinear(torch.autograd.Function):
-    """logits = Linear(GAP(x)): global average pool (head.hip) + hipBLASLt GEMM, one autograd node."""
+    """logits = Linear(GAP(x)): global average pool (head.hip) + fp32 MFMA GEMM (gemm_f32.hip), one
+    autograd node."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -631,7 +663,7 @@ class HeadLinear(torch.autograd.Function):
 
 class HeadCE(torch.autograd.Function):
     """Global average pool + Linear + softmax cross-entropy (mean) in one autograd node
-    (csrc/kernels/head.hip; the two GEMMs are plain hipBLASLt GEMMs through torch.mm).  The loss
+    (csrc/kernels/head.hip; the three GEMMs on the fp32 matrix cores, gemm_f32.hip).  The loss
     gradient is formed in the forward (as the VGG head does, fc_ce.hip); the backward scales it by
     the incoming gradient, reduces the bias gradient, and writes weight / bias gradients straight
     into the optimizer arena when the DDP wrapper offers a slot (``grad_slot``)."""

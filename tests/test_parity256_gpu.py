@@ -10,9 +10,11 @@ the same weights and data (reference: main.py:32-36, model.py:11-46):
   random operands, vs fp64 conv: rel ≤ 1e-5 (a wrong tile, split or reduction shows up as O(1));
 * the loss, all 34 parameter gradients and the 34 parameter updates of the whole step.  A
   random-init VGG-11 with BN at batch 256 is ill-conditioned (stock torch fp32 on CPU is off from
-  fp64 by up to ~3e-2 on single gradient tensors, measured), so the yardstick is torch's own fp32
-  error on the same step: x3 and the fp32 MFMA path must stay within a small factor of it on
-  every tensor, and on the median tensor be no worse than it;
+  fp64 by up to ~3e-2 on single gradient tensors, measured): a perturbation at fp32 rounding level
+  flips some 2x2 max-pool / ReLU decisions and moves single gradient tensors by 1e-3..1e-2.  The
+  yardstick is that floor, measured per tensor (torch fp32 and two fp64 runs perturbed by 2^-24):
+  x3 and the fp32 MFMA path must stay within 4x of it on every tensor, and on the median tensor
+  be no worse than torch fp32;
 * the layer-0 weight gradient, whose reduction runs over all 256·32·32 = 262,144 output pixels
   (the longest sum in the step), at the tuned x3 config vs fp32 MFMA vs fp64.
 """
@@ -50,6 +52,22 @@ def reference():
     opt.step()
     new = {n: p.detach().clone() for n, p in m.named_parameters()}
     return dict(sd0=sd0, x=x, t=t, loss=float(loss), grads=grads, new=new)
+
+
+def _fp64_perturbed_errors(ref, seed):
+    """The step's own conditioning: fp64 autograd on inputs and weights perturbed by random
+    relative noise of 2^-24 (one fp32 rounding), vs the unperturbed fp64 step.  A random-init
+    VGG-11 with BN amplifies such noise by orders of magnitude on some tensors (a 2x2 max-pool or
+    ReLU decision flips under it), so a per-tensor error is only meaningful against this floor."""
+    from distributed_pytorch_amd.models import VGG11
+
+    g = torch.Generator().manual_seed(seed)
+    pert = lambda t: t * (1 + 2.0 ** -24 * (2 * torch.rand(t.shape, generator=g, dtype=torch.float64) - 1))
+    m = VGG11().double()
+    m.load_state_dict({k: pert(v) if v.is_floating_point() else v for k, v in ref["sd0"].items()})
+    F.cross_entropy(m(pert(ref["x"])), ref["t"]).backward()
+    return {n: (_rel(p.grad, ref["grads"][n]) if ref["grads"][n].abs().max() >= 1e-7 else None)
+            for n, p in m.named_parameters()}
 
 
 def _torch_fp32_errors(ref):
@@ -108,6 +126,10 @@ def errors(reference):
             ue[n] = [err, allow]
         out[impl] = dict(loss=abs(loss - reference["loss"]) / abs(reference["loss"]), grads=ge, updates=ue)
     out["torch_fp32"] = dict(grads=_torch_fp32_errors(reference))
+    out["fp64_perturbed"] = [dict(grads=_fp64_perturbed_errors(reference, sd)) for sd in (1, 2)]
+    # per tensor: the largest error any reference-grade computation of this step shows
+    out["floor"] = {n: (None if e is None else max([e] + [p["grads"][n] for p in out["fp64_perturbed"]]))
+                    for n, e in out["torch_fp32"]["grads"].items()}
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/parity256_errors.json", "w") as f:
         json.dump(out, f, indent=1)
@@ -121,13 +143,16 @@ def test_loss_matches_fp64(errors, impl):
 
 @pytest.mark.parametrize("impl", ["fp32", "x3"])
 def test_all_gradients_fp32_grade(errors, impl):
-    ref = errors["torch_fp32"]["grads"]
+    """Every gradient tensor within 4x of the step's error floor (the largest error among torch
+    fp32 and two fp64 runs perturbed at fp32 rounding level), and the median tensor no worse than
+    torch fp32 itself."""
+    floor, tref = errors["floor"], errors["torch_fp32"]["grads"]
     ratios = []
     for n, e in errors[impl]["grads"].items():
         if e is None:
             continue
-        assert e <= 16.0 * ref[n] + 1e-5, (n, e, ref[n])
-        ratios.append(e / max(ref[n], 1e-12))
+        assert e <= 4.0 * floor[n] + 1e-5, (n, e, floor[n])
+        ratios.append(e / max(tref[n], 1e-12))
     ratios.sort()
     assert ratios[len(ratios) // 2] <= 1.5, ratios
 
@@ -142,43 +167,59 @@ def test_all_updates_match_fp64(errors, impl):
 CALLS = [(i, k) for i in range(8) for k in ("fprop", "dgrad", "wgrad") if not (i == 0 and k == "dgrad")]
 
 
-@pytest.fixture(scope="module")
-def x3_engine():
+_ENGINES = {}
+
+
+def _bench_engine(impl):
     from distributed_pytorch_amd.engine import VGGEngine
 
-    e = VGGEngine("VGG11", "cuda", max_batch=N, impl="x3")
-    e.init_parameters(seed=1)
-    return e
+    if impl not in _ENGINES:
+        e = VGGEngine("VGG11", "cuda", max_batch=N, impl=impl)
+        e.init_parameters(seed=1)
+        _ENGINES[impl] = e
+    return _ENGINES[impl]
 
 
+@pytest.mark.parametrize("impl", ["x3", "fp32"])
 @pytest.mark.parametrize("layer,kind", CALLS)
-def test_conv_call_at_bench_config(x3_engine, layer, kind):
+def test_conv_call_at_bench_config(impl, layer, kind):
     """One conv call of the step exactly as the engine issues it (tuned tile/splits, its own
-    workspaces and plane buffers) on random operands vs fp64."""
+    workspaces and operand buffers) on random operands vs fp64.  Both the x3 planes path and the
+    exact-fp32 MFMA path: each call's error is at fp32 rounding level (<= 1e-5 of the output's
+    scale), so the per-tensor spread of whole-step gradient errors (test_all_gradients_fp32_grade)
+    comes from the step's conditioning, not from any one reduction."""
     from distributed_pytorch_amd import _ext
 
     C = _ext.require()
-    e = x3_engine
+    e = _bench_engine(impl)
     l = e.spec.convs[layer]
     g = torch.Generator().manual_seed(100 * layer + len(kind))
     cin = l.cin
     act = torch.randn(N, l.hw, l.hw, cin, generator=g)
     w = e._to_torch_layout(f"{l.conv_key}.weight", e.params[f"{l.conv_key}.weight"]).cpu().double()  # OIHW
+    x4 = None
     if layer == 0:
         x4 = torch.zeros(N, 32, 32, 4)
         x4[..., :3] = act
-        C.pad_split8(x4.cuda(), e.x0p)
-    else:
+        x4 = x4.cuda()
+        if e.x0p is not None:
+            C.pad_split8(x4, e.x0p)
+    elif e.planes[layer]:
         C.split_planes(act.cuda().contiguous().view(-1), e.a3[layer - 1].view(3, -1))
+    else:
+        e.a[layer - 1].copy_(act.cuda())
     xd = act.permute(0, 3, 1, 2).double()
     torch.cuda.synchronize()
     if kind == "fprop":
-        e._conv_fwd(layer, None, N, reduce=True)
+        e._conv_fwd(layer, x4, N, reduce=True)
         out = e.z[layer].cpu().permute(0, 3, 1, 2).double()
         ref = F.conv2d(xd, w, padding=1)
     else:
         dz = torch.randn(N, l.hw, l.hw, l.cout, generator=g)
-        C.split_planes(dz.cuda().view(-1), e.dz3[layer].view(3, -1))
+        if e.planes[layer]:
+            C.split_planes(dz.cuda().view(-1), e.dz3[layer].view(3, -1))
+        else:
+            e.dz[layer].copy_(dz.cuda())
         dzd = dz.permute(0, 3, 1, 2).double()
         if kind == "dgrad":
             s = e._conv_dgrad(layer, N)
@@ -190,7 +231,7 @@ def test_conv_call_at_bench_config(x3_engine, layer, kind):
             out = out.permute(0, 3, 1, 2)
             ref = torch.nn.grad.conv2d_input(xd.shape, w, dzd, padding=1)
         else:
-            e._conv_wgrad(layer, None, N)
+            e._conv_wgrad(layer, x4, N)
             out = e._to_torch_layout(f"{l.conv_key}.weight", e.grads[f"{l.conv_key}.weight"]).cpu().double()
             ref = torch.nn.grad.conv2d_weight(xd, w.shape, dzd, padding=1)
     torch.cuda.synchronize()
