@@ -63,7 +63,7 @@ int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, c
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st, const float* bn_z, const float* bn_scale,
-                    const float* bn_shift);
+                    const float* bn_shift, int parts);
 int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                    int* correct_row, float* logits, float* acc, int B, int Cin, int J, hipStream_t st);
 int dpa_x3_splits(int Kred, int splits);
@@ -866,7 +866,8 @@ void bn_fused_bwd(Tensor gsrc, int64_t nsplit, Tensor z, bool pool, int64_t rmax
 // bn_z [B,2,2,Cin] fp32 + bn_scale/bn_shift [Cin] (optional): the features x [B,Cin] are computed
 // from the last conv's output (BN + ReLU + 2x2 max-pool) inside the head kernel and written to x
 void fc_ce_train(Tensor x, Tensor w, Tensor b, Tensor target, Tensor loss_row, Tensor dlogits, Tensor dx, Tensor dw,
-                 Tensor db, Tensor loss_out, OptT loss_accum, OptT bn_z, OptT bn_scale, OptT bn_shift) {
+                 Tensor db, Tensor loss_out, OptT loss_accum, OptT bn_z, OptT bn_scale, OptT bn_shift, int64_t parts) {
+  TORCH_CHECK(parts >= 1 && parts <= 3, "fc_ce_train: parts must be 1 (rows), 2 (weight gradient) or 3 (both)");
   need(x, "x");
   need(target, "target", at::kLong);
   const int B = x.size(0), Cin = x.size(1), J = w.size(0);
@@ -884,7 +885,7 @@ void fc_ce_train(Tensor x, Tensor w, Tensor b, Tensor target, Tensor loss_row, T
   }
   chk(dpa_fc_ce_train(fp(x), fp(w), fp(b), reinterpret_cast<const long long*>(target.data_ptr<int64_t>()),
                       fp(loss_row), fp(dlogits), fp(dx), fp(dw), fp(db), fp(loss_out), ofp(loss_accum), B, Cin, J,
-                      cur_stream(), zp, zp ? fp(*bn_scale) : nullptr, zp ? fp(*bn_shift) : nullptr),
+                      cur_stream(), zp, zp ? fp(*bn_scale) : nullptr, zp ? fp(*bn_shift) : nullptr, (int)parts),
       "fc_ce_train");
 }
 
@@ -1137,7 +1138,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("wgrad0_part_floats", [](int64_t N) { return dpa_wgrad0_part_floats((int)N); });
   m.def("fc_ce_train", &fc_ce_train, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("loss_row"),
         py::arg("dlogits"), py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("loss_out"), py::arg("loss_accum"),
-        py::arg("bn_z") = py::none(), py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none());
+        py::arg("bn_z") = py::none(), py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none(),
+        py::arg("parts") = 3);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -252,28 +252,35 @@ extern "C" {
 
 // bn_z / bn_scale / bn_shift (optional, VGG head): x is then OUTPUT -- the features are computed from
 // the last conv layer's z [B][2][2][Cin] (BN + ReLU + 2x2 max-pool, see BnIn) and stored there.
+// parts: bit 0 = the row kernel (loss rows, dlogits, dx), bit 1 = the weight-gradient kernel (dW, db,
+// batch loss).  The VGG engine issues the row kernel on the critical path and the weight gradient on
+// its weight-gradient stream (nothing on the critical path reads dW, db or the loss).
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
-                    int Cin, int J, hipStream_t st, const float* bn_z, const float* bn_scale, const float* bn_shift) {
+                    int Cin, int J, hipStream_t st, const float* bn_z, const float* bn_scale, const float* bn_shift,
+                    int parts) {
   if (J > GEN_J || Cin > 64 * GEN_CL || Cin % 4 || (long)B * J * 4 > 48 * 1024) return -2;
+  const bool rows = parts & 1, wg = parts & 2;
   if (bn_z) {
     if (!bn_scale || !bn_shift || J > 10 || Cin > 512) return -2;
-    fc_ce_rows_kernel<true, 10, 8, true><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(
-        x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin, J, BnIn{bn_z, bn_scale, bn_shift});
-    fc_ce_wgrad_kernel<10><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
-                                                                     loss_accum, B, Cin, J);
-    return (int)hipGetLastError();
-  }
-  if (J <= 10 && Cin <= 512) {
-    fc_ce_rows_kernel<true, 10, 8><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits, dx,
-                                                                          nullptr, nullptr, B, Cin, J);
-    fc_ce_wgrad_kernel<10><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
-                                                                     loss_accum, B, Cin, J);
-  } else {
+    if (rows)
+      fc_ce_rows_kernel<true, 10, 8, true><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(
+          x, w, b, target, loss_row, dlogits, dx, nullptr, nullptr, B, Cin, J, BnIn{bn_z, bn_scale, bn_shift});
+  } else if (J <= 10 && Cin <= 512) {
+    if (rows)
+      fc_ce_rows_kernel<true, 10, 8><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits, dx,
+                                                                            nullptr, nullptr, B, Cin, J);
+  } else if (rows) {
     fc_ce_rows_kernel<true, GEN_J, GEN_CL><<<cdiv(B, 4), 256, J * Cin * 4, st>>>(x, w, b, target, loss_row, dlogits,
                                                                                 dx, nullptr, nullptr, B, Cin, J);
-    fc_ce_wgrad_kernel<GEN_J><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
-                                                                        loss_accum, B, Cin, J);
+  }
+  if (wg) {
+    if (J <= 10)
+      fc_ce_wgrad_kernel<10><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
+                                                                       loss_accum, B, Cin, J);
+    else
+      fc_ce_wgrad_kernel<GEN_J><<<cdiv(Cin, 8) + 1, 256, B * J * 4, st>>>(x, dlogits, loss_row, dw, db, loss_out,
+                                                                          loss_accum, B, Cin, J);
   }
   return (int)hipGetLastError();
 }

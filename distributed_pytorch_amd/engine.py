@@ -224,6 +224,7 @@ class VGGEngine:
         self.ksig_timeout_us = max(int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "0")), comm_us + 60_000_000)
         # params_free hands the sync a later kernel's signal instead of recording an event (A/B: 0)
         self.free_signal = os.environ.get("DPA_FREE_SIGNAL", "1") == "1"
+        self.head_side = self.ksignal and os.environ.get("DPA_HEAD_SIDE", "1") == "1"
         self.slab = torch.empty(1, **f32)
         self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
         for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
@@ -250,8 +251,11 @@ class VGGEngine:
         # a statistics pass, an apply pass writing the pooled planes (first_layer.hip
         # conv0_bn_pool_kernel), and ONE backward pass over (g, x) that accumulates the BN sums and
         # the coefficient-free parts of the weight gradient (bn_bwd_l0_kernel).
+        # Off by default: the recompute trades 67 MB of z traffic for VALU work, and measured slower
+        # (forward 43 vs 45 us, backward 112 vs 82 us beside the weight-gradient stream; 173.5k-174.3k
+        # vs 176.5k-177.0k img/s, docs/PERF_NOTES.md).  Kept as an option and tested.
         self.l0_recompute = (self.fused_conv0 and self.fused_wgrad0 and hasattr(self.K, "bn_bwd_l0")
-                             and os.environ.get("DPA_L0_RECOMPUTE", "1") == "1")
+                             and os.environ.get("DPA_L0_RECOMPUTE", "0") == "1")
         self.l0part = torch.empty(self.K.bn_bwd_l0_part_floats(N), **f32) if self.l0_recompute else None
         # Head: the last layer's BN + ReLU + 2x2 max-pool folded into the classifier kernel's row load
         # (fc_ce.hip BnIn: one launch less on the critical path); DPA_FUSED_HEAD=0 runs bn_apply
@@ -263,8 +267,11 @@ class VGGEngine:
         # channel slice.  Used where z has at most DPA_BN_FUSED_MAX elements (0: never) and the tile
         # geometry fits (<= DPA_BN_FUSED_RMAX row blocks per slice).  Counters self-reset; the
         # workspace is zeroed once here.
-        self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", str(2200000))) if dev.type == "cuda" else 0
-        self.bn_fused_bwd_max = (int(os.environ.get("DPA_BN_FUSED_BWD_MAX", str(self.bn_fused_max)))
+        # Defaults from same-box A/B (docs/PERF_NOTES.md, round 3): forward for z <= 2.2M elements
+        # (layers 4-7 at batch 256), backward only for the 2x2 layers (<= 0.6M; beside the weight-
+        # gradient convs the 4x4 layers' rendezvous waits for CUs and loses to the three kernels).
+        self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", "2200000")) if dev.type == "cuda" else 0
+        self.bn_fused_bwd_max = (int(os.environ.get("DPA_BN_FUSED_BWD_MAX", "600000"))
                                  if dev.type == "cuda" else 0)
         self.bn_fused_rmax = int(os.environ.get("DPA_BN_FUSED_RMAX", "64"))
         self._fgeo: Dict[tuple, bool] = {}
@@ -683,9 +690,14 @@ class VGGEngine:
         feat = self.a[-1][:n].view(n, -1)
         bn_in = (dict(bn_z=self.z[-1][:n], bn_scale=self.stats[-1]["scale"], bn_shift=self.stats[-1]["shift"])
                  if self.fused_head else {})
-        K.fc_ce_train(feat, P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n], self.dlogits[:n],
-                      self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum, **bn_in)
-        if grad_ready is not None:
+        # the head's weight gradient / batch loss kernel goes to the wgrad stream (nothing on the critical
+        # path reads them); it waits for the first BN backward's start signal, which implies the row
+        # kernel (features, dlogits) has completed.  DPA_HEAD_SIDE=0 keeps both on the main stream.
+        head_side = bool(epoch) and self.wstream is not None and self.head_side
+        head_args = (feat, P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n], self.dlogits[:n],
+                     self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
+        K.fc_ce_train(*head_args, **bn_in, **({"parts": 1} if head_side else {}))
+        if grad_ready is not None and not head_side:
             grad_ready(["fc1.weight", "fc1.bias"])
         # Kernel-start signals (epoch > 0, signal.hip): each BN backward raises bsig[i] when it starts,
         # so every main-stream kernel enqueued before it (the data-gradient conv of layer i+1, the
@@ -732,7 +744,14 @@ class VGGEngine:
             joined = True
 
         def after_bn(i: int):
-            nonlocal free_later, side_later
+            nonlocal free_later, side_later, head_side
+            if head_side:  # first BN backward enqueued: its start signal orders the head's weight gradient
+                with torch.cuda.stream(ws):
+                    K.wait_signal(self.bsig[i:i + 1], epoch, self.ksig_timeout_us, self.ksig_tmo)
+                    K.fc_ce_train(*head_args, parts=2)
+                    if grad_ready is not None:
+                        grad_ready(["fc1.weight", "fc1.bias"])
+                head_side = False
             for nm in free_later:
                 params_free(nm, signal=(self.bsig[i:i + 1], epoch))
             free_later = []

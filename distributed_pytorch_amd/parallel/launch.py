@@ -77,6 +77,11 @@ def _timeout():
 
 
 def pick_device(local_rank: int, want: str = "auto") -> torch.device:
+    # RCCL and CUDA-tensor sharing across processes need the dmabuf IPC path on this platform
+    # (legacy IPC fails with hipIpcGetMemHandle: invalid argument).  spawn.py sets it for its ranks;
+    # under torchrun or a hand launch it must be in the environment before the HIP runtime starts,
+    # i.e. before the first torch.cuda query below.
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if want == "cpu" or (want == "auto" and not torch.cuda.is_available()):
         return torch.device("cpu")
     n = torch.cuda.device_count()

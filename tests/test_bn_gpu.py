@@ -66,6 +66,12 @@ def _inputs(shape, seed):
     rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
     Ho, Wo = (H // 2, W // 2) if pool else (H, W)
     gout = torch.randn(N, Ho, Wo, C, generator=g)
+    if pool:  # exact ties at a window's positive maximum: no gradient (torch's tie routing is machine-dependent)
+        zz4 = z.double()
+        y = torch.relu((zz4 - zz.mean(0)) * torch.rsqrt(zz.var(0, unbiased=False) + EPS) * gamma.double() + beta.double())
+        win = y.reshape(N, Ho, 2, Wo, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(N, Ho, Wo, C, 4)
+        top = win.sort(-1, descending=True).values
+        gout[(top[..., 0] == top[..., 1]) & (top[..., 0] > 0)] = 0.0
     return g, z, gamma, beta, bias, rm, rv, gout
 
 
