@@ -324,7 +324,7 @@ void* conv_out_ptr(const Tensor& out, int np, const char* name, int& obf) {
 
 // x3 [NP,N,H,W,C], w3 [NP,K,R,S,C], out [N,P,Q,K] fp32 (or bf16 when NP == 1)
 void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, bool posmajor) {
+                   int64_t tile, bool reduce, int64_t posmajor) {
   need_planes(x3, "x3");
   need_planes(w3, "w3");
   const int np = x3.size(0);
@@ -345,13 +345,13 @@ void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, 
     sl = fp(*slab);
   }
   chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), op, sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf, cur_stream()),
+                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf, cur_stream()),
       "conv_x3_fprop");
 }
 
 // x3 [NP,N,H,W,C], dz3 [NP,N,P,Q,K], dw [K,R,S,C] fp32
 void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool posmajor) {
+                   int64_t tile, int64_t posmajor) {
   need_planes(x3, "x3");
   need_planes(dz3, "dz3");
   need(dw, "dw");
@@ -371,14 +371,14 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
     sl = fp(*slab);
   }
   chk(dpa_conv_x3_wgrad(up(x3), x3.stride(0), up(dz3), dz3.stride(0), fp(dw), sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, posmajor ? 1 : 0, np, cur_stream()),
+                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream()),
       "conv_x3_wgrad");
 }
 
 // dz3 [NP,N,Hd,Wd,K], w3 [NP,K,R,S,C] (forward weight planes), dx [N,H,W,C] fp32: data gradient of
 // conv(x, w, stride, pad); stride a power of two.
 void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, bool posmajor, OptT add, OptT sig, int64_t sig_val) {
+                   int64_t tile, bool reduce, int64_t posmajor, OptT add, OptT sig, int64_t sig_val) {
   need_planes(dz3, "dz3");
   need_planes(w3, "w3");
   const int np = dz3.size(0);
@@ -409,7 +409,7 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
   }
   int* sp = opt_signal(sig, "conv_x3_dgrad");
   chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), op, sl, N, Hd, Wd, K, C, R, S, (int)stride,
-                        (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, posmajor ? 1 : 0, np, obf,
+                        (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf,
                         cur_stream(), ap, sp, (int)sig_val),
       "conv_x3_dgrad");
 }
@@ -1076,12 +1076,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("x3_splits", &x3_splits);
   m.def("conv_x3_fprop", &conv_x3_fprop, py::arg("x3"), py::arg("w3"), py::arg("out"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
-        py::arg("posmajor") = false);
+        py::arg("posmajor") = 0);
   m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
-        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0);
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
-        py::arg("posmajor") = false, py::arg("add") = py::none(), py::arg("sig") = py::none(),
+        py::arg("posmajor") = 0, py::arg("add") = py::none(), py::arg("sig") = py::none(),
         py::arg("sig_val") = 0);
   m.def("wait_signal", &wait_signal, py::arg("sig"), py::arg("val"), py::arg("timeout_us"), py::arg("tmo"));
   m.def("set_signal", &set_signal, py::arg("sig"), py::arg("val"));

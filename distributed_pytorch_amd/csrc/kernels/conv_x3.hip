@@ -27,6 +27,8 @@
 // waves of 64x32.  Each thread stages one 16-byte chunk per plane per operand per k step.
 #include "common.h"
 
+#include <algorithm>
+
 extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);  // sgd.hip
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -74,6 +76,8 @@ struct Args {
   int N, H, W, C, P, Q, R, S, stride, pad;
   int M, Nout, Ktot;
   int gm, gn, splits, posmajor;
+  int nmajor;         // block -> tile order: 0 = row tiles outer (an XCD's consecutive tiles share a
+                      // row tile), 1 = column tiles outer (they share a column tile: the weight slice)
   int imask, ishift;  // input dilation (DGRAD of a strided conv): 2^ishift, imask = 2^ishift - 1
   FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
   int* sig;  // optional kernel-start stream signal (common.h start_signal)
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
 
   const int nwg = a.gm * a.gn;
   const int tile = xcd_remap(blockIdx.x, nwg);
-  const int bm = tile / a.gn, bn = tile % a.gn;
+  const int bm = a.nmajor ? tile % a.gm : tile / a.gn, bn = a.nmajor ? tile / a.gm : tile % a.gn;
   const int m0 = bm * BM, n0 = bn * BN;
   const int split = blockIdx.y;
 
@@ -1004,6 +1008,298 @@ __global__ __launch_bounds__(256) void conv_halo_wgrad_kernel(WHArgs a) {
   }
 }
 
+// ---------------- position-major direct 3x3 convolution for small images (H*W <= 16) ----------------
+// The 4x4 and 2x2 layers (VGG-11 on 32x32 input) have 25-56 % of their 3x3 taps in the zero padding:
+// a corner output of a 2x2 image sees 4 of its 9 taps.  conv_halo_kernel's rows are NHWC pixels, so
+// a 32-row MFMA sub-tile mixes positions and every tap runs (padding taps read the zero slot), and
+// conv_x3_kernel skips padding taps only by re-gathering its A operand per tap.  Here a block owns
+// NI images x PPT output positions with the rows POSITION-MAJOR (row = position slot * NI + image):
+// every 32-row sub-tile is 32 images at ONE output position, so a tap is either entirely inside the
+// image for that sub-tile or entirely padding, and padding taps are skipped outright (no MFMAs, no
+// fragment reads).  Per chunk of BC reduction channels the block stages the input pixels its
+// positions can reach -- rows y0-1 .. y1+1 of its NI images, slot = pixel * NI + image -- ONCE into
+// LDS; the 9 per-tap weight tiles stream through a double-buffered LDS stage with PD tiles in flight
+// in registers, with conv_halo_kernel's B layouts and (chunk, tap, k-step, plane product) order
+// per accumulator, so the fp32 results are bit-identical to conv_halo_kernel with the same channel
+// chunk and split count: a skipped tap only ever added exact zeros there.  `perm` orders a tile's
+// positions so that the row waves carry near-equal numbers of in-image taps.  (A variant holding
+// the chunk's nine weight tiles in LDS at once, with no per-tap barrier, measured slower: its
+// 80-150 KB chunk loads left the prologue and the per-CU load rate exposed, docs/PERF_NOTES.md.)
+//   FPROP  out[p][n] = sum_{tap,c} x[p + d(tap)][c] * W[n][tap][c]
+//   DGRAD  dx[p][c]  = sum_{tap,k} dz[p + d(tap)][k] * W[k][8 - tap][c]
+struct PArgs {
+  const u16* x;  // A planes [NP][N,H,W,C] (DGRAD: dz)
+  long xps;
+  unsigned xbytes;
+  const u16* w;  // weight planes [Kf][3][3][Cf]
+  long wps;
+  unsigned wbytes;
+  float* out;  // [N,H,W,Nout] fp32, or split-K slabs
+  long slab;
+  int N, H, W, C, Nout;  // C: reduction channels
+  int gm, gn, cps;       // row tiles (image groups x position blocks), column tiles, chunks per split
+  int npb;               // position blocks per image group (H*W / PPT)
+  unsigned perm;         // position slot k -> local position, 4 bits per slot
+  int* sig;              // optional kernel-start stream signal (common.h start_signal)
+  int sig_val;
+};
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, int NI, int NSPX, int PD>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_pos_kernel(PArgs a) {
+  start_signal(a.sig, a.sig_val);
+  constexpr int THREADS = WAVES_M * WAVES_N * 64;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && NI % 32 == 0 && BM % NI == 0, "tile shape");
+  constexpr int SPP = NI / 32;   // 32-row sub-tiles per position
+  constexpr int PPT = BM / NI;   // positions per tile
+  static_assert(PPT <= 8, "perm holds 8 position slots");
+  constexpr int CPR = BC / 8;    // 16-B chunks per staged row
+  constexpr int RPB = 16 / CPR;  // staged rows per 256-B bank row
+  constexpr int SLOTS = NSPX * NI;
+  constexpr int A_PLANE = SLOTS * BC;
+  constexpr bool BSWZ = DG && BN >= 128;
+  constexpr int BPITCH = DG ? (BSWZ ? BN : BN + 32) : BC;
+  constexpr int B_PLANE = (DG ? BC : BN) * BPITCH;
+  constexpr int ACH = SLOTS * CPR;
+  constexpr int BCH = DG ? BC * BN / 8 : BN * CPR;
+  constexpr int NCA = (ACH + THREADS - 1) / THREADS;
+  constexpr int NCB = (BCH + THREADS - 1) / THREADS;
+  __shared__ __attribute__((aligned(16))) u16 lds[NP * A_PLANE + 2 * NP * B_PLANE];
+  u16* const As = lds;
+  u16* const Bs = lds + NP * A_PLANE;
+  auto swz = [](int row) { return (row / RPB) & (CPR - 1); };
+  auto rswz = [](int row, int col) { return BSWZ ? col ^ ((row & 3) << 5) : col; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the tap tests below branch on it
+  const int wr = wid / WAVES_N, wc = wid % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+  const int tile = xcd_remap(blockIdx.x, a.gm * a.gn);
+  const int bm = tile / a.gn, bn = tile % a.gn;
+  const int grp = bm / a.npb, pb = bm - grp * a.npb;
+  const int img0 = grp * NI, p0 = pb * PPT, n0 = bn * BN;
+  const int HW = a.H * a.W;
+  const int ylo = max(0, p0 / a.W - 1), yhi = min(a.H, (p0 + PPT - 1) / a.W + 2);
+  const int q0 = ylo * a.W, nq = (yhi - ylo) * a.W;  // staged pixels [q0, q0 + nq), nq <= NSPX (host check)
+
+  __amdgpu_buffer_rsrc_t rx[NP], rw[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    rx[p] = plane_rsrc(a.x + p * a.xps, a.xbytes);
+    rw[p] = plane_rsrc(a.w + p * a.wps, a.wbytes);
+  }
+
+  // A staging: chunk q = tid + j * THREADS is 16-B piece q % CPR of slot q / CPR = pixel * NI + image
+  long a_off[NCA];
+  bool a_ok[NCA];
+#pragma unroll
+  for (int j = 0; j < NCA; ++j) {
+    const int q = tid + j * THREADS;
+    const int slot = q / CPR, cc = q - slot * CPR;
+    const int pix = slot / NI, im = img0 + slot - pix * NI;
+    a_ok[j] = q < ACH && pix < nq && im < a.N;
+    a_off[j] = ((long)im * HW + q0 + pix) * a.C + cc * 8;
+  }
+  long b_off[NCB];
+  bool b_ok[NCB];
+#pragma unroll
+  for (int j = 0; j < NCB; ++j) {
+    const int q = tid + j * THREADS;
+    if constexpr (DG) {
+      const int k = q / (BN / 8), col = (q - k * (BN / 8)) * 8;
+      b_ok[j] = q < BCH && n0 + col < a.Nout;
+      b_off[j] = (long)k * 9 * a.Nout + n0 + col;
+    } else {
+      const int n = q / CPR, cc = q - n * CPR;
+      b_ok[j] = q < BCH && n0 + n < a.Nout;
+      b_off[j] = (long)(n0 + n) * 9 * a.C + cc * 8;
+    }
+  }
+
+  // B register ring: the weight tiles of the next PD steps are in flight
+  uint4 ra[NCA][NP], rb[PD][NCB][NP];
+  auto load_a = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < NCA; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) ra[j][p] = bload(rx[p], a_off[j] + c0, a_ok[j]);
+  };
+  auto store_a = [&]() {
+#pragma unroll
+    for (int j = 0; j < NCA; ++j) {
+      const int q = tid + j * THREADS;
+      const int slot = q / CPR, cc = q - slot * CPR;
+      if (ACH % THREADS == 0 || q < ACH) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          *reinterpret_cast<uint4*>(As + p * A_PLANE + slot * BC + ((cc ^ swz(slot)) << 3)) = ra[j][p];
+      }
+    }
+  };
+  auto load_b = [&](int rs, int step, int cb0) {  // weight tile of step `step` (chunk cb0 + step / 9)
+    const int tap = step % 9, c0 = (cb0 + step / 9) * BC;
+    const long d = DG ? ((long)c0 * 9 + 8 - tap) * a.Nout : (long)tap * a.C + c0;
+#pragma unroll
+    for (int j = 0; j < NCB; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rb[rs][j][p] = bload(rw[p], b_off[j] + d, b_ok[j]);
+  };
+  auto store_b = [&](int stage, int rs) {
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+      const int q = tid + j * THREADS;
+      if (BCH % THREADS == 0 || q < BCH) {
+        int idx;
+        if constexpr (DG) {
+          const int k = q / (BN / 8), col = (q - k * (BN / 8)) * 8;
+          idx = k * BPITCH + rswz(k, col);
+        } else {
+          const int n = q / CPR, cc = q - n * CPR;
+          idx = n * BC + ((cc ^ swz(n)) << 3);
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<uint4*>(Bs + (stage * NP + p) * B_PLANE + idx) = rb[rs][j][p];
+      }
+    }
+  };
+
+  // sub-tile i of this wave: position slot kp -> output position (py, px), image block ib
+  int fr_py[TM], fr_px[TM], fr_ib[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int k = wr * TM + i, kp = k / SPP;
+    const int pos = p0 + (int)((a.perm >> (4 * kp)) & 15u);
+    fr_py[i] = pos / a.W;
+    fr_px[i] = pos - fr_py[i] * a.W;
+    fr_ib[i] = (k - kp * SPP) * 32;
+  }
+
+  auto frag_k = [&](const u16* base, int row, int ks) -> bf16x8 {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + row * BC + (((2 * ks + lh) ^ swz(row)) << 3));
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto frag_r = [&](const u16* base, int col0, int ks) -> bf16x8 {
+    const int g = lane >> 4, idx = lane & 15;
+    const int q = idx >> 2, p4 = idx & 3;
+    const int col = col0 + 16 * (g & 1) + 4 * p4;
+    const int krow = 16 * ks + 8 * (g >> 1) + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const int scol = rswz(krow, col);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + krow * BPITCH + scol));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (krow + 4) * BPITCH + scol));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int tap, int stage) {
+    const int r = tap / 3, s = tap - 3 * (tap / 3);
+    bool v[TM];
+    int sl[TM];
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int iy = fr_py[i] + r - 1, ix = fr_px[i] + s - 1;
+      v[i] = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;  // wave-uniform
+      sl[i] = (iy * a.W + ix - q0) * NI + fr_ib[i] + li;
+      any = any || v[i];
+    }
+    if (!any) return;
+    const u16* Bst = Bs + stage * NP * B_PLANE;
+    constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};  // as mfma_tile
+#pragma unroll
+    for (int ks = 0; ks < BC / 16; ++ks) {
+      bf16x8 fb[TN][NP];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          if constexpr (DG)
+            fb[j][p] = frag_r(Bst + p * B_PLANE, wc * WTN + j * 32, ks);
+          else
+            fb[j][p] = frag_k(Bst + p * B_PLANE, wc * WTN + j * 32 + li, ks);
+        }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (!v[i]) continue;
+        bf16x8 fa[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fa[p] = frag_k(As + p * A_PLANE, sl[i], ks);
+#pragma unroll
+        for (int q = NP == 3 ? 0 : 5; q < 6; ++q)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[NP == 3 ? PA[q] : 0], fb[j][NP == 3 ? PB[q] : 0],
+                                                                acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- main loop: step = (chunk, tap) as in conv_halo_kernel; the weight tile of step s sits in
+  // register slot s % PD from PD steps ahead until it is written to LDS stage s & 1 ----
+  const int nch = a.C / BC;
+  const int cb = blockIdx.y * a.cps, ce = min(nch, cb + a.cps);
+  const int nsteps = max(0, ce - cb) * 9;
+  if (nsteps > 0) {
+    load_a(cb * BC);
+#pragma unroll
+    for (int j = 0; j < PD; ++j)
+      if (j < nsteps) load_b(j, j, cb);
+    store_a();
+    store_b(0, 0);
+    if (PD < nsteps) load_b(0, PD, cb);
+    if (cb + 1 < ce) load_a((cb + 1) * BC);
+    __syncthreads();
+    for (int s0 = 0; s0 < nsteps; s0 += PD) {
+#pragma unroll
+      for (int j = 0; j < PD; ++j) {
+        const int st = s0 + j;
+        if (st < nsteps) {
+          const int tap = st % 9, ch = cb + st / 9;
+          compute(tap, st & 1);
+          if (st + 1 < nsteps) {
+            store_b((st + 1) & 1, (j + 1) % PD);
+            if (st + 1 + PD < nsteps) load_b((j + 1) % PD, st + 1 + PD, cb);
+            if (tap == 8) {  // every wave is done with this chunk's image before it is replaced
+              __syncthreads();
+              store_a();
+              if (ch + 2 < ce) load_a((ch + 2) * BC);
+            }
+          }
+          __syncthreads();
+        }
+      }
+    }
+  }
+
+  // ---------------- epilogue: sub-tile rows are (image, position) -> NHWC row image * HW + position
+  float* out = a.out + (long)blockIdx.y * a.slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int pos = fr_py[i] * a.W + fr_px[i];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc * WTN + j * 32 + li;
+      if (col < a.Nout) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int im = img0 + fr_ib[i] + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (im < a.N) out[((long)im * HW + pos) * a.Nout + col] = acc[i][j][r];
+        }
+      }
+    }
+  }
+}
+
 // ---------------- fp32 -> bf16 planes ----------------
 // x [n] fp32 -> planes [NP][n] (n % 4 == 0)
 template <int NP>
@@ -1231,6 +1527,101 @@ int run_halo_wgrad(WHArgs& a, int tile, int splits, int np, float* dw, float* sl
   return launch_splitk_reduce(slab, dw, (long)a.K * 9 * a.C / 4, splits, st);
 }
 
+
+// ---- position-major tiles (small images): ids 24-29 ----
+//   24 / 25: 256 rows (32 images x 8 positions) x 128, 4x2 waves, 32-channel chunks, <= 12 staged
+//            pixels (4x4 images), weight tiles 1 / 4 steps ahead
+//   26:      256 rows (64 images x 4 positions) x 128, 4x2 waves, 32-channel chunks, <= 4 staged pixels
+//   27 / 28: 256 rows (64 images x 4 positions) x 64, 4x2 waves of 64x32, 32-channel chunks, <= 4
+//            staged pixels (2x2 images), weight tiles 1 / 4 steps ahead
+//   29:      as 24 with 16-channel chunks
+bool is_pos(int tile) { return tile >= 24 && tile <= 29; }
+int pos_bm(int) { return 256; }
+int pos_ni(int tile) { return (tile >= 26 && tile <= 28) ? 64 : 32; }
+int pos_bn(int tile) { return (tile == 27 || tile == 28) ? 64 : 128; }
+int pos_bc(int tile) { return tile == 29 ? 16 : 32; }
+int pos_nspx(int tile) { return (tile >= 26 && tile <= 28) ? 4 : 12; }
+int pos_waves_m(int) { return 4; }
+
+// staged pixels of the worst position block, or -1 when the positions do not tile the image
+int pos_staged(int H, int W, int ppt) {
+  if (H < 2 || W < 2 || (H * W) % ppt) return -1;
+  int worst = 0;
+  for (int p0 = 0; p0 < H * W; p0 += ppt) {
+    const int ylo = std::max(0, p0 / W - 1), yhi = std::min(H, (p0 + ppt - 1) / W + 2);
+    worst = std::max(worst, (yhi - ylo) * W);
+  }
+  return worst;
+}
+
+// Position order of a tile (4 bits per slot): longest-processing-time assignment of the positions of
+// the first position block to the row waves (PPT / waves_m positions each), by in-image tap count.
+unsigned pos_perm(int H, int W, int ppt, int waves_m) {
+  const int per = std::max(1, ppt / waves_m), groups = ppt / per;
+  int cnt[8], order[8], gsum[8] = {0}, gn[8] = {0}, slot[8][8];
+  for (int l = 0; l < ppt; ++l) {
+    const int y = l / W, x = l % W;
+    const int ry = 3 - (y == 0) - (y == H - 1), rx = 3 - (x == 0) - (x == W - 1);
+    cnt[l] = ry * rx;
+    order[l] = l;
+  }
+  std::stable_sort(order, order + ppt, [&](int u, int v) { return cnt[u] > cnt[v]; });
+  for (int t = 0; t < ppt; ++t) {
+    int best = -1;
+    for (int g = 0; g < groups; ++g)
+      if (gn[g] < per && (best < 0 || gsum[g] < gsum[best])) best = g;
+    slot[best][gn[best]++] = order[t];
+    gsum[best] += cnt[order[t]];
+  }
+  unsigned perm = 0;
+  int k = 0;
+  for (int g = 0; g < groups; ++g)
+    for (int e = 0; e < per; ++e) perm |= (unsigned)slot[g][e] << (4 * k++);
+  return perm;
+}
+
+template <int BM, int BN, int WM, int WN, bool DG, int NP, int BC, int NI, int NSPX, int PD>
+int launch_pos(const PArgs& a, int splits, hipStream_t st) {
+  dim3 grid(a.gm * a.gn, splits);
+  conv_pos_kernel<BM, BN, WM, WN, DG, NP, BC, NI, NSPX, PD><<<grid, WM * WN * 64, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+template <bool DG, int NP>
+int launch_pos_tile(const PArgs& a, int tile, int splits, hipStream_t st) {
+  switch (tile) {
+    case 24: return launch_pos<256, 128, 4, 2, DG, NP, 32, 32, 12, 1>(a, splits, st);
+    case 25: return launch_pos<256, 128, 4, 2, DG, NP, 32, 32, 12, 4>(a, splits, st);
+    case 26: return launch_pos<256, 128, 4, 2, DG, NP, 32, 64, 4, 1>(a, splits, st);
+    case 27: return launch_pos<256, 64, 4, 2, DG, NP, 32, 64, 4, 1>(a, splits, st);
+    case 28: return launch_pos<256, 64, 4, 2, DG, NP, 32, 64, 4, 4>(a, splits, st);
+    default: return launch_pos<256, 128, 4, 2, DG, NP, 16, 32, 12, 1>(a, splits, st);
+  }
+}
+
+// -6: the conv does not fit the tile (channels, or more staged pixels than the tile holds)
+template <bool DG>
+int run_pos(PArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st,
+            const void* add = nullptr) {
+  const int BM = pos_bm(tile), NI = pos_ni(tile), BC = pos_bc(tile), ppt = BM / NI;
+  const int ns = pos_staged(a.H, a.W, ppt);
+  if (obf || a.C % BC || a.Nout % 8 || ns < 0 || ns > pos_nspx(tile)) return -6;
+  if (add && splits > 1 && !reduce) return -4;
+  const long M = (long)a.N * a.H * a.W;
+  a.npb = a.H * a.W / ppt;
+  a.perm = pos_perm(a.H, a.W, ppt, pos_waves_m(tile));
+  a.gm = cdiv(a.N, NI) * a.npb;
+  a.gn = cdiv(a.Nout, pos_bn(tile));
+  a.cps = cdiv(a.C / BC, splits);
+  a.out = splits > 1 ? slab : (float*)out;
+  a.slab = splits > 1 ? M * a.Nout : 0;
+  const int rc = np == 3 ? launch_pos_tile<DG, 3>(a, tile, splits, st) : launch_pos_tile<DG, 1>(a, tile, splits, st);
+  if (rc) return rc;
+  if (splits == 1) return add ? dpa_add_inplace(out, add, M * a.Nout, 0, st) : 0;
+  if (!reduce) return 0;
+  return launch_splitk_reduce_t(slab, (float4*)out, M * a.Nout / 4, splits, st, (const float4*)add);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1240,6 +1631,8 @@ int dpa_x3_splits(int Kred, int splits) { return xsplits(Kred, splits); }
 // x planes [NP][N,H,W,C] (plane stride xps), w planes [NP][Kout][R][S][C] (stride wps; for a data
 // gradient pass the flipped/transposed Wd planes), out fp32 [N,P,Q,Kout] (or slabs, see
 // conv_gemm.hip).  np: 1 (bf16) or 3 (fp32 via bf16x6).  tile: 0 = 128x128, 1 = 64x64.
+// posmajor: bit 0 = position-major GEMM rows, bit 1 = column-tile-outer block order (Args.nmajor;
+// implicit-GEMM tiles only, the halo kernels ignore it).
 int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
                       int posmajor, int np, int obf, hipStream_t st) {
@@ -1258,6 +1651,21 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
     if (halo_bytes(h.xbytes, (long)N * H * W * C, h.wbytes, (long)Kout * 9 * C)) return -5;
     return run_halo<false>(h, tile, xsplits(9 * C, splits), np, obf, slab, out, reduce, st);
   }
+  if (is_pos(tile)) {
+    if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
+    PArgs q{};
+    q.x = x;
+    q.xps = xps;
+    q.w = w;
+    q.wps = wps;
+    q.N = N;
+    q.H = H;
+    q.W = W;
+    q.C = C;
+    q.Nout = Kout;
+    if (halo_bytes(q.xbytes, (long)N * H * W * C, q.wbytes, (long)Kout * 9 * C)) return -5;
+    return run_pos<false>(q, tile, xsplits(9 * C, splits), np, obf, slab, out, reduce, st);
+  }
   Args a{};
   a.x = x;
   a.xps = xps;
@@ -1270,7 +1678,8 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   a.gm = cdiv(a.M, tile_rows(tile));
   a.gn = cdiv(Kout, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
-  a.posmajor = posmajor ? 1 : 0;
+  a.posmajor = posmajor & 1;
+  a.nmajor = (posmajor >> 1) & 1;
   if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;
@@ -1312,6 +1721,23 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
     if (halo_bytes(h.xbytes, (long)N * H * W * K, h.wbytes, (long)K * 9 * C)) return -5;
     return run_halo<true>(h, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st, add);
   }
+  if (is_pos(tile)) {
+    if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
+    PArgs q{};
+    q.sig = sig;
+    q.sig_val = sig_val;
+    q.x = dz;
+    q.xps = dzps;
+    q.w = w;
+    q.wps = wps;
+    q.N = N;
+    q.H = H;
+    q.W = W;
+    q.C = K;
+    q.Nout = C;
+    if (halo_bytes(q.xbytes, (long)N * H * W * K, q.wbytes, (long)K * 9 * C)) return -5;
+    return run_pos<true>(q, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st, add);
+  }
   Args a{};
   a.sig = sig;
   a.sig_val = sig_val;
@@ -1334,7 +1760,8 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   a.gm = cdiv(a.M, tile_rows(tile));
   a.gn = cdiv(C, tile_cols(tile));
   a.splits = xsplits(a.Ktot, splits);
-  a.posmajor = posmajor ? 1 : 0;
+  a.posmajor = posmajor & 1;
+  a.nmajor = (posmajor >> 1) & 1;
   if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)dx;
   a.outb = (u16*)dx;
@@ -1381,7 +1808,8 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   a.gm = cdiv(Kout, tile_rows(tile));
   a.gn = cdiv(a.Ktot, tile_cols(tile));
   a.splits = xsplits(a.M, splits);
-  a.posmajor = posmajor ? 1 : 0;
+  a.posmajor = posmajor & 1;
+  a.nmajor = (posmajor >> 1) & 1;
   a.out = a.splits > 1 ? slab : dw;
   a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
   const int rc = np == 3 ? launch_tile<XM_WGRAD, 3>(a, tile, st) : launch_tile<XM_WGRAD, 1>(a, tile, st);

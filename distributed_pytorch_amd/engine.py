@@ -86,6 +86,10 @@ def tuning_table() -> Dict[str, list]:
         if os.path.exists(p) and os.environ.get("DPA_NO_TUNING", "0") != "1":
             with open(p) as f:
                 _TUNING = json.load(f)
+        extra = os.environ.get("DPA_TUNING_EXTRA")  # A/B of candidate entries (tools/tune_convs.py output)
+        if extra:
+            with open(extra) as f:
+                _TUNING.update(json.load(f))
     return _TUNING
 
 
@@ -98,6 +102,8 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
 HALO_TILES = (16, 17, 18, 19, 20, 21)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19) or 64 (20, 21)
                                        # output channels, 16 or 32-channel chunks
 HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
+POS_TILES = (24, 25, 26, 27, 28, 29)  # fprop / dgrad of small images: position-major rows, padding taps
+                                      # skipped (conv_x3.hip conv_pos_kernel)
 
 
 def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
@@ -111,6 +117,22 @@ def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
         return False
     bm, bc = (256 if tile in (16, 17, 20) else 128), (32 if tile & 1 or tile == 20 else 16)
     return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= bm + bm // 2
+
+
+def pos_ok(kind: str, tile: int, h: int, w: int, cred: int, cout: int) -> bool:
+    """Whether position-major tile `tile` runs conv call `kind` (fprop / dgrad of a 3x3/s1/p1 conv)
+    on h x w images; mirrors run_pos in conv_x3.hip (-6 otherwise)."""
+    if kind == "wgrad" or tile not in POS_TILES or h < 2 or w < 2:
+        return False
+    bm = 256
+    ni = 64 if tile in (26, 27, 28) else 32
+    bc = 16 if tile == 29 else 32
+    nspx = 4 if tile in (26, 27, 28) else 12
+    ppt = bm // ni
+    if (h * w) % ppt or cred % bc or cout % 8:
+        return False
+    worst = max((min(h, (p0 + ppt - 1) // w + 2) - max(0, p0 // w - 1)) * w for p0 in range(0, h * w, ppt))
+    return worst <= nspx
 
 
 class VGGEngine:
@@ -459,7 +481,7 @@ class VGGEngine:
             gm, gn, gk = M, l.cout, 9 * l.cin_pad
         t = tuning_table().get(conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout))
         if t is not None:
-            tile, s, pm = int(t[0]), int(t[1]), bool(t[2])
+            tile, s, pm = int(t[0]), int(t[1]), int(t[2])  # pm: bit 0 position-major, bit 1 column-tile order
         elif impl == "fp32":
             tile, s = conv_cfg("wgrad" if kind == "wgrad" else "fprop", gm, gn, gk)
             pm = l.hw <= 8
@@ -493,13 +515,15 @@ class VGGEngine:
         l = self.spec.convs[i]
         tiles = (0, 1) if impl == "fp32" else tuple(range(16))
         splits = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if kind == "wgrad" else (1, 2, 4, 8, 16)
-        out = [(t, s, pm) for t in tiles for s in splits for pm in (False, True)]
+        pms = (0, 1) if impl == "fp32" else (0, 1, 2, 3)  # x3 tiles: bit 1 = column-tile-outer block order
+        out = [(t, s, pm) for t in tiles for s in splits for pm in pms]
         if impl != "fp32":  # halo tiles ignore the row order flag
             if kind == "wgrad":
                 ok = [t for t in HALO_WGRAD_TILES if halo_ok(kind, t, l.hw, l.cin_pad, l.cout)]
             else:
                 cred, cout = (l.cin_pad, l.cout) if kind == "fprop" else (l.cout, l.cin_pad)
                 ok = [t for t in HALO_TILES if halo_ok(kind, t, l.hw, cred, cout)]
+                ok += [t for t in POS_TILES if pos_ok(kind, t, l.hw, l.hw, cred, cout)]
             out += [(t, s, False) for t in ok for s in splits]
         return out
 
@@ -540,6 +564,9 @@ class VGGEngine:
                     ev1.record()
                     torch.cuda.synchronize(self.device)
                     ms = ev0.elapsed_time(ev1) / iters
+                    if verbose and os.environ.get("DPA_TUNE_VERBOSE_ALL") == "1":
+                        print("  cand", conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout), [tile, s, pm, round(ms, 5)],
+                              flush=True)
                     if best is None or ms < best[3]:
                         best = [tile, s, pm, ms]
                 self._cfg_cache[key] = tuple(best[:3])

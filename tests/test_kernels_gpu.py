@@ -411,3 +411,74 @@ def test_conv_x3_dgrad_with_addend(shape, splits, tile, obf):
     torch.cuda.synchronize()
     ref = gx.permute(0, 2, 3, 1) + addd.double().cpu()
     assert rel_err(dx, ref) < (2e-2 if obf else 1e-5)
+
+
+# ----------------------------------------------------------------- position-major small-image kernels
+POS_SHAPES = [
+    # N, H, W, C, K   (3x3, stride 1, pad 1)
+    (40, 2, 2, 64, 96),      # partial image group (40 of 64) and a partial column tile
+    (70, 4, 4, 64, 128),     # 4x4: position blocks of 4 / 8, partial group
+    (8, 2, 4, 32, 32),       # non-square image
+    (256, 2, 2, 512, 512),   # VGG-11 layers 6-7 at batch 256
+    (64, 4, 4, 256, 512),    # VGG-11 layer 4 (a quarter of the batch)
+]
+
+
+def _pos_ok(kind, tile, h, w, cred, cout):
+    from distributed_pytorch_amd.engine import pos_ok
+
+    return pos_ok(kind, tile, h, w, cred, cout)
+
+
+@pytest.mark.parametrize("shape", POS_SHAPES)
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("tile", [24, 25, 26, 27, 28, 29])
+@pytest.mark.parametrize("np_", [3, 1])
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_conv_pos(shape, splits, tile, np_, dgrad):
+    """Position-major 3x3 fprop / data gradient with padding taps skipped (tiles 24-29) against
+    fp64, and bit-for-bit against the halo kernel with the same channel chunk and split count (a
+    skipped tap only adds exact zeros there)."""
+    C = _C()
+    N, H, W, Cin, K = shape
+    cred, cout = (K, Cin) if dgrad else (Cin, K)
+    kind = "dgrad" if dgrad else "fprop"
+    if not _pos_ok(kind, tile, H, W, cred, cout):
+        pytest.skip("shape outside this tile")
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(dgrad)
+    w = torch.randn(K, Cin, 3, 3, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, padding=1)
+    w3 = _planes(w.float().permute(0, 2, 3, 1), np_)
+    tol = 1e-5 if np_ == 3 else 2e-2
+    halo = 18 if tile == 29 else 19  # the halo tile with the same channel chunk (16 / 32)
+    outs = []
+    for t in (tile, halo):
+        if not dgrad:
+            out = torch.empty(N, H, W, K, device="cuda")
+            slab = torch.empty(splits * N * H * W * K, device="cuda") if splits > 1 else None
+            C.conv_x3_fprop(_planes(x.float().permute(0, 2, 3, 1), np_), w3, out, slab, 1, 1, splits, t, True, False)
+        else:
+            dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(20), dtype=torch.float64)
+            out = torch.empty(N, H, W, Cin, device="cuda")
+            slab = torch.empty(splits * N * H * W * Cin, device="cuda") if splits > 1 else None
+            C.conv_x3_dgrad(_planes(dy.float().permute(0, 2, 3, 1), np_), w3, out, slab, 1, 1, splits, t, True, False)
+        torch.cuda.synchronize()
+        outs.append(out)
+    if not dgrad:
+        ref = y.detach()
+    else:
+        (ref,) = torch.autograd.grad(y, x, dy)
+    assert rel_err(outs[0].permute(0, 3, 1, 2), ref) < tol
+    if _halo_ok(kind, halo, W, cred, cout):
+        assert torch.equal(outs[0], outs[1])
+
+
+def test_pos_rejects_unsupported_shapes():
+    """A position-major tile on an image with too many staged pixels fails loudly."""
+    C = _C()
+    x3 = torch.zeros(1, 32, 8, 8, 32, device="cuda", dtype=torch.bfloat16)  # 8x8: more than 12 staged pixels
+    w3 = torch.zeros(1, 32, 3, 3, 32, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(32, 8, 8, 32, device="cuda")
+    with pytest.raises(RuntimeError):
+        C.conv_x3_fprop(x3, w3, out, None, 1, 1, 1, 25, True, False)

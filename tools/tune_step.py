@@ -144,7 +144,7 @@ def main():
         for _ in range(2):
             step()
         if best != cur:
-            changed[k] = [best[0], best[1], bool(best[2]), iso.get(best, 0.0)]
+            changed[k] = [best[0], best[1], int(best[2]), iso.get(best, 0.0)]
         print(json.dumps({"key": k, "layers": layers, "choice": list(best), "was": list(cur),
                           "step_ms": round(best_ms, 4), "was_ms": round(cur_ms, 4)}), flush=True)
     final = step_ms(step, a.steps, a.reps * 2)
