@@ -69,7 +69,11 @@ int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long lo
 int dpa_x3_splits(int Kred, int splits);
 int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w, long wps, void* out, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
-                      int reduce, int posmajor, int np, int obf, hipStream_t st);
+                      int reduce, int posmajor, int np, int obf, hipStream_t st, float* stats);
+int dpa_conv_stats_rows(int tile);
+int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const float* gamma, const float* beta,
+                       const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
+                       float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* dz, long dzps, float* dw, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
                       int posmajor, int np, hipStream_t st);
@@ -324,7 +328,7 @@ void* conv_out_ptr(const Tensor& out, int np, const char* name, int& obf) {
 
 // x3 [NP,N,H,W,C], w3 [NP,K,R,S,C], out [N,P,Q,K] fp32 (or bf16 when NP == 1)
 void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, int64_t posmajor) {
+                   int64_t tile, bool reduce, int64_t posmajor, OptT stats) {
   need_planes(x3, "x3");
   need_planes(w3, "w3");
   const int np = x3.size(0);
@@ -344,9 +348,36 @@ void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, 
     TORCH_CHECK(slab->numel() >= (int64_t)eff * N * P * Q * K, "conv_x3_fprop: slab too small");
     sl = fp(*slab);
   }
+  float* stp = nullptr;
+  if (stats.has_value() && stats->defined()) {  // BN partials from the epilogue (one split only)
+    need(*stats, "stats");
+    const int rows = dpa_conv_stats_rows((int)tile);
+    TORCH_CHECK(rows > 0, "conv_x3_fprop: this tile cannot emit BN statistics");
+    TORCH_CHECK(stats->numel() >= 2 * (int64_t)((N * P * Q + rows - 1) / rows) * K, "conv_x3_fprop: stats too small");
+    stp = fp(*stats);
+  }
   chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), op, sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf, cur_stream()),
+                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf, cur_stream(), stp),
       "conv_x3_fprop");
+}
+
+// BN finalize from channel-major (mean, M2) partials [C][nblk] of row blocks of rpb rows (a conv
+// epilogue's statistics)
+void bn_finalize(Tensor part, int64_t nblk, int64_t rpb, int64_t M, Tensor gamma, Tensor beta, OptT bias, OptT rmean,
+                 OptT rvar, OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum,
+                 double eps) {
+  need(part, "part");
+  const int C = gamma.numel();
+  TORCH_CHECK(nblk == (M + rpb - 1) / rpb && part.numel() >= 2 * nblk * C, "bn_finalize: partial layout");
+  long long* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    need(*nbt, "nbt", at::kLong);
+    nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  chk(dpa_bn_finalize_cm(fp(part), (int)nblk, (int)rpb, (int)M, C, fp(gamma), fp(beta), ofp(bias), ofp(rmean),
+                         ofp(rvar), nb, fp(mean), fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps,
+                         cur_stream()),
+      "bn_finalize");
 }
 
 // x3 [NP,N,H,W,C], dz3 [NP,N,P,Q,K], dw [K,R,S,C] fp32
@@ -1076,7 +1107,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("x3_splits", &x3_splits);
   m.def("conv_x3_fprop", &conv_x3_fprop, py::arg("x3"), py::arg("w3"), py::arg("out"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
-        py::arg("posmajor") = 0);
+        py::arg("posmajor") = 0, py::arg("stats") = py::none());
+  m.def("conv_stats_rows", [](int64_t tile) { return (int64_t)dpa_conv_stats_rows((int)tile); });
+  m.def("bn_finalize", &bn_finalize);
   m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0);
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),

@@ -305,6 +305,62 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
   }
 }
 
+// Finalize from CHANNEL-MAJOR (mean, M2) partials part[c][k] (a conv epilogue's statistics,
+// conv_x3.hip epi_col_stats: up to thousands of row tiles per channel).  One block per channel:
+// 256 threads stride the channel's contiguous partials with 8 loads in flight, then a fixed-order
+// tree merge.
+__global__ __launch_bounds__(256) void bn_finalize_cm_kernel(const float2* __restrict__ part, int nblk, int rpb, int M,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta,
+                                                             const float* __restrict__ bias, float* __restrict__ rmean,
+                                                             float* __restrict__ rvar, long long* __restrict__ nbt,
+                                                             float* __restrict__ mean_out,
+                                                             float* __restrict__ invstd_out, float* __restrict__ scale,
+                                                             float* __restrict__ shift, float momentum, float eps) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const float2* pc = part + (long)c * nblk;
+  Welford acc{0.f, 0.f, 0.f};
+  int k = t;
+  for (; k + 7 * 256 < nblk; k += 8 * 256) {
+    float2 p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = pc[k + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kk = k + 256 * u;
+      acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
+    }
+  }
+  for (; k < nblk; k += 256) {
+    const float2 p = pc[k];
+    acc = merge(acc, Welford{(float)min(rpb, M - k * rpb), p.x, p.y});
+  }
+  __shared__ Welford sh[256];
+  sh[t] = acc;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if (t < o) sh[t] = merge(sh[t], sh[t + o]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    const Welford w = sh[0];
+    const float var = w.m2 / w.n;
+    const float inv = rsqrtf(var + eps);
+    const float gm = gamma[c];
+    mean_out[c] = w.mean;
+    invstd_out[c] = inv;
+    scale[c] = gm * inv;
+    shift[c] = beta[c] - w.mean * gm * inv;
+    if (rmean) {
+      const float b = bias ? bias[c] : 0.f;
+      const float unb = w.n > 1.f ? w.m2 / (w.n - 1.f) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (w.mean + b);
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+    }
+    if (c == 0 && nbt) nbt[0] += 1;
+  }
+}
+
 // Eval-mode affine: y = gamma*(z + b - rm)/sqrt(rv+eps) + beta = z*scale + shift
 __global__ void bn_eval_params_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                       const float* __restrict__ bias, const float* __restrict__ rmean,
@@ -1007,6 +1063,15 @@ int dpa_bn_finalize(const float* part, int nblk, int rpb, int M, int C, const fl
                     float* scale, float* shift, float momentum, float eps, hipStream_t st) {
   bn_finalize_kernel<<<cdiv(C, 4), 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, C, gamma, beta,
                                                   bias, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
+  return (int)hipGetLastError();
+}
+
+// Finalize from channel-major partials part[c][k] (conv epilogue statistics).
+int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const float* gamma, const float* beta,
+                       const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
+                       float* scale, float* shift, float momentum, float eps, hipStream_t st) {
+  bn_finalize_cm_kernel<<<C, 256, 0, st>>>(reinterpret_cast<const float2*>(part), nblk, rpb, M, gamma, beta, bias,
+                                           rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps);
   return (int)hipGetLastError();
 }
 

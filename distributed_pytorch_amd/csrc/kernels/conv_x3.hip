@@ -82,6 +82,7 @@ struct Args {
   FastDiv fd_C, fd_S, fd_Q, fd_PQ, fd_N;
   int* sig;  // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
+  float2* stats;  // FPROP, one split: per (row tile, output channel) BN (mean, M2) of the outputs
 };
 
 __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& img, unsigned& oh, unsigned& ow) {
@@ -131,6 +132,88 @@ __device__ __forceinline__ void mfma_tile(f32x16 (&acc)[TM][TN], const bf16x8 (&
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][PA[q]], fb[j][PB[q]], acc[i][j], 0, 0, 0);
+}
+
+// ---- BatchNorm statistics in the forward conv's epilogue ----
+// The BN that follows a conv needs per-channel (mean, M2) of its output; computing them here, from
+// the accumulators, saves the statistics pass's full read of z.  Per output column: each lane
+// over its TM x 16 rows in one pass of sums shifted by its first row (as bn_stats_kernel), the two
+// half-waves (lane, lane ^ 32), then the WAVES_M row waves through LDS, all merged in a fixed order
+// (deterministic).  The block writes (mean, M2) of its rows CHANNEL-MAJOR, part[col][row tile]
+// (bn_finalize_cm reads a channel's partials contiguously: a conv has up to thousands of row
+// tiles).  The statistics are those of the fp32 accumulators also when the output is stored as
+// bf16 (ROUND would take the rounded values: two more VALU operations per element in an epilogue
+// of memory-bound convs, for a difference far below bf16 resolution -- round-to-nearest-even
+// errors average out of a mean over thousands of rows).  Rows >= M are excluded.
+struct EWelford {
+  float n, mean, m2;
+};
+__device__ __forceinline__ EWelford ew_merge(EWelford a, EWelford b) {
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float n = a.n + b.n, d = b.mean - a.mean, f = b.n / n;
+  return EWelford{n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, bool ROUND>
+__device__ __forceinline__ void epi_col_stats(const f32x16 (&acc)[TM][TN], int rows_left, int wr, int wc, int lane,
+                                              float* sh, float2* part, int nblk, int bm, int ncols) {
+  constexpr int WTN = TN * 32, BNC = WAVES_N * WTN;
+  const int li = lane & 31, lh = lane >> 5;
+  __syncthreads();  // every wave is done with the main loop's LDS
+  const bool full = rows_left >= TM * 32;  // wave-uniform: no row of this wave tile is past M
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    float k0 = acc[0][j][0];
+    if (ROUND) k0 = bf16_f(bf16_rne(k0));
+    float n = 0.f, s1 = 0.f, s2 = 0.f;
+    if (full) {
+      n = TM * 16;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[i][j][r];
+          if (ROUND) v = bf16_f(bf16_rne(v));
+          const float d = v - k0;
+          s1 += d;
+          s2 = fmaf(d, d, s2);
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[i][j][r];
+          if (ROUND) v = bf16_f(bf16_rne(v));
+          const float d = v - k0;
+          if (i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh < rows_left) {
+            n += 1.f;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+          }
+        }
+    }
+    const float inv = n > 0.f ? 1.f / n : 0.f;
+    const EWelford mine{n, k0 + s1 * inv, fmaxf(s2 - s1 * s1 * inv, 0.f)};
+    const EWelford other{__shfl_xor(mine.n, 32), __shfl_xor(mine.mean, 32), __shfl_xor(mine.m2, 32)};
+    const EWelford w = lh == 0 ? ew_merge(mine, other) : ew_merge(other, mine);
+    if (lh == 0) {
+      float* o = sh + (wr * BNC + wc * WTN + j * 32 + li) * 3;
+      o[0] = w.n;
+      o[1] = w.mean;
+      o[2] = w.m2;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < BNC; c += WAVES_M * WAVES_N * 64) {
+    EWelford w{0.f, 0.f, 0.f};
+    for (int r = 0; r < WAVES_M; ++r) {
+      const float* o = sh + (r * BNC + c) * 3;
+      w = ew_merge(w, EWelford{o[0], o[1], o[2]});
+    }
+    if (c < ncols) part[(long)c * nblk + bm] = make_float2(w.mean, w.m2);
+  }
 }
 
 // BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  LDS image layouts: see the
@@ -543,6 +626,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         }
       }
     }
+  if constexpr (MODE == XM_FPROP) {
+    if (a.stats != nullptr)
+      epi_col_stats<TM, TN, WAVES_M, WAVES_N, false>(acc, a.M - (m0 + wr * WTM), wr, wc, lane,
+                                                  reinterpret_cast<float*>(lds), a.stats + (long)n0 * a.gm, a.gm, bm,
+                                                  a.Nout - n0);
+  }
 }
 
 // ---------------- halo-staged direct 3x3 convolution (stride 1, pad 1) ----------------
@@ -574,6 +663,7 @@ struct HArgs {
   int gm, gn, cps;          // row / column tiles, reduction chunks per split
   int* sig;                 // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
+  float2* stats;            // FPROP, one split: per (row tile, output channel) BN (mean, M2)
 };
 
 // staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
@@ -813,6 +903,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
         }
       }
     }
+  if constexpr (!DG) {
+    if (a.stats != nullptr)
+      epi_col_stats<TM, TN, WAVES_M, WAVES_N, false>(acc, a.M - (m0 + wr * WTM), wr, wc, lane,
+                                                  reinterpret_cast<float*>(lds), a.stats + (long)n0 * a.gm, a.gm, bm,
+                                                  a.Nout - n0);
+  }
 }
 
 // ---------------- halo-staged 3x3 weight gradient (stride 1, pad 1) ----------------
@@ -1628,14 +1724,20 @@ extern "C" {
 
 int dpa_x3_splits(int Kred, int splits) { return xsplits(Kred, splits); }
 
+// rows per row tile of fprop tile `tile` (the stats partial row block), 0 if it cannot emit stats
+int dpa_conv_stats_rows(int tile) { return is_pos(tile) ? 0 : (is_halo(tile) ? halo_bm(tile) : tile_rows(tile)); }
+
 // x planes [NP][N,H,W,C] (plane stride xps), w planes [NP][Kout][R][S][C] (stride wps; for a data
 // gradient pass the flipped/transposed Wd planes), out fp32 [N,P,Q,Kout] (or slabs, see
 // conv_gemm.hip).  np: 1 (bf16) or 3 (fp32 via bf16x6).  tile: 0 = 128x128, 1 = 64x64.
 // posmajor: bit 0 = position-major GEMM rows, bit 1 = column-tile-outer block order (Args.nmajor;
 // implicit-GEMM tiles only, the halo kernels ignore it).
+// stats (optional, one split, implicit-GEMM or halo tiles): float2 [Kout][row tiles of conv_stats_rows]
+// BN (mean, M2) partials of the output, channel-major (epi_col_stats), for dpa_bn_finalize_cm.
 int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
-                      int posmajor, int np, int obf, hipStream_t st) {
+                      int posmajor, int np, int obf, hipStream_t st, float* stats) {
+  if (stats && (is_pos(tile) || (is_halo(tile) ? xsplits(9 * C, splits) : xsplits(R * S * C, splits)) > 1)) return -7;
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     HArgs h{};
@@ -1648,6 +1750,7 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
     h.W = W;
     h.C = C;
     h.Nout = Kout;
+    h.stats = reinterpret_cast<float2*>(stats);
     if (halo_bytes(h.xbytes, (long)N * H * W * C, h.wbytes, (long)Kout * 9 * C)) return -5;
     return run_halo<false>(h, tile, xsplits(9 * C, splits), np, obf, slab, out, reduce, st);
   }
@@ -1680,6 +1783,7 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor & 1;
   a.nmajor = (posmajor >> 1) & 1;
+  a.stats = reinterpret_cast<float2*>(stats);
   if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;

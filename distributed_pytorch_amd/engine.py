@@ -307,6 +307,17 @@ class VGGEngine:
         self.fpart = torch.zeros(max(fpart, 1), **f32)
         self.fcnt = torch.zeros(max(fcnt, 32), dtype=torch.int32, device=dev)
         self.bn_tmo = torch.zeros(1, dtype=torch.int32, device=dev)
+        # BN statistics from the forward conv's epilogue (conv_x3.hip epi_col_stats) for layers whose
+        # conv runs one split and whose BN is not the one-launch kernel: the statistics pass's read
+        # of z goes; DPA_EPI_STATS=0 keeps bn_stats_kernel
+        self.epi_stats = (dev.type == "cuda" and os.environ.get("DPA_EPI_STATS", "1") == "1"
+                          and hasattr(self.K, "conv_stats_rows"))
+        epart = 0
+        for i, l in enumerate(L):
+            rows = self._epi_rows(i, N)
+            if rows:
+                epart = max(epart, 2 * ((N * l.hw * l.hw + rows - 1) // rows) * l.cout)
+        self.epart = torch.empty(max(epart, 1), **f32)
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -586,16 +597,24 @@ class VGGEngine:
     def _in_planes(self, i: int, n: int) -> torch.Tensor:
         return self.x0p[:, :n] if i == 0 else self.a3[i - 1][:, :n]
 
-    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool) -> int:
+    def _epi_rows(self, i: int, n: int) -> int:
+        """Rows per statistics partial when layer i's BN takes its statistics from the conv
+        epilogue at batch n, else 0."""
+        if not (self.epi_stats and self.planes[i] and i > 0) or self._fused(i, n, False):
+            return 0
+        tile, s, _ = self.conv_config(i, "fprop", n)
+        return self.K.conv_stats_rows(tile) if s == 1 else 0
+
+    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool, stats: Optional[torch.Tensor] = None) -> int:
         """Forward conv of layer i into z[i] (or split-K slabs); returns the split count left
-        UNREDUCED in self.slab (1 = result is in z[i])."""
+        UNREDUCED in self.slab (1 = result is in z[i]).  stats: BN partials from the epilogue."""
         l = self.spec.convs[i]
         tile, s, pm = self.conv_config(i, "fprop", n)
         self._ensure_slab(self._slab_need(i, "fprop", n))
         z = self.z[i][:n]
         slab = self.slab if s > 1 else None
         if self.planes[i]:
-            self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm)
+            self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm, stats)
         else:
             xin = x if i == 0 else self.a[i - 1][:n]
             self.K.conv_fprop(xin, self.params[f"{l.conv_key}.weight"], z, slab, 1, 1, s, tile, False, reduce, pm)
@@ -693,10 +712,21 @@ class VGGEngine:
                             st["scale"], st["shift"], self.bn_momentum, self.bn_eps)
                 K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
-            ns = self._conv_fwd(i, x, n, reduce=False)
+            erows = self._epi_rows(i, n)
+            ns = self._conv_fwd(i, x, n, reduce=False, stats=self.epart if erows else None)
             if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
                 buffers_wait()
                 buffers_wait = None
+            if erows:
+                M = n * l.hw * l.hw
+                K.bn_finalize(self.epart, (M + erows - 1) // erows, erows, M, P[f"{l.bn_key}.weight"],
+                              P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
+                              self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
+                              self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
+                              self.bn_momentum, self.bn_eps)
+                if not (i == len(L) - 1 and self.fused_head):
+                    K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
+                continue
             if self._fused(i, n, False):
                 head = i == len(L) - 1 and self.fused_head  # the head kernel applies it
                 K.bn_fused_fwd(self.slab if ns > 1 else z, ns, z, l.pool, self.bn_fused_rmax, self.fpart, self.fcnt,

@@ -231,11 +231,19 @@ _DEFERRED: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
 DEFER_JOIN = os.environ.get("DPA_DEFER_JOIN", "1") == "1"  # A/B switch (0: add pass as before)
 DEFER_STATS = {"summed_on_load": 0}  # BN backwards that consumed a deferred contribution (tests)
 BN_RELU_MASK = os.environ.get("DPA_BN_RELU_MASK", "1") == "1"  # A/B switch (0: backward re-reads the residual)
+# BN statistics from the producing conv's epilogue (conv_x3.hip epi_col_stats): a training conv with
+# one split registers its (mean, M2) partials under its output's address; the BN that normalises
+# that output finalizes from them instead of re-reading z (bn_stats_kernel).
+EPI_STATS = os.environ.get("DPA_EPI_STATS", "1") == "1"
+# (entries hold the output tensor itself, so its address cannot be reused while the entry lives)
+_STATS: Dict[int, Tuple[torch.Tensor, int, int, Tuple[int, int], torch.Tensor]] = {}
+STATS_USED = {"epilogue": 0}  # BN forwards that finalized from conv epilogue partials (tests)
 
 
 def clear_deferred():
     """Drop deferred contributions of an abandoned backward (called at every training forward)."""
     _DEFERRED.clear()
+    _STATS.clear()
 
 
 class GradJoin:
@@ -349,13 +357,23 @@ class Conv2dNHWC(torch.autograd.Function):
         z = torch.empty(N, P, Q, K, device=x.device, dtype=act_dtype)
         geom = (N, H, W, C, K, R, S, stride, pad)
 
-        def run(tile, s, pm):
+        def run(tile, s, pm, stats=None):
             slab = WS.get("slab", s * N * P * Q * K, x.device) if s > 1 else None
-            Kx.conv_x3_fprop(xp, wp, z, slab, stride, pad, s, tile, True, pm)
+            Kx.conv_x3_fprop(xp, wp, z, slab, stride, pad, s, tile, True, pm, stats)
 
         cfg = choose_config(impl, "fprop", geom, N * P * Q, K, R * S * C, P * Q <= 16, run,
                             lambda s: 4 * s * N * P * Q * K)
-        run(cfg[0], Kx.x3_splits(R * S * C, cfg[1]), cfg[2])
+        sk = Kx.x3_splits(R * S * C, cfg[1])
+        # training (grad mode is off inside forward; the weight needing a gradient is the signal)
+        rows = Kx.conv_stats_rows(cfg[0]) if (EPI_STATS and sk == 1 and ctx.needs_input_grad[1]) else 0
+        stats = None
+        if rows > 0:
+            nblk = (N * P * Q + rows - 1) // rows
+            stats = torch.empty(2 * nblk * K, device=x.device, dtype=torch.float32)
+            while len(_STATS) >= 64:  # a conv whose output no BN normalised (not in the supported models)
+                _STATS.pop(next(iter(_STATS)))
+            _STATS[z.data_ptr()] = (stats, nblk, rows, (N * P * Q, K), z)
+        run(cfg[0], sk, cfg[2], stats)
         ctx.save_for_backward(xp, wp)
         return z
 
@@ -447,7 +465,12 @@ class BnActNHWC(torch.autograd.Function):
         # per-channel statistics in fp32 on GPU (bf16 activations too); the CPU oracle also runs fp64
         f32 = dict(device=dev, dtype=torch.float32 if _native(z) else z.dtype)
         mean, invstd, scale, shift = (torch.empty(C, **f32) for _ in range(4))
-        if training:
+        st = _STATS.pop(z.data_ptr(), None) if training and _native(z) else None
+        if st is not None and st[3] == (N * H * W, C):  # partials from the producing conv's epilogue
+            K.bn_finalize(st[0], st[1], st[2], N * H * W, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale,
+                          shift, momentum, eps)
+            STATS_USED["epilogue"] += 1
+        elif training:
             part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), dev, zero=True) if _native(z) else None
             K.bn_fwd_stats(z, 1, z, part, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale, shift, momentum,
                            eps)

@@ -482,3 +482,61 @@ def test_pos_rejects_unsupported_shapes():
     out = torch.empty(32, 8, 8, 32, device="cuda")
     with pytest.raises(RuntimeError):
         C.conv_x3_fprop(x3, w3, out, None, 1, 1, 1, 25, True, False)
+
+
+# ----------------------------------------------------------------- BN statistics from the conv epilogue
+EPI_SHAPES = [
+    # N, H, W, C, K, R, stride, pad
+    (3, 9, 9, 32, 48, 3, 1, 1),      # partial row tile, partial column tile
+    (2, 14, 14, 64, 128, 1, 1, 0),   # 1x1 (ResNet bottleneck)
+    (4, 8, 8, 16, 64, 3, 2, 1),      # strided
+]
+
+
+@pytest.mark.parametrize("shape", EPI_SHAPES)
+@pytest.mark.parametrize("tile", [0, 1, 5, 7, 11, 14, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("np_", [1, 3])
+@pytest.mark.parametrize("posmajor", [0, 1])
+def test_conv_epilogue_bn_stats(shape, tile, np_, posmajor):
+    """A one-split forward conv writes per-(row tile, channel) (mean, M2) of its output; the BN
+    finalize from them gives the batch statistics of the output -- against fp64 statistics of the
+    stored output (for bf16 output the statistics are those of the fp32 accumulators: within bf16
+    rounding of the stored values' statistics)."""
+    C_ = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    if tile >= 16 and (R != 3 or st != 1 or not _halo_ok("fprop", tile, W, Cin, K)):
+        pytest.skip("halo tiles are 3x3/s1 only")
+    if tile >= 16 and posmajor:
+        pytest.skip("halo tiles ignore the row order")
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(K, R, R, Cin, generator=g) * 0.1 + 0.02  # nonzero channel means
+    P = (H + 2 * pd - R) // st + 1
+    out = torch.empty(N, P, P, K, device="cuda", dtype=torch.bfloat16 if np_ == 1 else torch.float32)
+    rows = C_.conv_stats_rows(tile)
+    nblk = (N * P * P + rows - 1) // rows
+    stats = torch.full((2 * nblk * K,), float("nan"), device="cuda")
+    C_.conv_x3_fprop(_planes(x, np_), _planes(w, np_), out, None, st, pd, 1, tile, True, posmajor, stats)
+    dev = dict(device="cuda", dtype=torch.float32)
+    gamma, beta = torch.rand(K, **dev) + 0.5, torch.randn(K, **dev)
+    rm, rv, nbt = torch.zeros(K, **dev), torch.ones(K, **dev), torch.zeros(1, dtype=torch.int64, device="cuda")
+    mean, invstd, scale, shift = (torch.empty(K, **dev) for _ in range(4))
+    C_.bn_finalize(stats, nblk, rows, N * P * P, gamma, beta, None, rm, rv, nbt, mean, invstd, scale, shift, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    zz = out.double().cpu().reshape(-1, K)
+    mu, var = zz.mean(0), zz.var(0, unbiased=False)
+    tol = 1e-5 if np_ == 3 else 2e-3
+    assert rel_err(mean, mu) < tol
+    assert rel_err(invstd, torch.rsqrt(var + 1e-5)) < 10 * tol
+    assert rel_err(rv, 0.9 + 0.1 * zz.var(0, unbiased=True)) < 10 * tol
+    assert int(nbt.item()) == 1
+
+
+def test_conv_epilogue_stats_refused_with_split_k():
+    C_ = _C()
+    x3 = torch.zeros(1, 2, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
+    w3 = torch.zeros(1, 64, 3, 3, 64, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(2, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
+    slab = torch.empty(4 * out.numel(), device="cuda")
+    with pytest.raises(RuntimeError):
+        C_.conv_x3_fprop(x3, w3, out, slab, 1, 1, 4, 0, True, 0, torch.empty(2 * 64 * 64, device="cuda"))
