@@ -40,10 +40,11 @@ def main(argv=None):
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"])
     ap.add_argument("--autotune", action="store_true",
                     help="time every conv kernel config during warmup and save tuning/generic_mi355x.json")
-    ap.add_argument("--graph", default="off", choices=["on", "off"],
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="1 GPU: capture the whole training step (forward, backward through autograd, fused SGD) "
                          "as one HIP graph after the warmup and replay it (removes the host/autograd gaps "
-                         "between kernels)")
+                         "between kernels: +2.3 %% at batch 128, docs/PERF_NOTES.md).  auto = on for one rank "
+                         "(the multi-rank step issues its collectives from autograd hooks and stays eager)")
     ap.add_argument("--profile", action="store_true", help="re-run under rocprofv3 --kernel-trace --stats")
     ap.add_argument("--profile-dir", default="gpurun_out/prof_resnet")
     ap.add_argument("--launch-timeout", type=float, default=1800.0)
@@ -86,7 +87,7 @@ def main(argv=None):
         last["loss"] = step()
 
     graphed = False
-    if a.graph == "on" and ctx.world == 1 and dev.type == "cuda":
+    if a.graph in ("on", "auto") and ctx.world == 1 and dev.type == "cuda" and not a.autotune:
         # torch.cuda.graph recipe: eager warmup on a side stream, then capture one whole step.  The
         # replays run the identical kernels on the same static input / parameter / gradient
         # buffers; only the Python host work (autograd graph walk, launches) disappears.

@@ -469,6 +469,9 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // the summed g is written to gout (consumed by the apply pass).  g2 (optional, nsplit == 1): a second
 // contribution to the same gradient, summed on load here and in the apply pass instead of by a
 // separate add pass (ResNet: a block input's two gradient contributions, ops/functional.GradJoin).
+// dyout (ACT 2, optional): the gradient through the add+ReLU, dy = relu'(u + r) * (g + g2), is
+// stored here (it is the residual's gradient dres); the apply pass then reads dy alone (ACT 1)
+// instead of g, g2 and the mask again.
 // part layout: [block][3][C]
 template <bool POOL, int ACT, typename TZ, int RTB>
 __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
@@ -481,7 +484,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             float* __restrict__ part, int N, int H, int W, int C,
                                                             int rpb, int* sig, int sig_val,
                                                             const TZ* __restrict__ g2,
-                                                            const unsigned char* __restrict__ mask) {
+                                                            const unsigned char* __restrict__ mask,
+                                                            TZ* __restrict__ dyout) {
   start_signal(sig, sig_val);
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
@@ -518,6 +522,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
           const float4 r0v = ACT == 2 && !mk ? ld4(res, gi0) : make_float4(0.f, 0.f, 0.f, 0.f);
           const float4 r1v = ACT == 2 && !mk ? ld4(res, gi1) : make_float4(0.f, 0.f, 0.f, 0.f);
           const unsigned m0 = mk ? mask[gi0] : 0u, m1 = mk ? mask[gi1] : 0u;
+          float dy0[4], dy1[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float za = F4GET(z0, k), zb = F4GET(z1, k);
@@ -532,6 +537,12 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             sdy[k] += dyb;
             sdx[k] = fmaf(dyb, xb, sdx[k]);
             sx[k] += xb;
+            dy0[k] = dya;
+            dy1[k] = dyb;
+          }
+          if (ACT == 2 && dyout) {
+            st4(dyout, gi0, make_float4(dy0[0], dy0[1], dy0[2], dy0[3]));
+            st4(dyout, gi1, make_float4(dy1[0], dy1[1], dy1[2], dy1[3]));
           }
         }
       }
@@ -546,6 +557,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
           const bool mk = ACT == 2 && mask;
           const float4 rv = ACT == 2 && !mk ? ld4(res, gi) : make_float4(0.f, 0.f, 0.f, 0.f);
           const unsigned m = mk ? mask[gi] : 0u;
+          float dyv[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float zz = F4GET(zv, k);
@@ -555,7 +567,9 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             sdy[k] += dy;
             sdx[k] = fmaf(dy, xh, sdx[k]);
             sx[k] += xh;
+            dyv[k] = dy;
           }
+          if (ACT == 2 && dyout) st4(dyout, gi, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
         } else {
           const int ow = r % Wo;
           const int tt = r / Wo;
@@ -697,7 +711,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
         const float dy = mk ? (((m >> k) & 1u) ? F4GET(gv, k) : 0.f)
                             : act_grad<ACT>(fmaf(zz, F4GET(q.sc, k), F4GET(q.sh, k)), F4GET(rv, k), F4GET(gv, k));
         dyv[k] = dy;
-        r[k] = F4GET(q.k1, k) * dy + F4GET(q.k2, k) * zz + F4GET(q.k3, k);
+        // explicit fma order: every ACT instantiation rounds alike (the dy pass's ACT 1 apply is
+        // bitwise the ACT 2 one it replaces)
+        r[k] = fmaf(F4GET(q.k1, k), dy, fmaf(F4GET(q.k2, k), zz, F4GET(q.k3, k)));
       }
       store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]));
       if constexpr (ACT == 2) st4(dres, i, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
@@ -718,7 +734,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
                F4GET(gv, k), d[0], d[1], d[2], d[3]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          out[u][k] = F4GET(q.k1, k) * d[u] + F4GET(q.k2, k) * F4GET(zq[u], k) + F4GET(q.k3, k);
+          out[u][k] = fmaf(F4GET(q.k1, k), d[u], fmaf(F4GET(q.k2, k), F4GET(zq[u], k), F4GET(q.k3, k)));
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -831,7 +847,7 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
                   const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                   float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
                   hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
-                  const unsigned char* mask = nullptr) {
+                  const unsigned char* mask = nullptr, TZ* dyout = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = bwd_rows_per_block(Mo, C);
@@ -840,10 +856,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
 #define RED(P, A)                                                                                                 \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
-                                                            N, H, W, C, rpb, sig, sig_val, g2, mask);                   \
+                                                            N, H, W, C, rpb, sig, sig_val, g2, mask, dyout);            \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
-                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask)
+                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout)
   if (pool) {
     RED(true, 0);
   } else if (act == 0) {
@@ -1011,8 +1027,21 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
                 const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2,
                 const unsigned char* mask) {
   if (nsplit < 1) nsplit = 1;
+  // add+ReLU: the reduce pass stores dy (= dres) and the apply pass reads it alone as an identity
+  // activation (DPA_BN_DY_PASS=0: the apply re-reads g, g2 and the mask / residual)
+  const char* dy_env = std::getenv("DPA_BN_DY_PASS");  // read per call: tests switch it in-process
+  const bool dy_pass = !(dy_env && dy_env[0] == '0');
+  const bool dyp = dy_pass && act == 2 && nsplit == 1 && !pool && dres != nullptr;
   bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
-                   C, pool, act, res, st, sig, sig_val, g2, mask);
+                   C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr);
+  if (dyp) {
+    act = 1;
+    gsrc = dres;
+    g2 = nullptr;
+    mask = nullptr;
+    res = nullptr;
+    dres = nullptr;
+  }
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
   const long total = (long)Mo * (C / 4);

@@ -28,6 +28,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);  // sgd.hip
 
@@ -83,6 +84,17 @@ struct Args {
   int* sig;  // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
   float2* stats;  // FPROP, one split: per (row tile, output channel) BN (mean, M2) of the outputs
+  // DGRAD of a stride-2 conv, phase-decomposed (nph = 4, blockIdx.z = phase): output rows of one
+  // phase (h % 2, w % 2) see only the filter taps r = r0 + 2 r', s = s0 + 2 s' that land on a dZ
+  // pixel, so each phase is a stride-1 gather over dZ with an R' x S' sub-filter (1x1/s2: one phase
+  // of 1 tap, three of 0; 3x3/s2: 1 + 2 + 2 + 4 taps) instead of the dilated form's 4x MFMA work
+  // on zeros.  Rows m of a phase are (img, i, j) of the H/2 x W/2 phase grid (P, Q, M), stored at
+  // dx pixel (img, 2i + ph, 2j + pw) of the outH x outW output.
+  int nph, outH, outW;
+  struct Phase {
+    int Ktot, S, r0, s0, padh, padw;
+    FastDiv fd_S;
+  } phase[4];
 };
 
 __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& img, unsigned& oh, unsigned& ow) {
@@ -272,11 +284,48 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   const int m0 = bm * BM, n0 = bn * BN;
   const int split = blockIdx.y;
 
+  // reduction geometry of this block (a phase of a phase-decomposed DGRAD has its own sub-filter)
+  int ktot = a.Ktot, sub_s = a.S, padh = a.pad, padw = a.pad, tap_r0 = 0, tap_s0 = 0, tap_st = 1, ph = 0, pw = 0;
+  FastDiv fd_sub = a.fd_S;
+  if constexpr (DG) {
+    if (a.nph > 1) {
+      const Args::Phase& q = a.phase[blockIdx.z];
+      ph = blockIdx.z >> 1;
+      pw = blockIdx.z & 1;
+      ktot = q.Ktot;
+      sub_s = q.S;
+      fd_sub = q.fd_S;
+      padh = q.padh;
+      padw = q.padw;
+      tap_r0 = q.r0;
+      tap_s0 = q.s0;
+      tap_st = 2;
+      if (ktot == 0) {  // a phase no tap reaches (1x1/s2: three of four): its rows of dx are zero;
+                        // 16-byte stores of the tile instead of the MFMA epilogue's 2/4-byte ones
+        constexpr int EPC = OB ? 8 : 4, CPRW = BN / EPC;
+        float* outz = a.out + (long)split * a.slab;
+        for (int q = tid; q < BM * CPRW; q += THREADS) {
+          const int rl = q / CPRW, col = n0 + (q - rl * CPRW) * EPC, row = m0 + rl;
+          if (row < a.M && col < a.Nout) {
+            const unsigned img = fdiv((unsigned)row, a.fd_PQ), pos = (unsigned)row - img * (unsigned)(a.P * a.Q);
+            const unsigned i = fdiv(pos, a.fd_Q), j = pos - i * (unsigned)a.Q;
+            const long mrow = ((long)img * a.outH + 2 * (int)i + ph) * a.outW + 2 * (int)j + pw;
+            if constexpr (OB)
+              *reinterpret_cast<uint4*>(a.outb + mrow * a.Nout + col) = make_uint4(0u, 0u, 0u, 0u);
+            else
+              *reinterpret_cast<float4*>(outz + mrow * a.Nout + col) = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+        return;
+      }
+    }
+  }
+
   // ---------------- reduction tile iterator with padding-tap skipping ----------------
   bool skip = false;
   int lo0 = 0, lo1 = 0, span1 = 1, per = 1, ntot;
   if constexpr (!WG) {
-    ntot = (a.Ktot + BK - 1) / BK;
+    ntot = (ktot + BK - 1) / BK;
     if (a.posmajor && a.imask == 0 && a.C % BK == 0 && a.N % BM == 0) {
       const int pos = m0 / a.N;
       const int oh = pos / a.Q, ow = pos - (pos / a.Q) * a.Q;
@@ -319,7 +368,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     else
       return (i0 * a.Q + i1) * a.N + sub * BK;
   };
-  const int KMAX = WG ? a.M : a.Ktot;
+  const int KMAX = WG ? a.M : ktot;
 
   // ---------------- per-thread staging slots ----------------
   // FPROP: chunk (row, kc) with kc = tid % CPR fixed, rows tid/CPR + j*(THREADS/CPR).
@@ -344,8 +393,8 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
         unsigned img, oh, ow;
         decode_row(a, (unsigned)m, img, oh, ow);
         a_img[j] = (int)img;
-        a_ih0[j] = (int)oh * a.stride - a.pad;
-        a_iw0[j] = (int)ow * a.stride - a.pad;
+        a_ih0[j] = (int)oh * a.stride - padh;
+        a_iw0[j] = (int)ow * a.stride - padw;
       }
     }
   } else {
@@ -376,8 +425,8 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
       const int k = kb + a_c8;
       const unsigned tap = fdiv((unsigned)k, a.fd_C);
       const int c = k - (int)tap * a.C;
-      const unsigned r = fdiv(tap, a.fd_S);
-      const int s = (int)(tap - r * a.S);
+      const unsigned r = fdiv(tap, fd_sub);
+      const int s = (int)(tap - r * sub_s);
       const bool kv = k < KMAX;
 #pragma unroll
       for (int j = 0; j < NCA; ++j) {
@@ -401,9 +450,10 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
           const bool vb = kr < KMAX && col < a.Nout;
           const unsigned tp = fdiv((unsigned)kr, a.fd_C);
           const int ko = kr - (int)tp * a.C;
-          const unsigned rr = fdiv(tp, a.fd_S);
-          const int ss = (int)(tp - rr * a.S);
-          const long boff = (((long)ko * a.R + (a.R - 1 - (int)rr)) * a.S + (a.S - 1 - ss)) * a.Nout + col;
+          const unsigned rr = fdiv(tp, fd_sub);
+          const int ss = (int)(tp - rr * sub_s);
+          const int fr = tap_r0 + tap_st * (int)rr, fs = tap_s0 + tap_st * ss;  // filter tap
+          const long boff = (((long)ko * a.R + (a.R - 1 - fr)) * a.S + (a.S - 1 - fs)) * a.Nout + col;
 #pragma unroll
           for (int p = 0; p < NP; ++p) rb[j][p] = bload(rw[p], boff, vb);
         }
@@ -617,6 +667,11 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
             if (remap) {
               const unsigned pos = fdiv((unsigned)row, a.fd_N);
               mrow = (long)(row - (int)pos * a.N) * PQ + pos;
+            }
+            if (DG && a.nph > 1) {  // phase grid row -> dx pixel
+              const unsigned img = fdiv((unsigned)row, a.fd_PQ), pos = (unsigned)row - img * (unsigned)PQ;
+              const unsigned i = fdiv(pos, a.fd_Q), j = pos - i * (unsigned)a.Q;
+              mrow = ((long)img * a.outH + 2 * (int)i + ph) * a.outW + 2 * (int)j + pw;
             }
             if constexpr (OB)
               a.outb[mrow * ldc + col] = bf16_rne(acc[i][j][r]);
@@ -1441,7 +1496,7 @@ __global__ __launch_bounds__(256) void pad_split_kernel(const float* __restrict_
 
 template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK, int NS, bool OB>
 int launch_x3(const Args& a, hipStream_t st) {
-  dim3 grid(a.gm * a.gn, a.splits);
+  dim3 grid(a.gm * a.gn, a.splits, a.nph > 1 ? a.nph : 1);
   conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS, OB><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
@@ -1850,15 +1905,47 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   a.w = w;
   a.wps = wps;
   if (stride < 1 || (stride & (stride - 1)) || R - 1 - pad < 0) return -3;
-  fill(a, N, Hd, Wd, K, R, S, 1, R - 1 - pad);
+  const int padd = R - 1 - pad;  // padding of the dilated-dZ gather
+  fill(a, N, Hd, Wd, K, R, S, 1, padd);
   if (set_bytes(a, (long)N * Hd * Wd * K, (long)K * R * S * C)) return -5;
-  a.P = H;
-  a.Q = W;
-  a.M = N * H * W;
-  a.fd_Q = make_fastdiv(W);
-  a.fd_PQ = make_fastdiv(H * W);
-  a.imask = stride - 1;
-  while ((1 << a.ishift) < stride) ++a.ishift;
+  const long Mfull = (long)N * H * W;
+  // stride 2 with even output sides: phase-decomposed (Args.phase); DPA_DGRAD_PHASE=0 keeps the
+  // dilated form (A/B)
+  const char* phase_env = getenv("DPA_DGRAD_PHASE");  // read per call: tests switch it in-process
+  const bool phase_on = !(phase_env && phase_env[0] == '0');
+  const bool phased = phase_on && stride == 2 && H % 2 == 0 && W % 2 == 0 && (posmajor & 1) == 0;
+  a.nph = 1;
+  if (phased) {
+    a.nph = 4;
+    a.outH = H;
+    a.outW = W;
+    a.P = H / 2;
+    a.Q = W / 2;
+    int kmax = 0;
+    for (int z = 0; z < 4; ++z) {
+      Args::Phase& q = a.phase[z];
+      const int zh = z >> 1, zw = z & 1;
+      q.r0 = (padd - zh) & 1;  // first tap with (h - padd + r) even for h = 2i + zh
+      q.s0 = (padd - zw) & 1;
+      const int Rp = q.r0 < R ? (R - q.r0 + 1) / 2 : 0, Sp = q.s0 < S ? (S - q.s0 + 1) / 2 : 0;
+      q.S = Sp > 0 ? Sp : 1;
+      q.fd_S = make_fastdiv(q.S);
+      q.Ktot = Rp * Sp * K;
+      // tap r0 + 2r' of phase row i reads dZ row i + r' + (zh - padd + r0) / 2
+      q.padh = -((zh - padd + q.r0) / 2);
+      q.padw = -((zw - padd + q.s0) / 2);
+      kmax = std::max(kmax, q.Ktot);
+    }
+    a.Ktot = kmax;
+  } else {
+    a.P = H;
+    a.Q = W;
+    a.imask = stride - 1;
+    while ((1 << a.ishift) < stride) ++a.ishift;
+  }
+  a.M = N * a.P * a.Q;
+  a.fd_Q = make_fastdiv(a.Q);
+  a.fd_PQ = make_fastdiv(a.P * a.Q);
   a.Nout = C;
   if (C % 8 || K % 8) return -2;
   a.gm = cdiv(a.M, tile_rows(tile));
@@ -1870,12 +1957,12 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   a.out = a.splits > 1 ? slab : (float*)dx;
   a.outb = (u16*)dx;
   if (add && a.splits > 1 && !reduce) return -4;
-  a.slab = a.splits > 1 ? (long)a.M * C : 0;
+  a.slab = a.splits > 1 ? Mfull * C : 0;
   const int rc = launch_any<XM_DGRAD>(a, tile, np, obf && a.splits == 1, st);
   if (rc) return rc;
-  if (a.splits == 1 && add) return dpa_add_inplace(dx, add, (long)a.M * C, obf, st);
+  if (a.splits == 1 && add) return dpa_add_inplace(dx, add, Mfull * C, obf, st);
   if (a.splits > 1 && reduce) {
-    const long n4 = (long)a.M * C / 4;
+    const long n4 = Mfull * C / 4;
     if (obf) return launch_splitk_reduce_t(slab, (ushort4*)dx, n4, a.splits, st, (const ushort4*)add);
     return launch_splitk_reduce_t(slab, (float4*)dx, n4, a.splits, st, (const float4*)add);
   }

@@ -214,6 +214,35 @@ def test_conv_x3_dgrad(shape, splits, tile, posmajor, np_):
     assert rel_err(dx.permute(0, 3, 1, 2), gx) < (1e-5 if np_ == 3 else 2e-2)
 
 
+@pytest.mark.parametrize("shape", [(4, 16, 16, 32, 64, 1, 2, 0), (4, 14, 14, 32, 64, 3, 2, 1),
+                                   (2, 20, 20, 8, 64, 7, 2, 3), (8, 8, 8, 64, 128, 1, 2, 0)])
+@pytest.mark.parametrize("phase", ["0", "1"])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("tile", [5, 10, 14])
+@pytest.mark.parametrize("np_", [3, 1])
+def test_conv_x3_dgrad_stride2_phases(monkeypatch, shape, phase, splits, tile, np_):
+    """Stride-2 data gradient, phase-decomposed (DPA_DGRAD_PHASE=1: one sub-filter gather per
+    output phase, zero-tap phases stored as zeros) and in the dilated form (=0), both against fp64
+    autograd; bf16 output (one plane) too."""
+    monkeypatch.setenv("DPA_DGRAD_PHASE", phase)
+    C = _C()
+    N, H, W, Cin, K, R, st, pd = shape
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(True)
+    w = torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, w, stride=st, padding=pd)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, dy)
+    dt = torch.bfloat16 if (np_ == 1 and splits == 1) else torch.float32
+    dx = torch.full((N, H, W, Cin), float("nan"), device="cuda", dtype=dt)  # every element is written
+    slab = torch.empty(splits * N * H * W * Cin, device="cuda") if splits > 1 else None
+    C.conv_x3_dgrad(_planes(dy.float().permute(0, 2, 3, 1), np_), _planes(w.float().permute(0, 2, 3, 1), np_), dx,
+                    slab, st, pd, splits, tile, True, False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dx.float()).all()
+    assert rel_err(dx.float().permute(0, 3, 1, 2), gx) < (1e-5 if np_ == 3 else 2e-2)
+
+
 def test_conv_x3_planes_as_arena_views():
     """Weight planes may be strided views of one plane arena (the engine's layout)."""
     C = _C()

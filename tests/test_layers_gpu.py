@@ -373,3 +373,89 @@ def test_resnet_epilogue_bn_stats(monkeypatch, impl):
     for n in (out[0][2] if impl == "x3" else ()):  # bf16: a last-bit statistics change moves the next
         a, b = out[0][2][n], out[1][2][n]             # layer's bf16 input roundings
         assert (a - b).abs().max().item() <= 1e-4 * max(a.abs().max().item(), 1e-6), n
+
+
+@pytest.mark.parametrize("impl", ["x3", "bf16"])
+def test_resnet_bn_dy_pass(monkeypatch, impl):
+    """Add+ReLU BN backward with the dy pass (DPA_BN_DY_PASS=1: the reduce kernel stores
+    dy = relu'(u + r) * (g + g2), which is the residual gradient, and the apply pass reads dy alone)
+    against the apply pass re-reading g, g2 and the mask (=0).  x3: dy is stored in fp32, so the
+    gradients are bitwise equal.  bf16: the apply pass reads the bf16-rounded dy; both paths are
+    compared with the x3 (fp32-grade) gradients, and the dy pass must be no less accurate."""
+    from distributed_pytorch_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    sd = R.ResNet([1, 3, 1, 1], 10, impl=impl).state_dict()
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(8, 64, 64, 3, generator=g).cuda()
+    t = torch.randint(0, 10, (8,), generator=g).cuda()
+
+    def run(impl_, dy_pass):
+        monkeypatch.setenv("DPA_BN_DY_PASS", "1" if dy_pass else "0")
+        m = R.ResNet([1, 3, 1, 1], 10, impl=impl_)
+        m.load_state_dict(sd)
+        m = m.cuda()
+        m(x, t).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().float().clone() for n, p in m.named_parameters()}
+
+    off, on = run(impl, False), run(impl, True)
+    if impl == "x3":
+        for n in off:
+            assert torch.equal(off[n], on[n]), n
+        return
+    ref = run("x3", False)
+    e_off = sorted(rel(off[n], ref[n]) for n in ref)
+    e_on = sorted(rel(on[n], ref[n]) for n in ref)
+    med = len(ref) // 2
+    assert e_on[med] <= 1.25 * e_off[med] + 1e-3, (e_on[med], e_off[med])
+    assert e_on[-1] <= 1.5 * e_off[-1] + 1e-2, (e_on[-1], e_off[-1])
+
+
+def test_resnet_graph_replay_matches_eager():
+    """bench_resnet.py --graph: a whole ResNet training step (forward, autograd backward through the
+    native kernels, DDP hooks, fused SGD) captured once and replayed gives bitwise the parameters of
+    the same number of eager steps."""
+    from distributed_pytorch_amd.models import resnet as R
+    from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel, FlatSGD
+
+    torch.manual_seed(0)
+    sd = R.ResNet([1, 2, 1, 1], 10, impl="bf16").state_dict()
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(16, 64, 64, 3, generator=g).cuda()
+    t = torch.randint(0, 10, (16,), generator=g).cuda()
+    out = []
+    for graph in (False, True):
+        m = R.ResNet([1, 2, 1, 1], 10, impl="bf16")
+        m.load_state_dict(sd)
+        ddp = DistributedDataParallel(m.cuda())
+        opt = FlatSGD(ddp, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        one = torch.ones((), device="cuda")
+
+        def step():
+            opt.zero_grad()
+            loss = ddp(x, t)
+            loss.backward(one)
+            opt.step(ddp.finish())
+            return loss
+
+        if not graph:
+            for _ in range(5):
+                step()
+        else:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    step()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                step()
+            for _ in range(3):
+                gr.replay()
+        torch.cuda.synchronize()
+        out.append(ddp.flat_params.detach().clone())
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1])
