@@ -99,13 +99,20 @@ def main(argv=None):
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = step()
-        graphed = True
+        try:
+            with torch.cuda.graph(graph):
+                static_loss = step()
+            graphed = True
+        except RuntimeError as err:  # capture refused: time the eager step, and say so
+            if a.graph == "on":
+                raise
+            print(f"[bench_resnet] stream capture failed ({err}); timing the eager step", file=sys.stderr, flush=True)
+            torch.cuda.synchronize(dev)
 
-        def timed_step():
-            graph.replay()
-            last["loss"] = static_loss
+        if graphed:
+            def timed_step():
+                graph.replay()
+                last["loss"] = static_loss
 
     el = benchlib.timed_steps(timed_step, a.steps, a.warmup, ctx, dev)  # max over ranks
     loss = last["loss"]

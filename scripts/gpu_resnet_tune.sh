@@ -1,4 +1,4 @@
-# ResNet-50 levers of round 3: kernel/layer tests, conv autotune of the table's missing entries
+# ResNet-50: kernel/layer tests, conv autotune of the table's missing entries
 # (copied to gpurun_out/), then same-box A/Bs of the BN dy pass and of HIP-graph replay.
 set -e
 export TMPDIR=/tmp
