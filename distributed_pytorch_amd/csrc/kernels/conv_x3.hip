@@ -689,6 +689,185 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   }
 }
 
+// ---------------- persistent streaming GEMM: 1x1 / stride-1 forward convolution, bf16 ----------------
+// A 1x1 conv is the GEMM Z[m][n] = sum_k X[m][k] W[n][k] (NHWC rows).  On ResNet-50 its reduction is
+// short (K = 64..2048, 2..64 steps of 32) and its bf16 output large, so conv_x3_kernel's
+// one-tile-per-block schedule runs each block as load -> few MFMA steps -> store with nothing in
+// flight across the phases: 1.7 TB/s and 13 % MFMA busy on the tile-7 calls
+// (profiles/r3_resnet50_pmc_traffic.txt).  Here a grid of at most 2 blocks per CU walks its tiles
+// (b, b + G, ...) as ONE flattened sequence of (tile, k-step) units through a double-buffered LDS
+// pipeline: the next unit's operand loads -- the next tile's first k-step at a tile boundary -- are
+// issued before the current unit's MFMAs and the tile's epilogue stores, so the output stream of one
+// tile overlaps the input stream of the next.  Tile 256x128, 8 waves of 64x64, operand staging, the
+// XOR-swizzled k-contiguous LDS images, fragment reads and the epilogue (with optional BN
+// statistics, epi_col_stats) are conv_x3_kernel's, so results are bitwise those of its tile 7.
+struct SArgs {
+  const u16* x;  // A [M][K] bf16
+  unsigned xbytes;
+  const u16* w;  // B [N][K] bf16 (weights [Nout][1][1][K])
+  unsigned wbytes;
+  u16* out;      // [M][N] bf16
+  int M, N, K;
+  int gm, gn;
+  float2* stats;  // optional: BN (mean, M2) partials, channel-major [N][gm] (epi_col_stats)
+};
+
+// TB (the data gradient of a 1x1 / stride-1 conv, dX[m][c] = sum_k dZ[m][k] W[k][c]): B is read
+// row-contiguous, rows k of W [K][N], kept [k][col] in LDS (64-B segments XOR-swizzled by row & 3)
+// and fetched with ds_read_b64_tr_b16, as conv_x3_kernel's DGRAD B operand.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool TB>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) __attribute__((amdgpu_waves_per_eu(4)))
+void gemm_stream_kernel(SArgs a) {  // <= 128 VGPRs: two 8-wave blocks per CU
+  constexpr int THREADS = WAVES_M * WAVES_N * 64;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int CPR = BK / 8, ROWSTEP = THREADS / CPR;
+  constexpr int NCA = BM / ROWSTEP;
+  constexpr int NCB = TB ? BK * BN / 8 / THREADS : (BN + ROWSTEP - 1) / ROWSTEP;
+  constexpr int BROWSTEP = THREADS / (BN / 8);  // TB: k rows per chunk pass
+  static_assert(BM % ROWSTEP == 0 && THREADS % CPR == 0, "A slot mapping");
+  static_assert(!TB || (BK * BN / 8) % THREADS == 0, "B slot mapping");
+  constexpr int RPB = 16 / CPR;
+  constexpr int A_PLANE = BM * BK, B_PLANE = BN * BK, STAGE = A_PLANE + B_PLANE;
+  auto rswz = [](int row, int col) { return col ^ ((row & 3) << 5); };
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
+  __shared__ float esh[WAVES_M * BN * 3];  // epilogue statistics scratch
+  auto swz = [](int row) { return (row / RPB) & (CPR - 1); };
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WAVES_N, wc = wid % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntile = a.gm * a.gn, G = gridDim.x;
+  const int b = xcd_remap(blockIdx.x, G);  // an XCD's blocks take neighbouring tiles (shared A rows)
+  const int KS = (a.K + BK - 1) / BK;
+  const int U = (b < ntile ? (ntile - 1 - b) / G + 1 : 0) * KS;
+  const __amdgpu_buffer_rsrc_t rx = plane_rsrc(a.x, a.xbytes), rw = plane_rsrc(a.w, a.wbytes);
+  const int r0 = tid / CPR, c8 = (tid % CPR) * 8;
+
+  uint4 ra[NCA], rb[NCB];
+  auto load = [&](int u) {
+    const int t = b + (u / KS) * G, ks = u - (u / KS) * KS;
+    const int m0 = (t / a.gn) * BM, n0 = (t - (t / a.gn) * a.gn) * BN;
+    const int k = ks * BK + c8;
+    const bool kv = k < a.K;
+#pragma unroll
+    for (int j = 0; j < NCA; ++j) {
+      const int m = m0 + r0 + j * ROWSTEP;
+      ra[j] = bload(rx, (long)m * a.K + k, kv && m < a.M);
+    }
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+      if constexpr (TB) {  // W [K][N]: row kr, 8 columns from n0 + bc8
+        const int kr = ks * BK + tid / (BN / 8) + j * BROWSTEP, col = n0 + (tid % (BN / 8)) * 8;
+        rb[j] = bload(rw, (long)kr * a.N + col, kr < a.K && col < a.N);
+      } else {
+        const int n = n0 + r0 + j * ROWSTEP;
+        rb[j] = bload(rw, (long)n * a.K + k, kv && n < a.N && r0 + j * ROWSTEP < BN);
+      }
+    }
+  };
+  auto store = [&](int st) {
+    u16* As = lds + st * STAGE;
+    u16* Bs = As + A_PLANE;
+#pragma unroll
+    for (int j = 0; j < NCA; ++j) {
+      const int row = r0 + j * ROWSTEP;
+      *reinterpret_cast<uint4*>(As + row * BK + (((c8 >> 3) ^ swz(row)) << 3)) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+      if constexpr (TB) {
+        const int kr = tid / (BN / 8) + j * BROWSTEP, col = (tid % (BN / 8)) * 8;
+        *reinterpret_cast<uint4*>(Bs + kr * BN + rswz(kr, col)) = rb[j];
+      } else {
+        const int row = r0 + j * ROWSTEP;
+        if (row < BN) *reinterpret_cast<uint4*>(Bs + row * BK + (((c8 >> 3) ^ swz(row)) << 3)) = rb[j];
+      }
+    }
+  };
+  auto frag = [&](const u16* base, int row, int ks) -> bf16x8 {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + row * BK + (((2 * ks + lh) ^ swz(row)) << 3));
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto frag_t = [&](const u16* base, int col0, int ks) -> bf16x8 {  // [k][col] image, transposed read
+    const int g = lane >> 4, idx = lane & 15;
+    const int q = idx >> 2, p4 = idx & 3;
+    const int col = col0 + 16 * (g & 1) + 4 * p4;
+    const int krow = 16 * ks + 8 * (g >> 1) + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const int scol = rswz(krow, col);  // rows krow and krow + 4 share (row & 3)
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + krow * BN + scol));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (krow + 4) * BN + scol));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x16 acc[TM][TN];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  };
+  auto compute = [&](int st) {
+    const u16* As = lds + st * STAGE;
+    const u16* Bs = As + A_PLANE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[TM][1], fb[TN][1];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i][0] = frag(As, wr * WTM + i * 32 + li, ks);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (TB)
+          fb[j][0] = frag_t(Bs, wc * WTN + j * 32, ks);
+        else
+          fb[j][0] = frag(Bs, wc * WTN + j * 32 + li, ks);
+      }
+      mfma_tile<TM, TN, 1>(acc, fa, fb);
+    }
+  };
+  auto epilogue = [&](int t) {
+    const int bm = t / a.gn, bn = t - (t / a.gn) * a.gn;
+    const int m0 = bm * BM, n0 = bn * BN;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wc * WTN + j * 32 + li;
+        if (col < a.N) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < a.M) a.out[(long)row * a.N + col] = bf16_rne(acc[i][j][r]);
+          }
+        }
+      }
+    if (a.stats != nullptr)
+      epi_col_stats<TM, TN, WAVES_M, WAVES_N, false>(acc, a.M - (m0 + wr * WTM), wr, wc, lane, esh,
+                                                    a.stats + (long)n0 * a.gm, a.gm, bm, a.N - n0);
+  };
+
+  if (U == 0) return;
+  zero();
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int u = 0; u < U; ++u) {
+    if (u + 1 < U) load(u + 1);  // the next unit's operands (the next tile's at a tile boundary)
+    compute(u & 1);
+    if (u % KS == KS - 1) {
+      epilogue(b + (u / KS) * G);
+      zero();
+    }
+    if (u + 1 < U) store((u + 1) & 1);
+    __syncthreads();
+  }
+}
+
 // ---------------- halo-staged direct 3x3 convolution (stride 1, pad 1) ----------------
 // conv_x3_kernel gathers its A operand afresh for every filter tap: each input pixel crosses the
 // L2 -> CU path once per tap and per column tile, and that gather traffic -- not the matrix cores
@@ -1679,6 +1858,36 @@ int run_halo_wgrad(WHArgs& a, int tile, int splits, int np, float* dw, float* sl
 }
 
 
+// ---- streaming GEMM tile (1x1 / stride 1 / pad 0 forward, bf16 in and out, one split): id 30 ----
+bool is_stream(int tile) { return tile == 30; }
+
+// -6: the call does not fit the streaming kernel (it is tuned as a candidate alongside the others)
+int run_stream(const u16* x, const u16* w, void* out, int M, int N, int K, int np, int obf, int splits,
+               float* stats, hipStream_t st, bool dgrad = false) {
+  if (np != 1 || !obf || splits != 1 || K % 8 || N % 8) return -6;
+  SArgs s{};
+  s.x = x;
+  s.w = w;
+  if ((long)M * K * 2 >= (1L << 31) || (long)N * K * 2 >= (1L << 31)) return -5;
+  s.xbytes = (unsigned)((long)M * K * 2);
+  s.wbytes = (unsigned)((long)N * K * 2);
+  s.out = (u16*)out;
+  s.M = M;
+  s.N = N;
+  s.K = K;
+  s.gm = cdiv(M, 256);
+  s.gn = cdiv(N, 128);
+  s.stats = reinterpret_cast<float2*>(stats);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = std::min(s.gm * s.gn, 2 * cus);
+  if (dgrad)
+    gemm_stream_kernel<256, 128, 4, 2, 32, true><<<grid, 512, 0, st>>>(s);
+  else
+    gemm_stream_kernel<256, 128, 4, 2, 32, false><<<grid, 512, 0, st>>>(s);
+  return (int)hipGetLastError();
+}
+
 // ---- position-major tiles (small images): ids 24-29 ----
 //   24 / 25: 256 rows (32 images x 8 positions) x 128, 4x2 waves, 32-channel chunks, <= 12 staged
 //            pixels (4x4 images), weight tiles 1 / 4 steps ahead
@@ -1780,7 +1989,9 @@ extern "C" {
 int dpa_x3_splits(int Kred, int splits) { return xsplits(Kred, splits); }
 
 // rows per row tile of fprop tile `tile` (the stats partial row block), 0 if it cannot emit stats
-int dpa_conv_stats_rows(int tile) { return is_pos(tile) ? 0 : (is_halo(tile) ? halo_bm(tile) : tile_rows(tile)); }
+int dpa_conv_stats_rows(int tile) {
+  return is_pos(tile) ? 0 : (is_stream(tile) ? 256 : (is_halo(tile) ? halo_bm(tile) : tile_rows(tile)));
+}
 
 // x planes [NP][N,H,W,C] (plane stride xps), w planes [NP][Kout][R][S][C] (stride wps; for a data
 // gradient pass the flipped/transposed Wd planes), out fp32 [N,P,Q,Kout] (or slabs, see
@@ -1793,6 +2004,10 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
                       int posmajor, int np, int obf, hipStream_t st, float* stats) {
   if (stats && (is_pos(tile) || (is_halo(tile) ? xsplits(9 * C, splits) : xsplits(R * S * C, splits)) > 1)) return -7;
+  if (is_stream(tile)) {
+    if (R != 1 || S != 1 || stride != 1 || pad != 0) return -6;
+    return run_stream(x, w, out, N * H * W, Kout, C, np, obf, xsplits(C, splits), stats, st);
+  }
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     HArgs h{};
@@ -1863,6 +2078,12 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
 int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx, float* slab, int N, int Hd, int Wd,
                       int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
                       int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig, int sig_val) {
+  if (is_stream(tile)) {  // dX = dZ W for a 1x1 / stride-1 conv (W [K][C] read row-contiguous)
+    if (R != 1 || S != 1 || stride != 1 || pad != 0 || sig) return -6;
+    const int rc = run_stream(dz, w, dx, N * H * W, C, K, np, obf, xsplits(K, splits), nullptr, st, true);
+    if (rc || !add) return rc;
+    return dpa_add_inplace(dx, add, (long)N * H * W * C, obf, st);
+  }
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
     HArgs h{};

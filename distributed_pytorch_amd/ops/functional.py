@@ -102,8 +102,8 @@ def note_use(p: torch.Tensor) -> int:
 # ------------------------------------------------------------------ conv launch configuration
 # Per-call (tile, splits, posmajor): measured table (tuning/generic_mi355x.json, written by the
 # autotuner: ``set_autotune(True)``, e.g. ``bench_resnet.py --autotune``), else a heuristic.
-TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
-                          "generic_mi355x.json")
+TABLE_PATH = os.environ.get("DPA_GENERIC_TABLE") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "generic_mi355x.json")  # env: A/B
 _table: Optional[Dict[str, list]] = None
 _chosen: Dict[str, Tuple[int, int, bool]] = {}
 _AUTOTUNE = {"on": os.environ.get("DPA_AUTOTUNE", "0") == "1", "dirty": False}
@@ -153,6 +153,17 @@ def halo_candidates(kind: str, geom: tuple) -> Tuple[int, ...]:
     return tuple(t for t in HALO_TILES if halo_ok(kind, t, W, cred, cout))
 
 
+STREAM_TILES = (30,)  # conv_x3.hip gemm_stream_kernel: 1x1 / stride 1 / pad 0 fprop + dgrad, bf16, one split
+
+
+def stream_candidates(impl: str, kind: str, geom: tuple) -> Tuple[int, ...]:
+    """The persistent streaming-GEMM tile when it can run this conv call."""
+    N, H, W, C, K, R, S, stride, pad = geom
+    ok = (impl == "bf16" and kind in ("fprop", "dgrad") and (R, S, stride, pad) == (1, 1, 1, 0) and C % 8 == 0
+          and K % 8 == 0)
+    return STREAM_TILES if ok else ()
+
+
 def _autotune(key: str, kind: str, red: int, run: Callable[[int, int, bool], None],
               slab_bytes: Callable[[int], int], extra_tiles: Tuple[int, ...] = ()) -> Tuple[int, int, bool]:
     Kx = _ext.require()
@@ -165,6 +176,8 @@ def _autotune(key: str, kind: str, red: int, run: Callable[[int, int, bool], Non
             s = Kx.x3_splits(red, s0)
             for pm in (False, True):
                 if (tile, s, pm) in seen or slab_bytes(s) > (512 << 20):
+                    continue
+                if tile in STREAM_TILES and (s > 1 or pm):  # one split, NHWC row order only
                     continue
                 seen.add((tile, s, pm))
                 run(tile, s, pm)
@@ -192,7 +205,8 @@ def choose_config(impl: str, kind: str, geom: tuple, M: int, Ngemm: int, Kred: i
     if t is not None:
         c = (int(t[0]), int(t[1]), bool(t[2]))
     elif _AUTOTUNE["on"] and run is not None:
-        c = _autotune(key, kind, M if kind == "wgrad" else Kred, run, slab_bytes, halo_candidates(kind, geom))
+        c = _autotune(key, kind, M if kind == "wgrad" else Kred, run, slab_bytes,
+                      halo_candidates(kind, geom) + stream_candidates(impl, kind, geom))
     else:
         c = conv_config(kind, M, Ngemm, Kred, hw_small)
     _chosen[key] = c

@@ -569,3 +569,56 @@ def test_conv_epilogue_stats_refused_with_split_k():
     slab = torch.empty(4 * out.numel(), device="cuda")
     with pytest.raises(RuntimeError):
         C_.conv_x3_fprop(x3, w3, out, slab, 1, 1, 4, 0, True, 0, torch.empty(2 * 64 * 64, device="cuda"))
+
+
+@pytest.mark.parametrize("shape", [(8, 56, 56, 64, 256), (4, 14, 14, 1024, 256), (2, 7, 7, 2048, 512),
+                                   (3, 9, 11, 40, 72), (1, 3, 3, 512, 2048)])
+@pytest.mark.parametrize("stats", [False, True])
+def test_stream_tile_1x1_fprop(shape, stats):
+    """The persistent streaming GEMM (tile 30, 1x1/s1 bf16 forward): bitwise the output (and BN
+    statistics partials) of the implicit-GEMM tile 7 with the same 256x128 tile and k order, and
+    against fp64 on the bf16-rounded operands."""
+    C = _C()
+    N, H, W, Cin, K = shape
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(N, H, W, Cin, generator=g).bfloat16()
+    w = (torch.randn(K, 1, 1, Cin, generator=g) * 0.1).bfloat16()
+    M = N * H * W
+    outs = {}
+    for tile in (7, 30):
+        out = torch.full((N, H, W, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+        st = torch.zeros(2 * (-(-M // 256)) * K, device="cuda") if stats else None
+        C.conv_x3_fprop(x.cuda().unsqueeze(0), w.cuda().unsqueeze(0), out, None, 1, 0, 1, tile, True, False, st)
+        torch.cuda.synchronize()
+        outs[tile] = (out.cpu(), st.cpu() if st is not None else None)
+    assert torch.equal(outs[7][0], outs[30][0])
+    if stats:
+        assert torch.equal(outs[7][1], outs[30][1])
+    ref = (x.double().reshape(M, Cin) @ w.double().reshape(K, Cin).t()).reshape(N, H, W, K)
+    assert rel_err(outs[30][0].float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(8, 56, 56, 256, 64), (4, 14, 14, 256, 1024), (2, 7, 7, 512, 2048),
+                                   (3, 9, 11, 72, 40)])
+@pytest.mark.parametrize("add", [False, True])
+def test_stream_tile_1x1_dgrad(shape, add):
+    """Tile 30 as the data gradient of a 1x1/s1 conv (W read row-contiguous, transposed LDS reads):
+    bitwise the implicit-GEMM tile 7 DGRAD, against fp64, and with a folded second contribution."""
+    C = _C()
+    N, H, W, Cin, K = shape  # forward conv Cin -> K; the data gradient maps dZ [.., K] to dX [.., Cin]
+    g = torch.Generator().manual_seed(43)
+    dz = torch.randn(N, H, W, K, generator=g).bfloat16()
+    w = (torch.randn(K, 1, 1, Cin, generator=g) * 0.1).bfloat16()
+    extra = torch.randn(N, H, W, Cin, generator=g).bfloat16()
+    outs = {}
+    for tile in (7, 30):
+        dx = torch.full((N, H, W, Cin), float("nan"), device="cuda", dtype=torch.bfloat16)
+        C.conv_x3_dgrad(dz.cuda().unsqueeze(0), w.cuda().unsqueeze(0), dx, None, 1, 0, 1, tile, True, False,
+                        extra.cuda() if add else None)
+        torch.cuda.synchronize()
+        outs[tile] = dx.cpu()
+    assert torch.equal(outs[7], outs[30])
+    ref = (dz.double().reshape(-1, K) @ w.double().reshape(K, Cin)).reshape(N, H, W, Cin)
+    if add:
+        ref = ref + extra.double()
+    assert rel_err(outs[30].float(), ref) < 1e-2
