@@ -715,7 +715,7 @@ struct SArgs {
 // TB (the data gradient of a 1x1 / stride-1 conv, dX[m][c] = sum_k dZ[m][k] W[k][c]): B is read
 // row-contiguous, rows k of W [K][N], kept [k][col] in LDS (64-B segments XOR-swizzled by row & 3)
 // and fetched with ds_read_b64_tr_b16, as conv_x3_kernel's DGRAD B operand.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool TB>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool TB, bool SEPI = true>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) __attribute__((amdgpu_waves_per_eu(4)))
 void gemm_stream_kernel(SArgs a) {  // <= 128 VGPRs: two 8-wave blocks per CU
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
@@ -830,22 +830,43 @@ void gemm_stream_kernel(SArgs a) {  // <= 128 VGPRs: two 8-wave blocks per CU
       mfma_tile<TM, TN, 1>(acc, fa, fb);
     }
   };
+  // Tile stores through LDS: per 32-row slice of its 64x64 wave tile, a wave writes its bf16 values
+  // into its own 4 KB region and reads them back as 16-byte row pieces, so each global store moves
+  // 16 B per lane (128-B row segments) instead of 2 B.  Called after a block barrier: both operand
+  // stages are free (the next unit's operands are still in registers).
+  static_assert(WTN == 64 && WAVES_M * WAVES_N * 32 * WTN * 2 <= 2 * STAGE * 2, "epilogue staging");
   auto epilogue = [&](int t) {
     const int bm = t / a.gn, bn = t - (t / a.gn) * a.gn;
     const int m0 = bm * BM, n0 = bn * BN;
+    if constexpr (!SEPI) {  // direct 2-byte stores (A/B: DPA_STREAM_EPI=0)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wc * WTN + j * 32 + li;
-        if (col < a.N) {
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wc * WTN + j * 32 + li;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (row < a.M) a.out[(long)row * a.N + col] = bf16_rne(acc[i][j][r]);
+            if (row < a.M && col < a.N) a.out[(long)row * a.N + col] = bf16_rne(acc[i][j][r]);
           }
         }
+    }
+    u16* ws = lds + wid * 32 * WTN;
+#pragma unroll
+    for (int i = 0; i < (SEPI ? TM : 0); ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ws[((r & 3) + 8 * (r >> 2) + 4 * lh) * WTN + j * 32 + li] = bf16_rne(acc[i][j][r]);
+#pragma unroll
+      for (int c = 0; c < 32 * WTN / 8 / 64; ++c) {
+        const int q = lane + 64 * c, rr = q / (WTN / 8), cc = q - rr * (WTN / 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(ws + rr * WTN + cc * 8);
+        const int row = m0 + wr * WTM + i * 32 + rr, col = n0 + wc * WTN + cc * 8;
+        if (row < a.M && col < a.N) *reinterpret_cast<uint4*>(a.out + (long)row * a.N + col) = v;
       }
+    }
     if (a.stats != nullptr)
       epi_col_stats<TM, TN, WAVES_M, WAVES_N, false>(acc, a.M - (m0 + wr * WTM), wr, wc, lane, esh,
                                                     a.stats + (long)n0 * a.gm, a.gm, bm, a.N - n0);
@@ -860,8 +881,10 @@ void gemm_stream_kernel(SArgs a) {  // <= 128 VGPRs: two 8-wave blocks per CU
     if (u + 1 < U) load(u + 1);  // the next unit's operands (the next tile's at a tile boundary)
     compute(u & 1);
     if (u % KS == KS - 1) {
+      __syncthreads();  // both LDS stages free for the epilogue's staging
       epilogue(b + (u / KS) * G);
       zero();
+      __syncthreads();
     }
     if (u + 1 < U) store((u + 1) & 1);
     __syncthreads();
@@ -1881,10 +1904,15 @@ int run_stream(const u16* x, const u16* w, void* out, int M, int N, int K, int n
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::min(s.gm * s.gn, 2 * cus);
-  if (dgrad)
-    gemm_stream_kernel<256, 128, 4, 2, 32, true><<<grid, 512, 0, st>>>(s);
-  else
-    gemm_stream_kernel<256, 128, 4, 2, 32, false><<<grid, 512, 0, st>>>(s);
+  const char* ee = getenv("DPA_STREAM_EPI");  // A/B: 0 = direct 2-byte epilogue stores
+  const bool sepi = !(ee && ee[0] == '0');
+  if (dgrad) {
+    if (sepi) gemm_stream_kernel<256, 128, 4, 2, 32, true><<<grid, 512, 0, st>>>(s);
+    else gemm_stream_kernel<256, 128, 4, 2, 32, true, false><<<grid, 512, 0, st>>>(s);
+  } else {
+    if (sepi) gemm_stream_kernel<256, 128, 4, 2, 32, false><<<grid, 512, 0, st>>>(s);
+    else gemm_stream_kernel<256, 128, 4, 2, 32, false, false><<<grid, 512, 0, st>>>(s);
+  }
   return (int)hipGetLastError();
 }
 
