@@ -90,6 +90,7 @@ struct Args {
   // of 1 tap, three of 0; 3x3/s2: 1 + 2 + 2 + 4 taps) instead of the dilated form's 4x MFMA work
   // on zeros.  Rows m of a phase are (img, i, j) of the H/2 x W/2 phase grid (P, Q, M), stored at
   // dx pixel (img, 2i + ph, 2j + pw) of the outH x outW output.
+  int sepi;  // OB outputs: 1 = stores staged through LDS as 16-byte row pieces (DPA_OB_EPI)
   int nph, outH, outW;
   struct Phase {
     int Ktot, S, r0, s0, padh, padw;
@@ -653,34 +654,69 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   const int ncols = WG ? a.Ktot : a.Nout;
   const bool remap = !WG && a.posmajor;
   const int PQ = a.P * a.Q;
+  auto mrow_of = [&](int row) -> long {
+    long mrow = row;
+    if (remap) {
+      const unsigned pos = fdiv((unsigned)row, a.fd_N);
+      mrow = (long)(row - (int)pos * a.N) * PQ + pos;
+    }
+    if (DG && a.nph > 1) {  // phase grid row -> dx pixel
+      const unsigned img = fdiv((unsigned)row, a.fd_PQ), pos = (unsigned)row - img * (unsigned)PQ;
+      const unsigned i = fdiv(pos, a.fd_Q), j = pos - i * (unsigned)a.Q;
+      mrow = ((long)img * a.outH + 2 * (int)i + ph) * a.outW + 2 * (int)j + pw;
+    }
+    return mrow;
+  };
+  bool staged = false;
+  if constexpr (OB) {
+    // bf16 output through LDS (as gemm_stream_kernel): per 16-row slice of its wave tile a wave writes
+    // its values into its own region and stores them as 16-byte row pieces instead of 2-byte values
+    constexpr int SR = 16;
+    static_assert(WAVES_M * WAVES_N * SR * WTN <= (int)(sizeof(lds) / sizeof(u16)), "OB epilogue staging");
+    if (a.sepi) {
+      staged = true;
+      __syncthreads();  // every wave is done with the main loop's LDS
+      u16* ws = lds + wid * SR * WTN;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wc * WTN + j * 32 + li;
-      if (col < ncols) {
+        for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < nrows) {
-            long mrow = row;
-            if (remap) {
-              const unsigned pos = fdiv((unsigned)row, a.fd_N);
-              mrow = (long)(row - (int)pos * a.N) * PQ + pos;
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 8 * h; r < 8 * h + 8; ++r)
+              ws[((r & 3) + 8 * ((r >> 2) - 2 * h) + 4 * lh) * WTN + j * 32 + li] = bf16_rne(acc[i][j][r]);
+#pragma unroll
+          for (int c = 0; c < SR * WTN / 8 / 64; ++c) {
+            const int q = lane + 64 * c, rr = q / (WTN / 8), cc = q - rr * (WTN / 8);
+            const uint4 v = *reinterpret_cast<const uint4*>(ws + rr * WTN + cc * 8);
+            const int row = m0 + wr * WTM + i * 32 + SR * h + rr, col = n0 + wc * WTN + cc * 8;
+            if (row < nrows && col < ncols) *reinterpret_cast<uint4*>(a.outb + mrow_of(row) * ldc + col) = v;
+          }
+        }
+    }
+  }
+  if (!staged) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wc * WTN + j * 32 + li;
+        if (col < ncols) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < nrows) {
+              const long mrow = mrow_of(row);
+              if constexpr (OB)
+                a.outb[mrow * ldc + col] = bf16_rne(acc[i][j][r]);
+              else
+                out[mrow * ldc + col] = acc[i][j][r];
             }
-            if (DG && a.nph > 1) {  // phase grid row -> dx pixel
-              const unsigned img = fdiv((unsigned)row, a.fd_PQ), pos = (unsigned)row - img * (unsigned)PQ;
-              const unsigned i = fdiv(pos, a.fd_Q), j = pos - i * (unsigned)a.Q;
-              mrow = ((long)img * a.outH + 2 * (int)i + ph) * a.outW + 2 * (int)j + pw;
-            }
-            if constexpr (OB)
-              a.outb[mrow * ldc + col] = bf16_rne(acc[i][j][r]);
-            else
-              out[mrow * ldc + col] = acc[i][j][r];
           }
         }
       }
-    }
+  }
   if constexpr (MODE == XM_FPROP) {
     if (a.stats != nullptr)
       epi_col_stats<TM, TN, WAVES_M, WAVES_N, false>(acc, a.M - (m0 + wr * WTM), wr, wc, lane,
@@ -1738,6 +1774,11 @@ int launch_any(const Args& a, int tile, int np, int obf, hipStream_t st) {
   if (obf) return launch_tile<MODE, 1, true>(a, tile, st);
   return np == 3 ? launch_tile<MODE, 3>(a, tile, st) : launch_tile<MODE, 1>(a, tile, st);
 }
+// bf16-output epilogue through LDS (conv_x3_kernel OB); DPA_OB_EPI=0: direct 2-byte stores (A/B)
+int ob_epi() {
+  const char* e = getenv("DPA_OB_EPI");
+  return (e && e[0] == '0') ? 0 : 1;
+}
 bool small_tile(int tile) { return tile == 1 || tile == 3 || tile == 6 || tile == 11 || tile == 15; }
 int tile_rows(int tile) { return small_tile(tile) ? 64 : ((tile == 7 || tile == 10 || tile == 14) ? 256 : 128); }
 int tile_cols(int tile) { return small_tile(tile) ? 64 : 128; }
@@ -2082,6 +2123,7 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   a.posmajor = posmajor & 1;
   a.nmajor = (posmajor >> 1) & 1;
   a.stats = reinterpret_cast<float2*>(stats);
+  a.sepi = ob_epi();
   if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;
@@ -2202,6 +2244,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   a.splits = xsplits(a.Ktot, splits);
   a.posmajor = posmajor & 1;
   a.nmajor = (posmajor >> 1) & 1;
+  a.sepi = ob_epi();
   if (obf && np != 1) return -4;
   a.out = a.splits > 1 ? slab : (float*)dx;
   a.outb = (u16*)dx;
