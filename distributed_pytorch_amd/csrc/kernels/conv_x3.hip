@@ -957,6 +957,7 @@ struct HArgs {
   int* sig;                 // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
   float2* stats;            // FPROP, one split: per (row tile, output channel) BN (mean, M2)
+  int sepi;                 // OB: stores staged through LDS (DPA_OB_EPI)
 };
 
 // staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
@@ -1178,24 +1179,53 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
 
   // ---------------- epilogue (rows are NHWC pixels) ----------------
   float* out = a.out + (long)blockIdx.y * a.slab;
+  bool staged = false;
+  if constexpr (OB) {  // bf16 output staged through LDS as 16-byte row pieces (conv_x3_kernel's OB path)
+    constexpr int SR = 16;
+    static_assert(WAVES_M * WAVES_N * SR * WTN <= (int)(sizeof(lds) / sizeof(u16)), "OB epilogue staging");
+    if (a.sepi) {
+      staged = true;
+      __syncthreads();  // every wave is done with the main loop's LDS
+      u16* ws = lds + wid * SR * WTN;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wc * WTN + j * 32 + li;
-      if (col < a.Nout) {
+        for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < a.M) {
-            if constexpr (OB)
-              a.outb[(long)row * a.Nout + col] = bf16_rne(acc[i][j][r]);
-            else
-              out[(long)row * a.Nout + col] = acc[i][j][r];
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 8 * h; r < 8 * h + 8; ++r)
+              ws[((r & 3) + 8 * ((r >> 2) - 2 * h) + 4 * lh) * WTN + j * 32 + li] = bf16_rne(acc[i][j][r]);
+#pragma unroll
+          for (int c = 0; c < SR * WTN / 8 / 64; ++c) {
+            const int q = lane + 64 * c, rr = q / (WTN / 8), cc = q - rr * (WTN / 8);
+            const uint4 v = *reinterpret_cast<const uint4*>(ws + rr * WTN + cc * 8);
+            const int row = m0 + wr * WTM + i * 32 + SR * h + rr, col = n0 + wc * WTN + cc * 8;
+            if (row < a.M && col < a.Nout) *reinterpret_cast<uint4*>(a.outb + (long)row * a.Nout + col) = v;
+          }
+        }
+    }
+  }
+  if (!staged) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wc * WTN + j * 32 + li;
+        if (col < a.Nout) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wr * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < a.M) {
+              if constexpr (OB)
+                a.outb[(long)row * a.Nout + col] = bf16_rne(acc[i][j][r]);
+              else
+                out[(long)row * a.Nout + col] = acc[i][j][r];
+            }
           }
         }
       }
-    }
+  }
   if constexpr (!DG) {
     if (a.stats != nullptr)
       epi_col_stats<TM, TN, WAVES_M, WAVES_N, false>(acc, a.M - (m0 + wr * WTM), wr, wc, lane,
@@ -1864,6 +1894,7 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
   a.M = a.N * a.H * a.W;
   a.gm = cdiv(a.M, BM);
   a.gn = cdiv(a.Nout, halo_bn(tile));
+  a.sepi = ob_epi();
   a.cps = cdiv(a.C / BC, splits);
   a.out = splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;
