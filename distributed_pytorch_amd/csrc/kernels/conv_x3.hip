@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);  // sgd.hip
 
@@ -227,6 +228,42 @@ __device__ __forceinline__ void epi_col_stats(const f32x16 (&acc)[TM][TN], int r
     }
     if (c < ncols) part[(long)c * nblk + bm] = make_float2(w.mean, w.m2);
   }
+}
+
+// Epilogue stores staged through LDS: a wave writes SR rows x WTN columns of its accumulators (as T:
+// bf16 bits or fp32) into its own LDS region `ws`, reads them back as 16-byte row pieces and hands each
+// piece to store(row_in_wave_tile, col_in_wave_tile, piece).  Slices of SR rows (8 or 16) of every
+// 32-row sub-tile, in order.  Wave-local: the caller barriers once before (main-loop LDS reuse).
+template <int TM, int TN, int WTN, int SR, typename T, typename Store>
+__device__ __forceinline__ void staged_store(const f32x16 (&acc)[TM][TN], T* ws, int lane, Store store) {
+  constexpr int EPC = 16 / sizeof(T);  // elements per 16-byte piece
+  constexpr int PPR = WTN / EPC;       // pieces per row
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int s = 0; s < 32 / SR; ++s) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if ((r >> 2) / (SR / 8) == s) {  // compile-time: accumulator r holds a row of slice s
+            const int lrow = (r & 3) + 8 * ((r >> 2) - s * (SR / 8)) + 4 * lh;
+            if constexpr (sizeof(T) == 2)
+              ws[lrow * WTN + j * 32 + li] = bf16_rne(acc[i][j][r]);
+            else
+              ws[lrow * WTN + j * 32 + li] = acc[i][j][r];
+          }
+        }
+#pragma unroll
+      for (int c = 0; c < (SR * PPR + 63) / 64; ++c) {
+        const int q = lane + 64 * c;
+        if (SR * PPR % 64 == 0 || q < SR * PPR) {
+          const int rr = q / PPR, pc = q - rr * PPR;
+          store(i * 32 + s * SR + rr, pc * EPC, *reinterpret_cast<const uint4*>(ws + rr * WTN + pc * EPC));
+        }
+      }
+    }
 }
 
 // BK: reduction depth per LDS stage (16/32/64 = 1/2/4 MFMA k-steps).  LDS image layouts: see the
@@ -668,32 +705,30 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
     return mrow;
   };
   bool staged = false;
-  if constexpr (OB) {
-    // bf16 output through LDS (as gemm_stream_kernel): per 16-row slice of its wave tile a wave writes
-    // its values into its own region and stores them as 16-byte row pieces instead of 2-byte values
-    constexpr int SR = 16;
-    static_assert(WAVES_M * WAVES_N * SR * WTN <= (int)(sizeof(lds) / sizeof(u16)), "OB epilogue staging");
-    if (a.sepi) {
-      staged = true;
-      __syncthreads();  // every wave is done with the main loop's LDS
-      u16* ws = lds + wid * SR * WTN;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 8 * h; r < 8 * h + 8; ++r)
-              ws[((r & 3) + 8 * ((r >> 2) - 2 * h) + 4 * lh) * WTN + j * 32 + li] = bf16_rne(acc[i][j][r]);
-#pragma unroll
-          for (int c = 0; c < SR * WTN / 8 / 64; ++c) {
-            const int q = lane + 64 * c, rr = q / (WTN / 8), cc = q - rr * (WTN / 8);
-            const uint4 v = *reinterpret_cast<const uint4*>(ws + rr * WTN + cc * 8);
-            const int row = m0 + wr * WTM + i * 32 + SR * h + rr, col = n0 + wc * WTN + cc * 8;
-            if (row < nrows && col < ncols) *reinterpret_cast<uint4*>(a.outb + mrow_of(row) * ldc + col) = v;
+  {
+    // outputs through LDS as 16-byte row pieces (as gemm_stream_kernel): bf16 (OB) or fp32, slices
+    // of 16 rows when the main loop's LDS holds them for every wave, else 8 (DPA_OB_EPI=0: direct)
+    typedef typename std::conditional<OB, u16, float>::type TO;
+    constexpr int LDSE = (int)(sizeof(lds) / sizeof(TO));
+    // (not the fp32-output data gradient: its phase / dilation epilogue would spill)
+    constexpr int SR = (DG && !OB) ? 0
+                       : (WAVES_M * WAVES_N * 16 * WTN <= LDSE ? 16 : (WAVES_M * WAVES_N * 8 * WTN <= LDSE ? 8 : 0));
+    if constexpr (SR > 0) {
+      if (a.sepi) {
+        staged = true;
+        __syncthreads();  // every wave is done with the main loop's LDS
+        TO* ws = reinterpret_cast<TO*>(lds) + wid * SR * WTN;
+        const int rb = m0 + wr * WTM, cb = n0 + wc * WTN;
+        staged_store<TM, TN, WTN, SR, TO>(acc, ws, lane, [&](int r, int c, uint4 v) {
+          const int row = rb + r, col = cb + c;
+          if (row < nrows && col < ncols) {
+            if constexpr (OB)
+              *reinterpret_cast<uint4*>(a.outb + mrow_of(row) * ldc + col) = v;
+            else
+              *reinterpret_cast<uint4*>(out + mrow_of(row) * ldc + col) = v;
           }
-        }
+        });
+      }
     }
   }
   if (!staged) {
@@ -1180,30 +1215,26 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   // ---------------- epilogue (rows are NHWC pixels) ----------------
   float* out = a.out + (long)blockIdx.y * a.slab;
   bool staged = false;
-  if constexpr (OB) {  // bf16 output staged through LDS as 16-byte row pieces (conv_x3_kernel's OB path)
-    constexpr int SR = 16;
-    static_assert(WAVES_M * WAVES_N * SR * WTN <= (int)(sizeof(lds) / sizeof(u16)), "OB epilogue staging");
-    if (a.sepi) {
-      staged = true;
-      __syncthreads();  // every wave is done with the main loop's LDS
-      u16* ws = lds + wid * SR * WTN;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 8 * h; r < 8 * h + 8; ++r)
-              ws[((r & 3) + 8 * ((r >> 2) - 2 * h) + 4 * lh) * WTN + j * 32 + li] = bf16_rne(acc[i][j][r]);
-#pragma unroll
-          for (int c = 0; c < SR * WTN / 8 / 64; ++c) {
-            const int q = lane + 64 * c, rr = q / (WTN / 8), cc = q - rr * (WTN / 8);
-            const uint4 v = *reinterpret_cast<const uint4*>(ws + rr * WTN + cc * 8);
-            const int row = m0 + wr * WTM + i * 32 + SR * h + rr, col = n0 + wc * WTN + cc * 8;
-            if (row < a.M && col < a.Nout) *reinterpret_cast<uint4*>(a.outb + (long)row * a.Nout + col) = v;
+  {  // outputs through LDS as 16-byte row pieces (conv_x3_kernel's epilogue)
+    typedef typename std::conditional<OB, u16, float>::type TO;
+    constexpr int LDSE = (int)(sizeof(lds) / sizeof(TO));
+    constexpr int SR = WAVES_M * WAVES_N * 16 * WTN <= LDSE ? 16 : (WAVES_M * WAVES_N * 8 * WTN <= LDSE ? 8 : 0);
+    if constexpr (SR > 0) {
+      if (a.sepi) {
+        staged = true;
+        __syncthreads();  // every wave is done with the main loop's LDS
+        TO* ws = reinterpret_cast<TO*>(lds) + wid * SR * WTN;
+        const int rb = m0 + wr * WTM, cb = n0 + wc * WTN;
+        staged_store<TM, TN, WTN, SR, TO>(acc, ws, lane, [&](int r, int c, uint4 v) {
+          const int row = rb + r, col = cb + c;
+          if (row < a.M && col < a.Nout) {
+            if constexpr (OB)
+              *reinterpret_cast<uint4*>(a.outb + (long)row * a.Nout + col) = v;
+            else
+              *reinterpret_cast<uint4*>(out + (long)row * a.Nout + col) = v;
           }
-        }
+        });
+      }
     }
   }
   if (!staged) {
@@ -2326,6 +2357,7 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   a.nmajor = (posmajor >> 1) & 1;
   a.out = a.splits > 1 ? slab : dw;
   a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
+  a.sepi = ob_epi();
   const int rc = np == 3 ? launch_tile<XM_WGRAD, 3>(a, tile, st) : launch_tile<XM_WGRAD, 1>(a, tile, st);
   if (rc) return rc;
   if (a.splits > 1) {
