@@ -28,6 +28,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -45,6 +46,17 @@ constexpr int RT = 1024;  // forward-statistics block size
 // grid size (A/B switches).
 constexpr int RTB = 256;
 constexpr int BWD_BLOCKS = 512;
+// Four bf16 rows' loads in flight per thread in the apply passes and the wide reduce (DPA_BN_UNROLL=0:
+// one / two rows, as before; A/B: ResNet-50 +0.6 %).  Set once from the host before the first launch.
+__constant__ int g_bn_unr = 1;
+inline void bn_unroll_init() {
+  static const bool done = [] {
+    const char* e = std::getenv("DPA_BN_UNROLL");
+    const int v = (e && e[0] == '0') ? 0 : 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_bn_unr), &v, sizeof(int)) == hipSuccess;
+  }();
+  (void)done;
+}
 constexpr long WIDE_MIN_F4 = 3L << 20;
 inline int bwd_force() {
   static const int f = [] {
@@ -431,7 +443,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
     const int c4 = (int)(i0 % C4);
     const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
     const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
-    for (long i = i0; i < total; i += stride) body(i, c4, sc, sh);
+    long i = i0;
+    // four rows' loads in flight per thread (memory-level parallelism of the bf16 passes)
+    if (sizeof(TZ) == 2 && g_bn_unr)  // bf16 rows (8 bytes per thread); fp32 as before
+    for (; i + 3 * stride < total; i += 4 * stride) {
+      body(i, c4, sc, sh);
+      body(i + stride, c4, sc, sh);
+      body(i + 2 * stride, c4, sc, sh);
+      body(i + 3 * stride, c4, sc, sh);
+    }
+    for (; i < total; i += stride) body(i, c4, sc, sh);
   } else {
     for (long i = i0; i < total; i += stride) {
       const int c4 = (int)(i % C4);
@@ -507,44 +528,47 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
       const float4 mu = reinterpret_cast<const float4*>(mean)[c4];
       const float4 is = reinterpret_cast<const float4*>(invstd)[c4];
       int r = r0 + lane_r;
-      // two rows' loads in flight: the 1024-thread geometry of large tensors (ResNet-50, +6 %);
-      // the 256-thread blocks that run beside the VGG weight-gradient convs keep one row
-      if (RTB == RT && !POOL && nsplit == 1) {
-        for (; r + gg.RPI < r1; r += 2 * gg.RPI) {
-          const long gi0 = (long)r * gg.C4 + c4, gi1 = gi0 + (long)gg.RPI * gg.C4;
-          float4 g0 = ld4(gsrc, gi0), g1 = ld4(gsrc, gi1);
-          if (g2) {
-            g0 = f4add(g0, ld4(g2, gi0));
-            g1 = f4add(g1, ld4(g2, gi1));
-          }
-          const float4 z0 = ld4(z, gi0), z1 = ld4(z, gi1);
+      // UNR rows' loads in flight: the 1024-thread geometry of large tensors (ResNet-50; two rows
+      // +6 %, four for 8-byte bf16 rows); the 256-thread blocks that run beside the VGG
+      // weight-gradient convs keep one row.  Rows are summed in order (deterministic).
+      auto rows = [&](auto unr) {
+        constexpr int UNR = decltype(unr)::value;
+        for (; r + (UNR - 1) * gg.RPI < r1; r += UNR * gg.RPI) {
+          long gi[UNR];
+          float4 gv[UNR], zv[UNR], rv[UNR];
+          unsigned mv[UNR];
           const bool mk = ACT == 2 && mask;
-          const float4 r0v = ACT == 2 && !mk ? ld4(res, gi0) : make_float4(0.f, 0.f, 0.f, 0.f);
-          const float4 r1v = ACT == 2 && !mk ? ld4(res, gi1) : make_float4(0.f, 0.f, 0.f, 0.f);
-          const unsigned m0 = mk ? mask[gi0] : 0u, m1 = mk ? mask[gi1] : 0u;
-          float dy0[4], dy1[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float za = F4GET(z0, k), zb = F4GET(z1, k);
-            const float dya = mk ? (((m0 >> k) & 1u) ? F4GET(g0, k) : 0.f)
-                                 : act_grad<ACT>(fmaf(za, F4GET(sc, k), F4GET(sh, k)), F4GET(r0v, k), F4GET(g0, k));
-            const float dyb = mk ? (((m1 >> k) & 1u) ? F4GET(g1, k) : 0.f)
-                                 : act_grad<ACT>(fmaf(zb, F4GET(sc, k), F4GET(sh, k)), F4GET(r1v, k), F4GET(g1, k));
-            const float xa = (za - F4GET(mu, k)) * F4GET(is, k), xb = (zb - F4GET(mu, k)) * F4GET(is, k);
-            sdy[k] += dya;
-            sdx[k] = fmaf(dya, xa, sdx[k]);
-            sx[k] += xa;
-            sdy[k] += dyb;
-            sdx[k] = fmaf(dyb, xb, sdx[k]);
-            sx[k] += xb;
-            dy0[k] = dya;
-            dy1[k] = dyb;
+          for (int u = 0; u < UNR; ++u) {
+            gi[u] = (long)(r + u * gg.RPI) * gg.C4 + c4;
+            gv[u] = ld4(gsrc, gi[u]);
+            if (g2) gv[u] = f4add(gv[u], ld4(g2, gi[u]));
+            zv[u] = ld4(z, gi[u]);
+            rv[u] = ACT == 2 && !mk ? ld4(res, gi[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            mv[u] = mk ? mask[gi[u]] : 0u;
           }
-          if (ACT == 2 && dyout) {
-            st4(dyout, gi0, make_float4(dy0[0], dy0[1], dy0[2], dy0[3]));
-            st4(dyout, gi1, make_float4(dy1[0], dy1[1], dy1[2], dy1[3]));
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            float dyu[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float zz = F4GET(zv[u], k);
+              const float dy = mk ? (((mv[u] >> k) & 1u) ? F4GET(gv[u], k) : 0.f)
+                                  : act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv[u], k),
+                                                  F4GET(gv[u], k));
+              const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
+              sdy[k] += dy;
+              sdx[k] = fmaf(dy, xh, sdx[k]);
+              sx[k] += xh;
+              dyu[k] = dy;
+            }
+            if (ACT == 2 && dyout) st4(dyout, gi[u], make_float4(dyu[0], dyu[1], dyu[2], dyu[3]));
           }
         }
+      };
+      if (RTB == RT && !POOL && nsplit == 1) {
+        if (sizeof(TZ) == 2 && g_bn_unr) rows(std::integral_constant<int, 4>());
+        rows(std::integral_constant<int, 2>());
       }
       for (; r < r1; r += gg.RPI) {
         const long gi = (long)r * gg.C4 + c4;
@@ -745,7 +769,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
   if (stride % C4 == 0) {  // every element of this thread has the same channel group (launcher's grid)
     const int c4 = (int)(i0 % C4);
     const Co q = coefs(c4);
-    for (long i = i0; i < total; i += stride) body(i, c4, q);
+    long i = i0;
+    if (sizeof(TZ) == 2 && g_bn_unr)  // bf16 rows (8 bytes per thread); fp32 as before
+    for (; i + 3 * stride < total; i += 4 * stride) {  // four rows' loads in flight per thread
+      body(i, c4, q);
+      body(i + stride, c4, q);
+      body(i + 2 * stride, c4, q);
+      body(i + 3 * stride, c4, q);
+    }
+    for (; i < total; i += stride) body(i, c4, q);
   } else {
     for (long i = i0; i < total; i += stride) {
       const int c4 = (int)(i % C4);
@@ -1114,6 +1146,7 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
 // 1 none, 2 relu(. + res).  zbf: z and res are bf16.
 int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
                  int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st, unsigned char* mask) {
+  bn_unroll_init();
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && !res)) return -2;
   if (mask && act != 2) return -2;
   if (zbf)
@@ -1132,6 +1165,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2,
                const unsigned char* mask) {
+  bn_unroll_init();
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && ((!res && !mask) || !dres))) return -2;
   if (mask && act != 2) return -2;
   if (zbf && nsplit > 1) return -2;
@@ -1153,6 +1187,7 @@ int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, c
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
                       float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val) {
+  bn_unroll_init();
   if (nsplit < 1) nsplit = 1;
   if (CP < 3) return -2;
   bn_bwd_stats<float>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, 32,
