@@ -180,7 +180,10 @@ def _autotune(key: str, kind: str, red: int, run: Callable[[int, int, bool], Non
                 if tile in STREAM_TILES and (s > 1 or pm):  # one split, NHWC row order only
                     continue
                 seen.add((tile, s, pm))
-                run(tile, s, pm)
+                try:
+                    run(tile, s, pm)
+                except RuntimeError:  # the tile refuses this call (shape / size limits): not a candidate
+                    continue
                 ev0.record()
                 for _ in range(3):
                     run(tile, s, pm)
