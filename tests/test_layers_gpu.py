@@ -459,3 +459,30 @@ def test_resnet_graph_replay_matches_eager():
         out.append(ddp.flat_params.detach().clone())
     assert torch.isfinite(out[0]).all()
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("impl", ["x3", "bf16"])
+def test_resnet_staged_epilogue_bitwise(monkeypatch, impl):
+    """Conv epilogues staged through LDS (DPA_OB_EPI=1: 16-byte row stores of bf16 / fp32 outputs and
+    split-K slabs) store exactly the values the direct 2/4-byte stores do: a ResNet step's loss and
+    every gradient are bitwise equal."""
+    from distributed_pytorch_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    sd = R.ResNet([1, 2, 1, 1], 10, impl=impl).state_dict()
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(8, 64, 64, 3, generator=g).cuda()
+    t = torch.randint(0, 10, (8,), generator=g).cuda()
+    out = []
+    for epi in ("0", "1"):
+        monkeypatch.setenv("DPA_OB_EPI", epi)
+        m = R.ResNet([1, 2, 1, 1], 10, impl=impl)
+        m.load_state_dict(sd)
+        m = m.cuda()
+        loss = m(x, t)
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((loss.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    assert torch.equal(out[0][0], out[1][0])
+    for n in out[0][1]:
+        assert torch.equal(out[0][1][n], out[1][1][n]), n
