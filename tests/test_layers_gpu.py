@@ -463,8 +463,8 @@ def test_resnet_graph_replay_matches_eager():
 
 @pytest.mark.parametrize("impl", ["x3", "bf16"])
 def test_resnet_staged_epilogue_bitwise(monkeypatch, impl):
-    """Conv epilogues staged through LDS (DPA_OB_EPI=1: 16-byte row stores of bf16 / fp32 outputs and
-    split-K slabs) store exactly the values the direct 2/4-byte stores do: a ResNet step's loss and
+    """Conv epilogues staged through LDS (DPA_OB_EPI=1, DPA_STREAM_EPI=1: 16-byte row stores of bf16 / fp32
+    outputs) store exactly the values the direct 2/4-byte stores do: a ResNet step's loss and
     every gradient are bitwise equal."""
     from distributed_pytorch_amd.models import resnet as R
 
@@ -476,6 +476,7 @@ def test_resnet_staged_epilogue_bitwise(monkeypatch, impl):
     out = []
     for epi in ("0", "1"):
         monkeypatch.setenv("DPA_OB_EPI", epi)
+        monkeypatch.setenv("DPA_STREAM_EPI", epi)
         m = R.ResNet([1, 2, 1, 1], 10, impl=impl)
         m.load_state_dict(sd)
         m = m.cuda()
