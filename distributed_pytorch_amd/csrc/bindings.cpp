@@ -76,7 +76,7 @@ int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const
                        float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* dz, long dzps, float* dw, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
-                      int posmajor, int np, hipStream_t st);
+                      int posmajor, int np, hipStream_t st, unsigned* fix, long nfix);
 int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
 int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
@@ -382,7 +382,7 @@ void bn_finalize(Tensor part, int64_t nblk, int64_t rpb, int64_t M, Tensor gamma
 
 // x3 [NP,N,H,W,C], dz3 [NP,N,P,Q,K], dw [K,R,S,C] fp32
 void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, int64_t posmajor) {
+                   int64_t tile, int64_t posmajor, OptT fix) {
   need_planes(x3, "x3");
   need_planes(dz3, "dz3");
   need(dw, "dw");
@@ -401,8 +401,16 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
     TORCH_CHECK(slab->numel() >= (int64_t)eff * K * R * S * C, "conv_x3_wgrad: slab too small");
     sl = fp(*slab);
   }
+  unsigned* fx = nullptr;  // optional per-tile split-K counters (int32, zeroed once): in-kernel fix-up
+  long nfx = 0;
+  if (fix.has_value() && fix->defined()) {
+    TORCH_CHECK(fix->is_cuda() && fix->scalar_type() == torch::kInt32 && fix->is_contiguous(),
+                "conv_x3_wgrad: fix must be a contiguous int32 device tensor");
+    fx = reinterpret_cast<unsigned*>(fix->data_ptr<int32_t>());
+    nfx = fix->numel();
+  }
   chk(dpa_conv_x3_wgrad(up(x3), x3.stride(0), up(dz3), dz3.stride(0), fp(dw), sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream()),
+                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream(), fx, nfx),
       "conv_x3_wgrad");
 }
 
@@ -1111,7 +1119,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_stats_rows", [](int64_t tile) { return (int64_t)dpa_conv_stats_rows((int)tile); });
   m.def("bn_finalize", &bn_finalize);
   m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
-        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0);
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0,
+        py::arg("fix") = py::none());
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
         py::arg("posmajor") = 0, py::arg("add") = py::none(), py::arg("sig") = py::none(),

@@ -97,6 +97,12 @@ struct Args {
     int Ktot, S, r0, s0, padh, padw;
     FastDiv fd_S;
   } phase[4];
+  // WGRAD split-K fix-up in the kernel (optional): per-tile arrival counters (zeroed once,
+  // self-resetting) and the final dW.  The last split block of a tile to arrive sums the tile's
+  // slabs in split order into fout: no separate reduce launch (splitk_fixup below).
+  unsigned* fix;
+  float* fout;
+  int fix_wt;  // 1: slab stores are agent-scope (write-through) stores and the release fence is skipped
 };
 
 __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& img, unsigned& oh, unsigned& ow) {
@@ -130,6 +136,64 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, long elem_off, 
 }
 
 enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
+
+// ---- split-K fix-up inside the weight-gradient kernel (ticketed, deterministic) ----
+// Every split block of a tile stores its fp32 slab as before, drains its stores, and one lane
+// releases them at agent scope and takes a ticket on the tile's counter (bn_fused.hip's hand-off).
+// The block that draws the last ticket re-arms the counter (the next launch is stream-ordered behind
+// this one), acquires, and sums the tile's slabs in split order 0..S-1 into fout: the same value
+// whichever block arrives last, so results are deterministic.  No block waits for another (no
+// residency assumption, no spin); the separate reduce launch and its re-read of every slab from a
+// cold kernel are gone.  flag: 4 bytes of the kernel's LDS (every wave is past its epilogue reads).
+// Slab stores of a fix-up launch: agent-scope (device-coherent) stores, written through the XCD's L2,
+// so the hand-off needs no agent-scope release fence (that fence writes back the whole L2 of the
+// XCD, dirty lines of every other kernel included, once per block).
+__device__ __forceinline__ void store4_agent(float* p, uint4 v) {
+  typedef __attribute__((address_space(1))) unsigned long long gu64;
+  const unsigned long long lo = v.x | ((unsigned long long)v.y << 32), hi = v.z | ((unsigned long long)v.w << 32);
+  __hip_atomic_store((gu64*)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64*)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int BM, int BN, int THREADS>
+__device__ __forceinline__ void splitk_fixup(const Args& a, int tile, int m0, int n0, unsigned* flag) {
+  typedef __attribute__((address_space(1))) unsigned gu32;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's device-coherent slab stores are acked
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (!a.fix_wt) {  // slabs stored through the L2 (plain stores): release them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned t = __hip_atomic_fetch_add((gu32*)(a.fix + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = t == (unsigned)a.splits - 1;
+    if (last) {
+      __hip_atomic_store((gu32*)(a.fix + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (*flag == 0u) return;
+  constexpr int C4 = BN / 4;
+  for (int q = threadIdx.x; q < BM * C4; q += THREADS) {
+    const int r = q / C4, row = m0 + r, col = n0 + (q - r * C4) * 4;
+    if (row < a.Nout && col < a.Ktot) {
+      const long off = (long)row * a.Ktot + col;
+      float4 s = *reinterpret_cast<const float4*>(a.out + off);
+#pragma unroll 4
+      for (int k = 1; k < a.splits; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(a.out + k * a.slab + off);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+      *reinterpret_cast<float4*>(a.fout + off) = s;
+    }
+  }
+}
 
 // The plane products of one k-slice over a TM x TN register tile, product-major: the TM*TN
 // accumulators are independent, so back-to-back MFMAs never wait on each other's result (an
@@ -724,6 +788,8 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
           if (row < nrows && col < ncols) {
             if constexpr (OB)
               *reinterpret_cast<uint4*>(a.outb + mrow_of(row) * ldc + col) = v;
+            else if (WG && a.fix_wt)
+              store4_agent(out + mrow_of(row) * ldc + col, v);
             else
               *reinterpret_cast<uint4*>(out + mrow_of(row) * ldc + col) = v;
           }
@@ -745,12 +811,18 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
               const long mrow = mrow_of(row);
               if constexpr (OB)
                 a.outb[mrow * ldc + col] = bf16_rne(acc[i][j][r]);
+              else if (WG && a.fix_wt)
+                __hip_atomic_store((__attribute__((address_space(1))) float*)(out + mrow * ldc + col), acc[i][j][r],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               else
                 out[mrow * ldc + col] = acc[i][j][r];
             }
           }
         }
       }
+  }
+  if constexpr (WG && !OB) {
+    if (a.fix != nullptr) splitk_fixup<BM, BN, THREADS>(a, tile, m0, n0, reinterpret_cast<unsigned*>(lds));
   }
   if constexpr (MODE == XM_FPROP) {
     if (a.stats != nullptr)
@@ -2326,7 +2398,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] Xcol[m][rsc]; x planes [NP][N,H,W,C], dz planes [NP][N,P,Q,Kout]
 int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* dw, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int posmajor, int np,
-                      hipStream_t st) {
+                      hipStream_t st, unsigned* fix, long nfix) {
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     WHArgs h{};
@@ -2358,9 +2430,16 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   a.out = a.splits > 1 ? slab : dw;
   a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
   a.sepi = ob_epi();
+  if (fix != nullptr && a.splits > 1) {  // slabs summed by each tile's last split block
+    if (nfix < (long)a.gm * a.gn) return -8;
+    a.fix = fix;
+    a.fout = dw;
+    const char* e = getenv("DPA_FIXUP_WT");  // A/B: 0 = plain slab stores + release fence
+    a.fix_wt = !(e && e[0] == '0');
+  }
   const int rc = np == 3 ? launch_tile<XM_WGRAD, 3>(a, tile, st) : launch_tile<XM_WGRAD, 1>(a, tile, st);
   if (rc) return rc;
-  if (a.splits > 1) {
+  if (a.splits > 1 && a.fix == nullptr) {
     const long n4 = (long)Kout * a.Ktot / 4;
     return launch_splitk_reduce(slab, dw, n4, a.splits, st);
   }

@@ -249,6 +249,13 @@ class VGGEngine:
         self.head_side = self.ksignal and os.environ.get("DPA_HEAD_SIDE", "1") == "1"
         self.slab = torch.empty(1, **f32)
         self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
+        # split-K weight gradients with at most this many splits sum their slabs inside the conv
+        # kernel (conv_x3.hip splitk_fixup: per-tile tickets, one self-resetting counter array per
+        # stream) instead of a separate reduce launch; 0 = always the reduce kernel
+        self.wgrad_fixup_max = int(os.environ.get("DPA_WGRAD_FIXUP_MAX", "0")) if dev.type == "cuda" else 0
+        self.wfix_main = torch.zeros(4096, dtype=torch.int32, device=dev) if self.wgrad_fixup_max > 0 else None
+        self.wfix_side = (torch.zeros(4096, dtype=torch.int32, device=dev)
+                          if self.wgrad_fixup_max > 0 and self.wstream is not None else None)
         for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
             for kind in ("fprop", "dgrad", "wgrad"):
                 if kind == "dgrad" and i == 0:
@@ -651,7 +658,13 @@ class VGGEngine:
         slab = (self.wslab if side else self.slab) if s > 1 else None
         dw = self.grads[f"{l.conv_key}.weight"]
         if self.planes[i]:
-            self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
+            fix = None
+            if s > 1 and s <= self.wgrad_fixup_max:  # slabs summed in-kernel by each tile's last split
+                fix = self.wfix_side if side else self.wfix_main
+            if fix is not None:
+                self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm, fix)
+            else:
+                self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
         else:
             xin = x if i == 0 else self.a[i - 1][:n]
             self.K.conv_wgrad(xin, self.dz[i][:n], dw, slab, 1, 1, s, tile, pm)
