@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define DPA_WAVE 64
 
@@ -92,51 +93,66 @@ __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __r
                                                                const TO* __restrict__ add) {
   __shared__ float4 part[G > 1 ? G : 1][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + c;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (i < n4) {
+  // grid-stride over 64-column groups (a capped grid leaves CUs to the other stream's kernels)
+  for (long i0 = (long)blockIdx.x * 64; i0 < n4; i0 += (long)gridDim.x * 64) {
+    const long i = i0 + c;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n4) {
 #pragma unroll 4
-    for (int k = g; k < splits; k += G) {
-      const float4 v = slabs[(long)k * n4 + i];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
+      for (int k = g; k < splits; k += G) {
+        const float4 v = slabs[(long)k * n4 + i];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
     }
-  }
-  if constexpr (G > 1) {
-    part[g][c] = s;
-    __syncthreads();
-    if (g != 0) return;
+    if constexpr (G > 1) {
+      part[g][c] = s;
+      __syncthreads();
+      if (g == 0) {
 #pragma unroll
-    for (int j = 1; j < G; ++j) {
-      s.x += part[j][c].x;
-      s.y += part[j][c].y;
-      s.z += part[j][c].z;
-      s.w += part[j][c].w;
+        for (int j = 1; j < G; ++j) {
+          s.x += part[j][c].x;
+          s.y += part[j][c].y;
+          s.z += part[j][c].z;
+          s.w += part[j][c].w;
+        }
+      }
+      __syncthreads();  // part is rewritten by the next group
+    }
+    if (g == 0 && i < n4) {
+      if (add) {
+        const float4 a = ld_add4(add, i);
+        s.x += a.x;
+        s.y += a.y;
+        s.z += a.z;
+        s.w += a.w;
+      }
+      st_out4(out, i, s);
     }
   }
-  if (i < n4) {
-    if (add) {
-      const float4 a = ld_add4(add, i);
-      s.x += a.x;
-      s.y += a.y;
-      s.z += a.z;
-      s.w += a.w;
-    }
-    st_out4(out, i, s);
-  }
+}
+
+// DPA_SPLITK_BLOCKS (A/B): cap on the reduce grid (0 = one block per 64 float4 columns)
+inline long splitk_block_cap() {
+  static const long cap = [] {
+    const char* e = getenv("DPA_SPLITK_BLOCKS");
+    return e ? atol(e) : 0L;
+  }();
+  return cap;
 }
 
 // out: float4 (fp32) or ushort4 (bf16, round-to-nearest-even); add: optional addend of out's type
 template <typename TO>
 inline int launch_splitk_reduce_t(const float* slabs, TO* o4, long n4, int splits, hipStream_t st,
                                   const TO* add = nullptr) {
-  const long blocks = (n4 + 63) / 64;
+  const long full = (n4 + 63) / 64, cap = splitk_block_cap();
+  const long blocks = cap > 0 && full > cap ? cap : full;
   const float4* in4 = reinterpret_cast<const float4*>(slabs);
-  if (splits >= 16 && blocks < 4096)
+  if (splits >= 16 && full < 4096)
     splitk_reduce_kernel<16, TO><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits, add);
-  else if (splits >= 4 && blocks < 16384)
+  else if (splits >= 4 && full < 16384)
     splitk_reduce_kernel<4, TO><<<blocks, 256, 0, st>>>(in4, o4, n4, splits, add);
   else
     splitk_reduce_kernel<1, TO><<<blocks, 64, 0, st>>>(in4, o4, n4, splits, add);
