@@ -75,6 +75,9 @@ def parse(argv=None):
                          "tail bucket, per-bucket update inside backward) on the real fabric and keep the fastest "
                          "(max over ranks, so every rank picks the same plan); off = --bucket-mb / defaults")
     ap.add_argument("--comm-tune-steps", type=int, default=8, help="timed steps per plan and repetition")
+    ap.add_argument("--rccl-channels", default="16,8",
+                    help="N>1 with the native RCCL communicator: channel (workgroup) budgets the comm tuner also "
+                         "tries, each on its own communicator (comma list; 'off' = RCCL's default only)")
     ap.add_argument("--profile", action="store_true",
                     help="re-run this command under rocprofv3 --kernel-trace --stats (prints the command)")
     ap.add_argument("--profile-dir", default="gpurun_out/prof")
@@ -141,24 +144,50 @@ def make_step(engine, sync, it, graphed=None, probe=None):
     return step
 
 
-def comm_plans(a):
-    """Candidate gradient-sync plans (bucket_mb, tail_mb, per-bucket update) for the warmup tuner.
-    Per-tensor modes keep their granularity (the reference's semantics) and only try the update
-    placement; an explicit --bucket-mb pins the bucket size."""
+def comm_plans(a, rccl: bool = False):
+    """Candidate gradient-sync plans (bucket_mb, tail_mb, per-bucket update, rccl_channels) for the
+    warmup tuner.  Per-tensor modes keep their granularity (the reference's semantics) and only try
+    the update placement; an explicit --bucket-mb pins the bucket size.  With a native RCCL
+    communicator (``rccl``) the default plan is also tried on communicators limited to
+    ``--rccl-channels`` workgroups: fewer RCCL workgroups leave more CUs to the backward the
+    collectives overlap (channels 0 = the communicator RCCL sized itself)."""
     fixed = a.bucket_mb
     if a.mode == "ddp":
         sizes = [fixed] if fixed is not None else [10.0, 25.0, 5.0]
-        plans = [(b, 2.0, False) for b in sizes] + [(sizes[0], 2.0, True), (sizes[0], 0.4, False)]
+        plans = [(b, 2.0, False, 0) for b in sizes] + [(sizes[0], 2.0, True, 0), (sizes[0], 0.4, False, 0)]
     elif a.mode == "allreduce":
-        plans = [(fixed, 2.0, False), (fixed, 2.0, True)]
+        plans = [(fixed, 2.0, False, 0), (fixed, 2.0, True, 0)]
     else:
         plans = []
+    if plans and rccl:
+        plans += [plans[0][:3] + (c,) for c in channel_budgets(a)]
     seen, out = set(), []
     for p in plans:
         if p not in seen:
             seen.add(p)
             out.append(p)
     return out
+
+
+def channel_budgets(a):
+    """RCCL channel budgets the tuner tries besides the default (``--rccl-channels``: a comma list,
+    'off' = none; DPA_RCCL_CHANNELS pins the main communicator's budget instead)."""
+    if a.rccl_channels == "off" or os.environ.get("DPA_RCCL_CHANNELS"):
+        return []
+    return [int(c) for c in a.rccl_channels.split(",") if int(c) > 0]
+
+
+def comm_for_channels(ctx, dev, channels: int, cache: dict):
+    """A communicator over the same ranks limited to ``channels`` RCCL workgroups (0: ctx.comm)."""
+    if channels == 0:
+        return ctx.comm
+    if channels not in cache:
+        from distributed_pytorch_amd.parallel.comm import RcclComm
+
+        store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
+        cache[channels] = RcclComm(ctx.rank, ctx.world, dev, store=store, tag=f"dpa_rccl_uid_ch{channels}",
+                                   channels=channels)
+    return cache[channels]
 
 
 def tune_comm(a, engine, sync, ctx, dev, batches):
@@ -169,16 +198,24 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     run: the numerics of every plan are identical (bitwise, tests/test_multirank_gpu.py).  The
     tuning steps draw their own batches and the training state is restored afterwards, so the
     run that follows is the same as without tuning."""
-    plans = comm_plans(a)
+    from distributed_pytorch_amd.parallel.comm import RcclComm
+
+    plans = comm_plans(a, rccl=isinstance(ctx.comm, RcclComm) and ctx.world > 1)
     if ctx.world <= 1 or a.comm_tune == "off" or len(plans) < 2 or a.no_overlap:
         return sync, None
     it = batches()
     snap = [t.clone() for t in (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt,
                                 engine.loss_accum)]
     steps_taken = engine.steps_taken
-    syncs = {}
-    for p in plans:
-        s = make_sync(a.mode, engine, ctx.comm, bucket_mb=p[0], overlap=True, broadcast_init=False, tail_mb=p[1])
+    syncs, comms = {}, {}
+    for p in list(plans):
+        try:
+            comm = comm_for_channels(ctx, dev, p[3], comms)
+        except RuntimeError as e:  # deterministic on every rank (a config RCCL refuses): drop the plan
+            print(f"[rank {ctx.rank}] comm tuner: no {p[3]}-channel communicator ({e})", flush=True)
+            plans.remove(p)
+            continue
+        s = make_sync(a.mode, engine, comm, bucket_mb=p[0], overlap=True, broadcast_init=False, tail_mb=p[1])
         s.fuse_step = p[2] and s.fusable_step
         syncs[p] = s
     n = max(1, a.comm_tune_steps)
@@ -210,9 +247,14 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     for sy in syncs.values():
         if hasattr(sy, "_bufs_fresh"):
             sy._bufs_fresh = False  # the next forward broadcasts rank 0's (restored) buffers again
-    report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2]},
-              "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}": round(score[p], 4)
-                              for p in plans}}
+    report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2],
+                         "rccl_channels": best[3] or None},
+              "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else ""):
+                              round(score[p], 4) for p in plans}}
+    if best[3]:  # the bounded communicator carries the run from here on (and the replica check)
+        ctx.comm = comms.pop(best[3])
+    for c in comms.values():  # the other bounded communicators are drained and left idle
+        c.synchronize()
     return syncs[best], report
 
 

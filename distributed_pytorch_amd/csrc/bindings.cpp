@@ -1031,10 +1031,10 @@ ncclRedOp_t nccl_op(const std::string& op) {
 class PyRcclComm {
  public:
   PyRcclComm(int rank, int world, py::bytes uid, int device, bool high_priority, double timeout_s, double poll_s,
-             bool watchdog, bool exit_on_error, bool debug_sync)
+             bool watchdog, bool exit_on_error, bool debug_sync, int max_ctas)
       : stream_(c10::hip::getStreamFromPool(high_priority, (c10::DeviceIndex)device)),
         comm_(rank, world, std::string(uid), device, stream_.stream(),
-              dpa::WatchdogConfig{timeout_s, poll_s, watchdog, exit_on_error, debug_sync}) {}
+              dpa::WatchdogConfig{timeout_s, poll_s, watchdog, exit_on_error, debug_sync}, max_ctas) {}
 
   void track(const Tensor& t) { c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_); }
 
@@ -1087,6 +1087,7 @@ class PyRcclComm {
   int64_t outstanding() { return (int64_t)comm_.outstanding(); }
   int64_t ops_issued() { return (int64_t)comm_.ops_issued(); }
   int comm_count() { return comm_.comm_count(); }
+  int max_ctas() const { return comm_.max_ctas(); }
   int rank() const { return comm_.rank(); }
   int world() const { return comm_.world(); }
 
@@ -1238,10 +1239,11 @@ PYBIND11_MODULE(_C, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("barrier", &dpa::TcpStoreClient::barrier, py::call_guard<py::gil_scoped_release>());
   py::class_<PyRcclComm>(m, "RcclComm")
-      .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool>(), py::arg("rank"),
+      .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool, int>(), py::arg("rank"),
            py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("high_priority") = false,
            py::arg("timeout_s") = 600.0, py::arg("poll_s") = 0.2, py::arg("watchdog") = true,
-           py::arg("exit_on_error") = true, py::arg("debug_sync") = false)
+           py::arg("exit_on_error") = true, py::arg("debug_sync") = false, py::arg("max_ctas") = 0)
+      .def_property_readonly("max_ctas", &PyRcclComm::max_ctas)
       .def("outstanding", &PyRcclComm::outstanding)
       .def("ops_issued", &PyRcclComm::ops_issued)
       .def("comm_count", &PyRcclComm::comm_count)

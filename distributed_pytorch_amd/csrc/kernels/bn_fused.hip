@@ -25,10 +25,15 @@
 // counter and the last departer zeroes both (no block of this launch polls any more by then; the
 // next launch is stream-ordered behind this one).  The workspace is zeroed once at allocation.
 //
-// Residency: a slice's R blocks must run concurrently.  Blocks are numbered slice-major, grids are
-// <= 512 blocks of 256 threads at <= 128 VGPRs (>= 2048 resident on an idle chip); a block that
-// waits longer than `ticks` of the wall clock sets tmo[0] = 1 and continues (garbage, never a hang;
-// the engine checks the word with its signal timeouts).
+// Residency: a slice's R blocks must run concurrently.  Blocks are numbered slice-major and the
+// dispatcher places them in order, so the rendezvous can only stall while other kernels (the
+// weight-gradient stream, RCCL) hold the CUs it needs -- they never wait for this kernel, so the
+// stall ends when they do.  The geometry query refuses (the engine then runs the three-kernel BN)
+// any grid above 512 blocks or above a quarter of the chip's co-resident capacity for this kernel
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs, or DPA_BN_FUSED_CAP blocks when set: tests
+// force the fallback with it).  A block that waits longer than `ticks` of the wall clock (the
+// engine's own short bound, DPA_BN_FUSED_TIMEOUT_US, 2 s by default) sets tmo[0] = 1 and continues
+// (garbage, never a hang; the engine raises on the word after the step).
 #include "common.h"
 
 namespace {
@@ -65,6 +70,7 @@ struct FArgs {
   float momentum, eps;
   int* tmo;
   unsigned long long ticks;
+  int phantom;  // tests only (DPA_BN_FUSED_TEST_PHANTOM): wait for R + phantom arrivals, i.e. time out
   int* sig;  // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
 };
@@ -123,7 +129,7 @@ __device__ __forceinline__ void slice_rendezvous(const FArgs& a, unsigned* cnt) 
     typedef __attribute__((address_space(1))) unsigned gu32;
     __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)a.R) {
+    while (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(a.R + a.phantom)) {
       if (wall_clock64() - t0 > a.ticks) {
         __hip_atomic_store((gint*)a.tmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -536,6 +542,80 @@ void launch_bwd(bool pool, int np, int grid, const FArgs& a, hipStream_t st) {
 #undef LB
 }
 
+// Co-resident blocks per CU of the kernel a geometry runs, minimum over the output plane counts.
+template <int U, int CL>
+int occupancy(bool bwd, bool pool) {
+  int lo = 1 << 30;
+  auto take = [&](const void* fn) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, FT, 0) != hipSuccess) n = 0;
+    lo = n < lo ? n : lo;
+  };
+#define OCC(B, P)                                                            \
+  do {                                                                       \
+    take(reinterpret_cast<const void*>(&B##_kernel<P, 0, U, CL>));           \
+    take(reinterpret_cast<const void*>(&B##_kernel<P, 1, U, CL>));           \
+    take(reinterpret_cast<const void*>(&B##_kernel<P, 3, U, CL>));           \
+  } while (0)
+  if (bwd) {
+    if (pool) {
+      if constexpr (U <= UMAX_BWD_POOL) OCC(bn_fused_bwd, true);
+    } else {
+      if constexpr (U <= UMAX_BWD) OCC(bn_fused_bwd, false);
+    }
+  } else {
+    if (pool) {
+      if constexpr (U <= UMAX_FWD_POOL) OCC(bn_fused_fwd, true);
+    } else {
+      OCC(bn_fused_fwd, false);
+    }
+  }
+#undef OCC
+  return lo == (1 << 30) ? 0 : lo;
+}
+
+// Blocks of this geometry's kernel that the idle chip holds at once (DPA_BN_FUSED_CAP overrides).
+long resident_capacity(bool bwd, bool pool, const Geo& g) {
+  if (const char* e = getenv("DPA_BN_FUSED_CAP")) return atol(e);
+  // occupancy per (direction, pool, U, CL), queried once per process (host calls on every launch
+  // would add to the enqueue time of the step)
+  static int cache[2][2][5][2] = {};
+  const int ui = g.U == 1 ? 0 : g.U == 2 ? 1 : g.U == 4 ? 2 : g.U == 8 ? 3 : 4;
+  int& slot = cache[bwd][pool][ui][g.CL == 16];
+  if (slot) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return (long)(slot - 1) * cus;
+  }
+  int occ = 0;
+#define CASE(UU) \
+  case UU: occ = g.CL == 16 ? occupancy<UU, 16>(bwd, pool) : occupancy<UU, 8>(bwd, pool); break;
+  switch (g.U) {
+    CASE(1)
+    CASE(2)
+    CASE(4)
+    CASE(8)
+    CASE(16)
+    default: break;
+  }
+#undef CASE
+  slot = occ + 1;
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return (long)occ * cus;
+}
+
+constexpr int GRID_MAX = 512;
+
+// pick_geo plus the residency guard (see the header comment)
+bool pick_geo_resident(int Mo, int C, bool pool, bool bwd, int rmax, Geo& g) {
+  if (!pick_geo(Mo, C, pool, bwd, rmax, g)) return false;
+  const long grid = (long)g.slices * g.R;
+  return grid <= GRID_MAX && 4 * grid <= resident_capacity(bwd, pool, g);
+}
+
 template <int CL>
 int dispatch(bool bwd, bool pool, int np, const Geo& g, const FArgs& a, hipStream_t st) {
   const int grid = g.slices * g.R;
@@ -565,6 +645,11 @@ unsigned long long ticks_of(long long us) {
   return (unsigned long long)us * (unsigned long long)khz / 1000ull;
 }
 
+int test_phantom() {
+  const char* e = getenv("DPA_BN_FUSED_TEST_PHANTOM");
+  return e ? atoi(e) : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -572,7 +657,7 @@ extern "C" {
 // rmax row blocks per channel slice; writes the workspace floats and counter words it needs.
 int dpa_bn_fused_geo(int Mo, int C, int pool, int bwd, int rmax, long* part_floats, long* cnt_words, int* blocks) {
   Geo g;
-  if (!pick_geo(Mo, C, pool != 0, bwd != 0, rmax, g)) return -6;
+  if (!pick_geo_resident(Mo, C, pool != 0, bwd != 0, rmax, g)) return -6;
   if (part_floats) *part_floats = (long)g.slices * g.R * (bwd ? 3 : 2) * 4 * g.CL;
   if (cnt_words) *cnt_words = (long)g.slices * 32;
   if (blocks) *blocks = g.slices * g.R;
@@ -589,7 +674,7 @@ int dpa_bn_fused_fwd(const float* src, int nsplit, float* zw, int N, int H, int 
                      int* tmo, long long timeout_us, hipStream_t st) {
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   Geo g;
-  if (C % 4 || !pick_geo(Mo, C, pool != 0, false, rmax, g)) return -6;
+  if (C % 4 || !pick_geo_resident(Mo, C, pool != 0, false, rmax, g)) return -6;
   FArgs a{};
   a.src = src;
   a.nsplit = nsplit < 1 ? 1 : nsplit;
@@ -604,6 +689,7 @@ int dpa_bn_fused_fwd(const float* src, int nsplit, float* zw, int N, int H, int 
   a.momentum = momentum, a.eps = eps;
   a.tmo = tmo;
   a.ticks = ticks_of(timeout_us);
+  a.phantom = test_phantom();
   return g.CL == 16 ? dispatch<16>(false, pool != 0, np, g, a, st) : dispatch<8>(false, pool != 0, np, g, a, st);
 }
 
@@ -616,7 +702,7 @@ int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H
                      int sig_val) {
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   Geo g;
-  if (C % 4 || !pick_geo(Mo, C, pool != 0, true, rmax, g)) return -6;
+  if (C % 4 || !pick_geo_resident(Mo, C, pool != 0, true, rmax, g)) return -6;
   FArgs a{};
   a.src = gsrc;
   a.nsplit = nsplit < 1 ? 1 : nsplit;
@@ -632,6 +718,7 @@ int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H
   a.out = out, a.out3 = out3, a.ps = ps;
   a.tmo = tmo;
   a.ticks = ticks_of(timeout_us);
+  a.phantom = test_phantom();
   a.sig = sig;
   a.sig_val = sig_val;
   return g.CL == 16 ? dispatch<16>(true, pool != 0, np, g, a, st) : dispatch<8>(true, pool != 0, np, g, a, st);

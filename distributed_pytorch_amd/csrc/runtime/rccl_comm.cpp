@@ -45,13 +45,23 @@ unsigned event_flags() {
 }  // namespace
 
 RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,
-                   WatchdogConfig wd)
+                   WatchdogConfig wd, int max_ctas)
     : rank_(rank), world_(world), device_(device), stream_(comm_stream), wd_(wd) {
   if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("bad RCCL unique id size");
   hip_check(hipSetDevice(device), "hipSetDevice");
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
-  check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  if (max_ctas > 0) {
+    // a bounded channel count: fewer RCCL workgroups share the CUs with the backward kernels
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 1;
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = max_ctas;
+    check(ncclCommInitRankConfig(&comm_, world, id, rank, &cfg), "ncclCommInitRankConfig");
+  } else {
+    check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  }
+  max_ctas_ = max_ctas;
   comm_raw_ = comm_;
   hip_check(hipEventCreateWithFlags(&ev_in_, event_flags()), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_out_, event_flags()), "hipEventCreate");
@@ -79,7 +89,30 @@ void RcclComm::warmup_connections() {
     check(ncclSend(b + (size_t)world_ * n, n, ncclFloat32, 0, comm_, stream_), "ncclSend");
   }
   check(ncclGroupEnd(), "ncclGroupEnd");
-  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize(warmup)");
+  // Bounded wait: the watchdog thread does not run yet, and a peer that dies between
+  // ncclCommInitRank and here would leave an unbounded synchronize hanging.  Only this
+  // thread knows the communicator, so aborting it here is safe.
+  hipEvent_t ev;
+  hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventRecord(ev, stream_), "hipEventRecord");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) break;
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (q != hipErrorNotReady || waited > wd_.timeout_s) {
+      hipEventDestroy(ev);
+      std::fprintf(stderr, "[dpa rank %d] RCCL connection warm-up %s after %.1f s\n", rank_,
+                   q != hipErrorNotReady ? hipGetErrorString(q) : "timed out", waited);
+      std::fflush(stderr);
+      if (wd_.exit_on_error) std::_Exit(70);
+      ncclCommAbort(comm_);
+      comm_ = comm_raw_ = nullptr;
+      throw std::runtime_error("RCCL connection warm-up failed (peer dead or hung)");
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  hipEventDestroy(ev);
   hip_check(hipFree(buf), "hipFree");
 }
 
@@ -101,9 +134,7 @@ RcclComm::~RcclComm() {
 
 void RcclComm::release_locked(bool abort) {
   if (comm_) {
-    if (aborted_unlocked_.load())
-      ;  // already aborted by the watchdog while an issuer was stuck in RCCL: only drop the handle
-    else if (abort)
+    if (abort)
       ncclCommAbort(comm_);
     else
       ncclCommDestroy(comm_);
@@ -175,8 +206,9 @@ void RcclComm::fail(const std::string& msg) {
   }
   // Abort under comm_mu_: an issue that is in flight finishes first (enqueue calls return without
   // waiting on peers), and no issuer can ever see the handle after it is released.  An issuer that
-  // holds the lock longer than the timeout is itself stuck inside RCCL: abort the communicator
-  // from here without the lock (unblocking it), then drop the handle once it lets go.
+  // holds the lock longer than the timeout is itself stuck inside RCCL on this blocking
+  // communicator; aborting it from here would free state that thread still uses, so
+  // the process ends as in the default mode.
   const auto t0 = std::chrono::steady_clock::now();
   while (!stop_) {
     Lock g(comm_mu_, std::defer_lock);
@@ -185,12 +217,12 @@ void RcclComm::fail(const std::string& msg) {
       return;
     }
     const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (!aborted_unlocked_.load() && waited > wd_.timeout_s && comm_raw_) {
-      std::fprintf(stderr, "[dpa rank %d] RCCL watchdog: an enqueue is stuck inside RCCL; aborting the communicator\n",
+    if (waited > wd_.timeout_s) {
+      std::fprintf(stderr,
+                   "[dpa rank %d] RCCL watchdog: an enqueue is stuck inside RCCL; terminating the process (exit 70)\n",
                    rank_);
       std::fflush(stderr);
-      ncclCommAbort(comm_raw_);
-      aborted_unlocked_ = true;
+      std::_Exit(70);
     }
   }
 }

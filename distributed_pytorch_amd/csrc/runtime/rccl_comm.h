@@ -43,8 +43,10 @@ struct WatchdogConfig {
 class RcclComm {
  public:
   // uid: NCCL_UNIQUE_ID_BYTES bytes created by rank 0 (unique_id()) and shared out of band.
+  // max_ctas > 0: the communicator runs its collectives on at most that many workgroups (RCCL
+  // channels, ncclConfig_t::maxCTAs) -- the CU footprint beside the overlapped backward.
   RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,
-           WatchdogConfig wd = WatchdogConfig());
+           WatchdogConfig wd = WatchdogConfig(), int max_ctas = 0);
   ~RcclComm();
 
   static std::string unique_id();
@@ -55,6 +57,8 @@ class RcclComm {
   hipStream_t stream() const { return stream_; }
   // ranks RCCL itself reports for this communicator (ncclCommCount); -1 once aborted
   int comm_count();
+  // the channel (workgroup) budget the communicator was created with; 0 = RCCL's default
+  int max_ctas() const { return max_ctas_; }
 
   // All ops: comm stream waits for everything already queued on `after` (the compute stream),
   // then runs the collective.  Returns immediately.
@@ -97,7 +101,7 @@ class RcclComm {
   // issuer has held the lock past the timeout it is stuck inside RCCL (ncclCommAbort is callable
   // from another thread and unblocks it); the handle is then only cleared, never released again.
   ncclComm_t comm_raw_ = nullptr;
-  std::atomic<bool> aborted_unlocked_{false};
+  int max_ctas_ = 0;
   std::timed_mutex comm_mu_;
   hipStream_t stream_;
   hipEvent_t ev_in_, ev_out_;

@@ -242,8 +242,14 @@ class VGGEngine:
         # A wait may legitimately last as long as the main stream is held behind the previous step's
         # collectives (a slow peer: up to the communicator's DPA_COMM_TIMEOUT, after which the RCCL
         # watchdog aborts), so the bound is never shorter than that plus a minute.
+        # DPA_KSIGNAL_TIMEOUT_US, when set, is taken as given (tests use short bounds).
         comm_us = int(float(os.environ.get("DPA_COMM_TIMEOUT", "600")) * 1e6)
-        self.ksig_timeout_us = max(int(os.environ.get("DPA_KSIGNAL_TIMEOUT_US", "0")), comm_us + 60_000_000)
+        env_tmo = os.environ.get("DPA_KSIGNAL_TIMEOUT_US")
+        self.ksig_timeout_us = int(env_tmo) if env_tmo else comm_us + 60_000_000
+        # The one-launch BN's slice rendezvous waits only for blocks of its own grid (never for the
+        # communicator), so it has its own short bound: a residency shortfall surfaces in seconds,
+        # not after the communicator's timeout.
+        self.bn_fused_timeout_us = int(os.environ.get("DPA_BN_FUSED_TIMEOUT_US", "2000000"))
         # params_free hands the sync a later kernel's signal instead of recording an event (A/B: 0)
         self.free_signal = os.environ.get("DPA_FREE_SIGNAL", "1") == "1"
         self.head_side = self.ksignal and os.environ.get("DPA_HEAD_SIDE", "1") == "1"
@@ -747,7 +753,7 @@ class VGGEngine:
                                self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                                self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
                                None if head else self._act_out(i, n), self.bn_momentum, self.bn_eps, self.bn_tmo,
-                               self.ksig_timeout_us)
+                               self.bn_fused_timeout_us)
                 continue
             K.bn_fwd_stats(self.slab if ns > 1 else z, ns, z, self.part, P[f"{l.bn_key}.weight"],
                            P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
@@ -865,7 +871,7 @@ class VGGEngine:
                 K.bn_fused_bwd(self.slab if gsplit > 1 else g, gsplit, z, l.pool, self.bn_fused_rmax, self.fpart,
                                self.fcnt, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
                                G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf,
-                               self.bn_tmo, self.ksig_timeout_us, **bsig)
+                               self.bn_tmo, self.bn_fused_timeout_us, **bsig)
             else:
                 K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                          st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
@@ -944,7 +950,8 @@ class VGGEngine:
             raise RuntimeError("VGGEngine: a wgrad-stream signal wait timed out "
                                f"(DPA_KSIGNAL_TIMEOUT_US={self.ksig_timeout_us}); weight gradients are invalid")
         if int(self.bn_tmo.item()) != 0:
-            raise RuntimeError("VGGEngine: a one-launch BatchNorm slice rendezvous timed out; this step's "
+            raise RuntimeError("VGGEngine: a one-launch BatchNorm slice rendezvous timed out "
+                               f"(DPA_BN_FUSED_TIMEOUT_US={self.bn_fused_timeout_us}); this step's "
                                "activations / gradients are invalid")
 
     def finish_step(self):

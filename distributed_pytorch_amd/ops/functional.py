@@ -342,7 +342,8 @@ class GradJoin:
 
 class Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, impl: str, join: Optional[GradJoin] = None):
+    def forward(ctx, x, w, stride: int, pad: int, impl: str, join: Optional[GradJoin] = None,
+                grad_mode: bool = True):
         N, H, W, Cx = x.shape
         K, R, S, C = w.shape  # C: the weight's (padded) input channels; x may carry fewer (network input)
         P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
@@ -381,8 +382,11 @@ class Conv2dNHWC(torch.autograd.Function):
         cfg = choose_config(impl, "fprop", geom, N * P * Q, K, R * S * C, P * Q <= 16, run,
                             lambda s: 4 * s * N * P * Q * K)
         sk = Kx.x3_splits(R * S * C, cfg[1])
-        # training (grad mode is off inside forward; the weight needing a gradient is the signal)
-        rows = Kx.conv_stats_rows(cfg[0]) if (EPI_STATS and sk == 1 and ctx.needs_input_grad[1]) else 0
+        # a training forward: grad mode as it was at the call site (it is off inside forward) and a
+        # weight that needs a gradient.  An eval / no_grad forward registers nothing: its BN never
+        # pops the entry, which would pin z until the next training step.
+        rows = (Kx.conv_stats_rows(cfg[0]) if (EPI_STATS and sk == 1 and grad_mode and ctx.needs_input_grad[1])
+                else 0)
         stats = None
         if rows > 0:
             nblk = (N * P * Q + rows - 1) // rows
@@ -416,7 +420,7 @@ class Conv2dNHWC(torch.autograd.Function):
                     dw = slot.copy_(dw)
             if ctx.join is not None and ctx.needs_input_grad[0]:
                 dx = ctx.join.contribute(dx.contiguous())
-            return dx, dw, None, None, None, None
+            return dx, dw, None, None, None, None, None
         Kx = _ext.require()
         xp, wp = a, b
         np_ = xp.shape[0]
@@ -460,7 +464,7 @@ class Conv2dNHWC(torch.autograd.Function):
             dx = dx[..., :ctx.cx].contiguous()
         if join is not None and dx is not None and addend is None:
             dx = join.contribute(dx)  # not last (stash; autograd gets None), or a sliced input
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, impl: str = "bf16",
@@ -469,7 +473,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0,
     extra pass."""
     if impl not in NPLANES:
         raise ValueError(f"impl must be one of {list(NPLANES)}")
-    return Conv2dNHWC.apply(x.contiguous(), w, int(stride), int(pad), impl, join)
+    return Conv2dNHWC.apply(x.contiguous(), w, int(stride), int(pad), impl, join, torch.is_grad_enabled())
 
 
 class BnActNHWC(torch.autograd.Function):

@@ -226,12 +226,14 @@ class RcclComm(Comm):
     async RCCL errors and timeouts abort the communicator and, unless ``DPA_WATCHDOG_EXIT=0``,
     end the process with exit code 70 so the launcher tears the job down.  ``DPA_DEBUG_SYNC=1``
     makes every collective host-synchronous and error-checked (ordering/race debugging).
-    ``DPA_WATCHDOG=0`` disables the thread."""
+    ``DPA_WATCHDOG=0`` disables the thread.  ``channels`` (default ``DPA_RCCL_CHANNELS``, 0 = RCCL's
+    choice) bounds the workgroups the collectives run on (``ncclConfig_t.maxCTAs``): the CU
+    footprint of the communication beside the overlapped backward."""
 
     name = "rccl"
 
     def __init__(self, rank: int, world: int, device: torch.device, store=None, uid: Optional[bytes] = None,
-                 tag: str = "dpa_rccl_uid"):
+                 tag: str = "dpa_rccl_uid", channels: Optional[int] = None):
         from .. import _ext
 
         C = _ext.require()
@@ -247,7 +249,10 @@ class RcclComm(Comm):
                                  timeout_s=float(os.environ.get("DPA_COMM_TIMEOUT", "600")),
                                  watchdog=os.environ.get("DPA_WATCHDOG", "1") == "1",
                                  exit_on_error=os.environ.get("DPA_WATCHDOG_EXIT", "1") == "1",
-                                 debug_sync=os.environ.get("DPA_DEBUG_SYNC", "0") == "1")
+                                 debug_sync=os.environ.get("DPA_DEBUG_SYNC", "0") == "1",
+                                 max_ctas=channels if channels is not None else
+                                 int(os.environ.get("DPA_RCCL_CHANNELS", "0")))
+        self.channels = self._c.max_ctas
         self.stream = torch.cuda.ExternalStream(self._c.stream_ptr(), device=self.device)
         self._join_in, self._join_out = StreamJoin(), StreamJoin()
         self._store = store

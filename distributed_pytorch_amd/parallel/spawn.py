@@ -67,9 +67,14 @@ class _Stopped(Exception):
         self.signum = signum
 
 
+_STOP_SIGNALS = (signal.SIGTERM, signal.SIGHUP, signal.SIGINT)
+
+
 def _die_with_parent(parent: int):
     """preexec_fn of every rank (runs in the child between fork and exec): SIGTERM when the launcher
-    dies; exit at once if it is already gone."""
+    dies; exit at once if it is already gone.  The launcher blocks the stop signals while it starts
+    ranks and exec keeps the signal mask, so the child unblocks them here."""
+    signal.pthread_sigmask(signal.SIG_UNBLOCK, _STOP_SIGNALS)
     try:
         ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
     except OSError:
@@ -100,17 +105,27 @@ def launch(script: str, argv: Sequence[str], nprocs: int, timeout_s: float = 180
         def _on_signal(signum, _frame):
             raise _Stopped(signum)
 
-        for sg in (signal.SIGTERM, signal.SIGHUP, signal.SIGINT):
+        for sg in _STOP_SIGNALS:
             old_handlers[sg] = signal.signal(sg, _on_signal)
     code = 0
     failed: Optional[int] = None
+    main = threading.current_thread() is threading.main_thread()
     try:
-        for r in range(nprocs):
-            env = rank_env(r, nprocs, port, store_port)
-            if extra_env:
-                env.update(extra_env)
-            procs.append(subprocess.Popen([py, script, *argv], env=env, start_new_session=True,
-                                          preexec_fn=lambda: _die_with_parent(parent)))
+        # Stop signals stay pending while ranks start: one arriving between a fork and the append
+        # below would otherwise leave a rank the teardown never signals.  They are
+        # delivered (and raise into the teardown) once every started rank is in `procs`.
+        if main:
+            signal.pthread_sigmask(signal.SIG_BLOCK, _STOP_SIGNALS)
+        try:
+            for r in range(nprocs):
+                env = rank_env(r, nprocs, port, store_port)
+                if extra_env:
+                    env.update(extra_env)
+                procs.append(subprocess.Popen([py, script, *argv], env=env, start_new_session=True,
+                                              preexec_fn=lambda: _die_with_parent(parent)))
+        finally:
+            if main:
+                signal.pthread_sigmask(signal.SIG_UNBLOCK, _STOP_SIGNALS)
         deadline = time.monotonic() + timeout_s
         while True:
             alive = 0

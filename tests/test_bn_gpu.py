@@ -256,3 +256,60 @@ def test_bn_fused_geometry_limits():
                         (256 * 16, 256, True), (256 * 64, 256, False)):
         geo = C_.bn_fused_geo(mo, c, pool, False, 64)
         assert geo is not None and geo[2] <= 512, (mo, c, pool, geo)
+
+
+def test_bn_fused_residency_guard_falls_back(monkeypatch):
+    """a one-launch BN grid that could exceed the co-resident capacity is refused
+    by the geometry query (DPA_BN_FUSED_CAP pretends a small chip), and the engine then runs the
+    three-kernel BN for every layer; the step still trains and matches the default engine."""
+    from distributed_pytorch_amd.engine import VGGEngine
+
+    C_ = _C()
+    assert C_.bn_fused_geo(256 * 4, 512, True, False, 64) is not None
+    monkeypatch.setenv("DPA_BN_FUSED_CAP", "8")
+    assert C_.bn_fused_geo(256 * 4, 512, True, False, 64) is None
+    torch.manual_seed(0)
+    x = torch.zeros(64, 32, 32, 4, device="cuda")
+    x[..., :3] = torch.randn(64, 32, 32, 3, device="cuda")
+    t = torch.randint(0, 10, (64,), device="cuda")
+    res = []
+    for cap in ("8", None):
+        if cap is None:
+            monkeypatch.delenv("DPA_BN_FUSED_CAP")
+        eng = VGGEngine("VGG11", "cuda", max_batch=64, impl="x3")
+        eng.init_parameters(seed=1)
+        fused = [eng._fused(i, 64, b) for i in range(8) for b in (False, True)]
+        assert any(fused) == (cap is None), fused
+        loss = float(eng.forward_backward(x, t).item())
+        torch.cuda.synchronize()
+        eng.check_signals()
+        res.append((loss, eng.grads.flat.clone()))
+    assert abs(res[0][0] - res[1][0]) <= 1e-4 * abs(res[1][0])
+    rel = ((res[0][1] - res[1][1]).norm() / res[1][1].norm()).item()
+    assert rel < 1e-3, rel
+
+
+def test_bn_fused_rendezvous_timeout_sets_flag(monkeypatch):
+    """A slice rendezvous that can never complete (test-only phantom arrivals) gives up after its
+    own short bound, raises the timeout word and leaves the counters re-armed: no hang."""
+    C_ = _C()
+    shape = (256, 4, 4, 512, True)
+    ws = _fused_ws(C_, shape, False, 64)
+    part, cnt = ws
+    g, z, gamma, beta, bias, rm, rv, _ = _inputs(shape, 5)
+    d = lambda t: t.cuda()
+    monkeypatch.setenv("DPA_BN_FUSED_TEST_PHANTOM", "1")
+    mean, invstd, scale, shift = (torch.zeros(512, device="cuda") for _ in range(4))
+    tmo = torch.zeros(1, dtype=torch.int32, device="cuda")
+    zd = d(z)
+    C_.bn_fused_fwd(zd, 1, zd, True, 64, part, cnt, d(gamma), d(beta), d(bias), d(rm), d(rv), None, mean, invstd,
+                    scale, shift, None, MOM, EPS, tmo, 20_000)
+    torch.cuda.synchronize()
+    assert int(tmo.item()) == 1
+    assert int(cnt.abs().sum().item()) == 0, "slice counters not reset after a timeout"
+    monkeypatch.delenv("DPA_BN_FUSED_TEST_PHANTOM")
+    tmo.zero_()
+    C_.bn_fused_fwd(zd, 1, zd, True, 64, part, cnt, d(gamma), d(beta), d(bias), d(rm), d(rv), None, mean, invstd,
+                    scale, shift, None, MOM, EPS, tmo, 2_000_000)
+    torch.cuda.synchronize()
+    assert int(tmo.item()) == 0

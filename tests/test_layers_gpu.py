@@ -375,6 +375,25 @@ def test_resnet_epilogue_bn_stats(monkeypatch, impl):
         assert (a - b).abs().max().item() <= 1e-4 * max(a.abs().max().item(), 1e-6), n
 
 
+def test_eval_no_grad_registers_no_epilogue_stats():
+    """An eval forward under no_grad (parameters still requiring grad) registers no epilogue BN
+    statistics: eval-mode BN never pops them, and each entry pins its conv output."""
+    from distributed_pytorch_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    m = R.ResNet([1, 1, 1, 1], 10, impl="x3").cuda()
+    x = torch.randn(4, 64, 64, 3).cuda()
+    t = torch.randint(0, 10, (4,)).cuda()
+    m(x, t).backward()  # a training step first (clears and repopulates the table)
+    torch.cuda.synchronize()
+    R.Fn._STATS.clear()
+    m.eval()
+    with torch.no_grad():
+        m(x, t)
+    torch.cuda.synchronize()
+    assert len(R.Fn._STATS) == 0
+
+
 @pytest.mark.parametrize("impl", ["x3", "bf16"])
 def test_resnet_bn_dy_pass(monkeypatch, impl):
     """Add+ReLU BN backward with the dy pass (DPA_BN_DY_PASS=1: the reduce kernel stores
