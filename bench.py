@@ -75,6 +75,9 @@ def parse(argv=None):
                          "tail bucket, per-bucket update inside backward) on the real fabric and keep the fastest "
                          "(max over ranks, so every rank picks the same plan); off = --bucket-mb / defaults")
     ap.add_argument("--comm-tune-steps", type=int, default=8, help="timed steps per plan and repetition")
+    ap.add_argument("--ipc", default="auto", choices=["auto", "on", "off"],
+                    help="N>1 on one node: bucket all-reduces on the peer-memory kernel (parallel/ipc.py). "
+                         "auto = one more comm-tuner plan; on = always (any --comm; several ranks may share a GPU)")
     ap.add_argument("--rccl-channels", default="16,8",
                     help="N>1 with the native RCCL communicator: channel (workgroup) budgets the comm tuner also "
                          "tries, each on its own communicator (comma list; 'off' = RCCL's default only)")
@@ -144,23 +147,27 @@ def make_step(engine, sync, it, graphed=None, probe=None):
     return step
 
 
-def comm_plans(a, rccl: bool = False):
-    """Candidate gradient-sync plans (bucket_mb, tail_mb, per-bucket update, rccl_channels) for the
-    warmup tuner.  Per-tensor modes keep their granularity (the reference's semantics) and only try
-    the update placement; an explicit --bucket-mb pins the bucket size.  With a native RCCL
-    communicator (``rccl``) the default plan is also tried on communicators limited to
+def comm_plans(a, rccl: bool = False, ipc: bool = False):
+    """Candidate gradient-sync plans (bucket_mb, tail_mb, per-bucket update, rccl_channels,
+    ipc) for the warmup tuner.  Per-tensor modes keep their granularity (the reference's semantics)
+    and only try the update placement; an explicit --bucket-mb pins the bucket size.  With a native
+    RCCL communicator (``rccl``) the default plan is also tried on communicators limited to
     ``--rccl-channels`` workgroups: fewer RCCL workgroups leave more CUs to the backward the
-    collectives overlap (channels 0 = the communicator RCCL sized itself)."""
+    collectives overlap (channels 0 = the communicator RCCL sized itself).  ``ipc``: the default
+    plan is also tried with the bucket all-reduces on the peer-memory kernel (parallel/ipc.py)."""
     fixed = a.bucket_mb
     if a.mode == "ddp":
         sizes = [fixed] if fixed is not None else [10.0, 25.0, 5.0]
-        plans = [(b, 2.0, False, 0) for b in sizes] + [(sizes[0], 2.0, True, 0), (sizes[0], 0.4, False, 0)]
+        plans = [(b, 2.0, False, 0, False) for b in sizes] + [(sizes[0], 2.0, True, 0, False),
+                                                               (sizes[0], 0.4, False, 0, False)]
     elif a.mode == "allreduce":
-        plans = [(fixed, 2.0, False, 0), (fixed, 2.0, True, 0)]
+        plans = [(fixed, 2.0, False, 0, False), (fixed, 2.0, True, 0, False)]
     else:
         plans = []
     if plans and rccl:
-        plans += [plans[0][:3] + (c,) for c in channel_budgets(a)]
+        plans += [plans[0][:3] + (c, False) for c in channel_budgets(a)]
+    if plans and ipc:
+        plans += [plans[0][:3] + (0, True)]
     seen, out = set(), []
     for p in plans:
         if p not in seen:
@@ -190,6 +197,24 @@ def comm_for_channels(ctx, dev, channels: int, cache: dict):
     return cache[channels]
 
 
+def ipc_possible(ctx, dev) -> bool:
+    """Every rank on this node and on a GPU: the peer-memory all-reduce can map the peers."""
+    return (dev.type == "cuda" and ctx.world > 1
+            and int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world)) == ctx.world and ctx.world <= 8)
+
+
+def ipc_comm(ctx, dev, engine, cache: dict):
+    """The peer-memory communicator over ctx.comm with the gradient arena registered (collective)."""
+    if "ipc" not in cache:
+        from distributed_pytorch_amd.parallel.ipc import IpcComm
+
+        store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
+        c = IpcComm(ctx.comm, store, dev, timeout_s=float(os.environ.get("DPA_IPC_TUNE_TIMEOUT", "20")))
+        c.register(engine.grads.flat)
+        cache["ipc"] = c
+    return cache["ipc"]
+
+
 def tune_comm(a, engine, sync, ctx, dev, batches):
     """Warmup-phase choice among ``comm_plans``: each plan runs ``--comm-tune-steps`` steps per
     repetition (2 repetitions, interleaved); the score of a plan is its best repetition's time,
@@ -199,8 +224,12 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     tuning steps draw their own batches and the training state is restored afterwards, so the
     run that follows is the same as without tuning."""
     from distributed_pytorch_amd.parallel.comm import RcclComm
+    from distributed_pytorch_amd.parallel.ipc import IpcComm
 
-    plans = comm_plans(a, rccl=isinstance(ctx.comm, RcclComm) and ctx.world > 1)
+    if isinstance(ctx.comm, IpcComm):  # --ipc on: the transport is fixed
+        return sync, None
+    plans = comm_plans(a, rccl=isinstance(ctx.comm, RcclComm) and ctx.world > 1,
+                       ipc=a.ipc == "auto" and ipc_possible(ctx, dev))
     if ctx.world <= 1 or a.comm_tune == "off" or len(plans) < 2 or a.no_overlap:
         return sync, None
     it = batches()
@@ -210,9 +239,9 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     syncs, comms = {}, {}
     for p in list(plans):
         try:
-            comm = comm_for_channels(ctx, dev, p[3], comms)
+            comm = ipc_comm(ctx, dev, engine, comms) if p[4] else comm_for_channels(ctx, dev, p[3], comms)
         except RuntimeError as e:  # deterministic on every rank (a config RCCL refuses): drop the plan
-            print(f"[rank {ctx.rank}] comm tuner: no {p[3]}-channel communicator ({e})", flush=True)
+            print(f"[rank {ctx.rank}] comm tuner: no communicator for plan {p} ({e})", flush=True)
             plans.remove(p)
             continue
         s = make_sync(a.mode, engine, comm, bucket_mb=p[0], overlap=True, broadcast_init=False, tail_mb=p[1])
@@ -232,6 +261,12 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
             benchlib.device_barrier(ctx, dev)
             el = ctx.all_max(time.perf_counter() - t0) / n * 1e3
             score[p] = min(score.get(p, el), el)
+    # a plan whose peer-memory waits timed out (any rank) is disqualified
+    if "ipc" in comms:
+        bad = ctx.all_max(1.0 if comms["ipc"]._c.take_timeout() else 0.0) > 0
+        if bad:
+            print(f"[rank {ctx.rank}] comm tuner: IPC all-reduce timed out; plan dropped", flush=True)
+            plans = [p for p in plans if not p[4]]
     # the first plan is the default: another one must beat it by 1 % (run-to-run noise of a few
     # steps), so the choice does not flap between equivalent plans
     best = min(plans, key=lambda p: score[p])
@@ -248,10 +283,12 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
         if hasattr(sy, "_bufs_fresh"):
             sy._bufs_fresh = False  # the next forward broadcasts rank 0's (restored) buffers again
     report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2],
-                         "rccl_channels": best[3] or None},
-              "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else ""):
-                              round(score[p], 4) for p in plans}}
-    if best[3]:  # the bounded communicator carries the run from here on (and the replica check)
+                         "rccl_channels": best[3] or None, "ipc_allreduce": best[4]},
+              "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else "")
+                              + ("_ipc" if p[4] else ""): round(score[p], 4) for p in plans}}
+    if best[4]:  # the peer-memory communicator carries the run from here on
+        ctx.comm = comms.pop("ipc")
+    elif best[3]:  # the bounded communicator carries the run from here on (and the replica check)
         ctx.comm = comms.pop(best[3])
     for c in comms.values():  # the other bounded communicators are drained and left idle
         c.synchronize()
@@ -305,7 +342,14 @@ def main(argv=None):
             solo_img_s = solo_phase(a, dev, solo_steps, min(a.warmup, 5))
         ctx.barrier()
 
+    if a.ipc == "on" and ipc_possible(ctx, dev):
+        from distributed_pytorch_amd.parallel.ipc import IpcComm
+
+        store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
+        ctx.comm = IpcComm(ctx.comm, store, dev)
     engine, sync, batches = build_parts(a, dev, ctx.rank, ctx.world, ctx.comm)
+    if a.ipc == "on" and hasattr(ctx.comm, "register"):
+        ctx.comm.register(engine.grads.flat)
     sync, tune_report = tune_comm(a, engine, sync, ctx, dev, batches)
     it = batches()
     graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
@@ -366,6 +410,7 @@ def main(argv=None):
             "solo_img_s": round(solo_img_s, 1) if solo_img_s else None,
             "scaling_efficiency": round(per_gpu / solo_img_s, 4) if solo_img_s else None,
             "rccl_world": cw,
+            "ipc_allreduce_ops": getattr(ctx.comm, "ipc_ops", None),
             "replicas_identical": pdiff == 0.0,
             "replica_param_max_diff": pdiff,
             "comm_diag": diag,

@@ -4,6 +4,7 @@
 #include <c10/hip/HIPCachingAllocator.h>
 #include <torch/extension.h>
 
+#include "runtime/ipc_comm.h"
 #include "runtime/rccl_comm.h"
 #include "runtime/tcp_store.h"
 
@@ -71,6 +72,14 @@ int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
                       int reduce, int posmajor, int np, int obf, hipStream_t st, float* stats);
 int dpa_conv_stats_rows(int tile);
+int dpa_conv_x3_dgrad_bnin(const float* gin, const float* zin, int pool, const float* bsc, const float* bsh,
+                           const float* coef, unsigned short* dz3w, long dz3ps, const unsigned short* w, long wps,
+                           void* dx, float* slab, int N, int H, int W, int K, int C, int splits, int tile, int np,
+                           hipStream_t st, int* sig, int sig_val);
+long dpa_ipc_slice(long n, int world);
+int dpa_conv_x3_fprop_bnin(const float* zin, int pool, const float* bsc, const float* bsh, unsigned short* a3w,
+                           long a3ps, const unsigned short* w, long wps, void* out, float* slab, int N, int H, int W,
+                           int C, int Kout, int splits, int tile, int np, hipStream_t st, float* stats);
 int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const float* gamma, const float* beta,
                        const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
                        float* scale, float* shift, float momentum, float eps, hipStream_t st);
@@ -359,6 +368,119 @@ void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, 
   chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), op, sl, N, H, W, C, K, R, S, (int)stride,
                         (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf, cur_stream(), stp),
       "conv_x3_fprop");
+}
+
+// Forward conv with the previous layer's BatchNorm (+ReLU, +2x2 max-pool) applied on load: zin fp32
+// [N, H(*2), W(*2), C], scale/shift [C]; a3w (optional) receives the operand planes [NP,N,H,W,C];
+// w3 [NP,K,3,3,C]; out fp32 [N,H,W,K] (one split) or slabs (left unreduced).  Halo tiles 17 / 19.
+void conv_x3_fprop_bnin(Tensor zin, bool pool, Tensor scale, Tensor shift, OptT a3w, Tensor w3, Tensor out, OptT slab,
+                        int64_t splits, int64_t tile, OptT stats) {
+  need(zin, "zin");
+  need(scale, "scale");
+  need(shift, "shift");
+  need_planes(w3, "w3");
+  need(out, "out");
+  const int np = w3.size(0);
+  const int N = zin.size(0), C = zin.size(3);
+  const int H = pool ? zin.size(1) / 2 : zin.size(1), W = pool ? zin.size(2) / 2 : zin.size(2);
+  const int K = w3.size(1);
+  TORCH_CHECK(w3.size(2) == 3 && w3.size(3) == 3 && w3.size(4) == C, "conv_x3_fprop_bnin: weight shape");
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && C <= 512 && C % 32 == 0, "conv_x3_fprop_bnin: channels");
+  TORCH_CHECK(!pool || (zin.size(1) % 2 == 0 && zin.size(2) % 2 == 0), "conv_x3_fprop_bnin: odd pooled map");
+  TORCH_CHECK(out.size(0) == N && out.size(1) == H && out.size(2) == W && out.size(3) == K,
+              "conv_x3_fprop_bnin: out shape");
+  u16* a3p = nullptr;
+  long a3ps = 0;
+  if (a3w.has_value() && a3w->defined()) {
+    need_planes(*a3w, "a3w");
+    TORCH_CHECK(a3w->size(0) == np && a3w->size(1) == N && a3w->size(2) == H && a3w->size(3) == W &&
+                    a3w->size(4) == C,
+                "conv_x3_fprop_bnin: a3w shape");
+    a3p = up(*a3w);
+    a3ps = a3w->stride(0);
+  }
+  float* sl = nullptr;
+  const int eff = dpa_x3_splits(9 * C, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_fprop_bnin: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * K, "conv_x3_fprop_bnin: slab too small");
+    sl = fp(*slab);
+  }
+  float* stp = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    need(*stats, "stats");
+    const int rows = dpa_conv_stats_rows((int)tile);
+    TORCH_CHECK(rows > 0 && stats->numel() >= 2 * (int64_t)((N * H * W + rows - 1) / rows) * K,
+                "conv_x3_fprop_bnin: stats");
+    stp = fp(*stats);
+  }
+  chk(dpa_conv_x3_fprop_bnin(fp(zin), pool ? 1 : 0, fp(scale), fp(shift), a3p, a3ps, up(w3), w3.stride(0), fp(out), sl,
+                             N, H, W, C, K, (int)splits, (int)tile, np, cur_stream(), stp),
+      "conv_x3_fprop_bnin");
+}
+
+// Data gradient of a 3x3/s1/p1 conv with this layer's BatchNorm backward applied on load: g fp32
+// [N, H(/2), W(/2), K] (the summed dL/d(layer output)), z [N,H,W,K], scale/shift (forward) and coef
+// [3K] (bn_bwd statistics); dz3w (optional) receives dz's planes [3,N,H,W,K]; w3 [3,K,3,3,C];
+// dx fp32 [N,H,W,C] (one split) or slabs (left unreduced).  Halo tiles 17 / 19 / 20 / 21.
+void conv_x3_dgrad_bnin(Tensor g, Tensor z, bool pool, Tensor scale, Tensor shift, Tensor coef, OptT dz3w, Tensor w3,
+                        Tensor dx, OptT slab, int64_t splits, int64_t tile, OptT sig, int64_t sig_val) {
+  need(g, "g");
+  need(z, "z");
+  need(scale, "scale");
+  need(shift, "shift");
+  need(coef, "coef");
+  need_planes(w3, "w3");
+  need(dx, "dx");
+  const int np = w3.size(0);
+  const int N = z.size(0), H = z.size(1), W = z.size(2), K = z.size(3);
+  const int C = w3.size(4);
+  TORCH_CHECK(w3.size(1) == K && w3.size(2) == 3 && w3.size(3) == 3, "conv_x3_dgrad_bnin: weight shape");
+  TORCH_CHECK(g.numel() == (int64_t)N * H * W * K / (pool ? 4 : 1), "conv_x3_dgrad_bnin: g shape");
+  TORCH_CHECK(scale.numel() == K && shift.numel() == K && coef.numel() >= 3 * K && K <= 512 && K % 32 == 0,
+              "conv_x3_dgrad_bnin: channels");
+  TORCH_CHECK(dx.numel() == (int64_t)N * H * W * C, "conv_x3_dgrad_bnin: dx shape");
+  u16* dzp = nullptr;
+  long dzps = 0;
+  if (dz3w.has_value() && dz3w->defined()) {
+    need_planes(*dz3w, "dz3w");
+    TORCH_CHECK(dz3w->size(0) == np && dz3w->numel() == np * z.numel(), "conv_x3_dgrad_bnin: dz3w shape");
+    dzp = up(*dz3w);
+    dzps = dz3w->stride(0);
+  }
+  float* sl = nullptr;
+  const int eff = dpa_x3_splits(9 * K, (int)splits);
+  if (eff > 1) {
+    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_dgrad_bnin: split-K needs a slab workspace");
+    need(*slab, "slab");
+    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * C, "conv_x3_dgrad_bnin: slab too small");
+    sl = fp(*slab);
+  }
+  chk(dpa_conv_x3_dgrad_bnin(fp(g), fp(z), pool ? 1 : 0, fp(scale), fp(shift), fp(coef), dzp, dzps, up(w3),
+                             w3.stride(0), fp(dx), sl, N, H, W, K, C, (int)splits, (int)tile, np, cur_stream(),
+                             opt_signal(sig, "conv_x3_dgrad_bnin"), (int)sig_val),
+      "conv_x3_dgrad_bnin");
+}
+
+// BN backward statistics only (reduce + finalize: dgamma, dbeta, dbias, coef); dz is formed on load
+// by the data-gradient conv (conv_x3_dgrad_bnin).  fp32, ReLU activation.
+void bn_bwd_stats(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean,
+                  Tensor invstd, Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias,
+                  bool pool, OptT sig, int64_t sig_val) {
+  need(gsrc, "gsrc");
+  need(g, "g");
+  need(z, "z");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
+  TORCH_CHECK(g.numel() == (int64_t)Mo * C, "bn_bwd_stats: g shape");
+  TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_bwd_stats: gsrc too small");
+  TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd_stats: part too small");
+  TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd_stats: coef too small");
+  chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
+                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), nullptr, nullptr, 0, N, H, W, C, pool ? 1 : 0, 0, nullptr,
+                 nullptr, 0, cur_stream(), opt_signal(sig, "bn_bwd_stats"), (int)sig_val, nullptr, nullptr),
+      "bn_bwd_stats");
 }
 
 // BN finalize from channel-major (mean, M2) partials [C][nblk] of row blocks of rpb rows (a conv
@@ -1096,6 +1218,33 @@ class PyRcclComm {
   dpa::RcclComm comm_;
 };
 
+// Peer-memory communicator (runtime/ipc_comm.cpp, kernels/ipc_allreduce.hip)
+class PyIpcComm {
+ public:
+  PyIpcComm(int rank, int world, int device, int64_t stage_floats) : c_(rank, world, device, (long)stage_floats) {}
+  py::bytes sig_handle() { return py::bytes(c_.sig_handle()); }
+  py::bytes stage_handle() { return py::bytes(c_.stage_handle()); }
+  static py::bytes tensor_handle(const Tensor& t) {
+    TORCH_CHECK(t.is_cuda(), "ipc: GPU tensor expected");
+    return py::bytes(dpa::IpcComm::export_handle(t.data_ptr()));
+  }
+  void set_peers(const std::vector<std::string>& sig, const std::vector<std::string>& stage) { c_.set_peers(sig, stage); }
+  int add_region(const std::vector<std::string>& handles, Tensor local) {
+    TORCH_CHECK(local.is_cuda() && local.is_contiguous() && local.scalar_type() == at::kFloat,
+                "ipc: region must be a contiguous fp32 GPU tensor");
+    return c_.add_region(handles, local.data_ptr<float>(), (long)local.numel());
+  }
+  void all_reduce(int id, int64_t off, int64_t n, int blocks, int64_t timeout_us) {
+    c_.all_reduce(id, (long)off, (long)n, blocks, (long long)timeout_us, cur_stream());
+  }
+  bool take_timeout() { return c_.take_timeout(); }
+  int rank() const { return c_.rank(); }
+  int world() const { return c_.world(); }
+
+ private:
+  dpa::IpcComm c_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -1114,6 +1263,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
   m.def("wflip", &wflip);
   m.def("x3_splits", &x3_splits);
+  m.def("conv_x3_dgrad_bnin", &conv_x3_dgrad_bnin, py::arg("g"), py::arg("z"), py::arg("pool"), py::arg("scale"),
+        py::arg("shift"), py::arg("coef"), py::arg("dz3w"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
+        py::arg("splits"), py::arg("tile"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
+  m.def("bn_bwd_stats", &bn_bwd_stats, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
+        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
+        py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("pool"),
+        py::arg("sig") = py::none(), py::arg("sig_val") = 0);
+  m.def("conv_x3_fprop_bnin", &conv_x3_fprop_bnin, py::arg("zin"), py::arg("pool"), py::arg("scale"),
+        py::arg("shift"), py::arg("a3w"), py::arg("w3"), py::arg("out"), py::arg("slab"), py::arg("splits"),
+        py::arg("tile"), py::arg("stats") = py::none());
   m.def("conv_x3_fprop", &conv_x3_fprop, py::arg("x3"), py::arg("w3"), py::arg("out"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
         py::arg("posmajor") = 0, py::arg("stats") = py::none());
@@ -1238,6 +1397,20 @@ PYBIND11_MODULE(_C, m) {
       .def("wait", &dpa::TcpStoreClient::wait, py::arg("keys"), py::arg("timeout_s") = -1.0,
            py::call_guard<py::gil_scoped_release>())
       .def("barrier", &dpa::TcpStoreClient::barrier, py::call_guard<py::gil_scoped_release>());
+  py::class_<PyIpcComm>(m, "IpcComm")
+      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("stage_floats"))
+      .def("sig_handle", &PyIpcComm::sig_handle)
+      .def("stage_handle", &PyIpcComm::stage_handle)
+      .def_static("tensor_handle", &PyIpcComm::tensor_handle)
+      .def("set_peers", &PyIpcComm::set_peers)
+      .def("add_region", &PyIpcComm::add_region)
+      .def("all_reduce", &PyIpcComm::all_reduce, py::arg("region"), py::arg("off"), py::arg("n"), py::arg("blocks"),
+           py::arg("timeout_us"))
+      .def("take_timeout", &PyIpcComm::take_timeout, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &PyIpcComm::rank)
+      .def_property_readonly("world", &PyIpcComm::world);
+  m.def("ipc_slice", [](int64_t n, int world) { return (int64_t)dpa_ipc_slice((long)n, world); });
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool, int>(), py::arg("rank"),
            py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("high_priority") = false,

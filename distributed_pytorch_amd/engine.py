@@ -331,6 +331,19 @@ class VGGEngine:
             if rows:
                 epart = max(epart, 2 * ((N * l.hw * l.hw + rows - 1) // rows) * l.cout)
         self.epart = torch.empty(max(epart, 1), **f32)
+        # Consumer-side BatchNorm, forward: a forward conv on a halo tile applies
+        # the previous layer's BN + ReLU (+ 2x2 max-pool) while it stages its operand from that layer's
+        # fp32 z (conv_x3.hip BNIN), so the bn_apply pass (or the one-launch BN's apply phase) and the
+        # read of its planes go; the conv also stores the planes for the weight-gradient conv.
+        # DPA_BN_ON_LOAD=0 keeps the apply passes (A/B).
+        self.bn_on_load = (dev.type == "cuda" and os.environ.get("DPA_BN_ON_LOAD", "0") == "1"
+                           and hasattr(self.K, "conv_x3_fprop_bnin"))
+        # ... and backward (item 1b): the data-gradient conv of layer i forms dz = k1*dy + k2*z + k3 on
+        # load from the summed g, z and the BN backward coefficients (conv_x3.hip BNIN 3/4) and stores
+        # dz's planes for the weight-gradient conv, which then waits for that conv to END (the next BN
+        # backward's start signal) instead of its start.  DPA_BN_BWD_ON_LOAD=0 keeps bn_bwd_apply.
+        self.bn_bwd_on_load = (dev.type == "cuda" and os.environ.get("DPA_BN_BWD_ON_LOAD", "0") == "1"
+                               and hasattr(self.K, "conv_x3_dgrad_bnin"))
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
@@ -618,14 +631,51 @@ class VGGEngine:
         tile, s, _ = self.conv_config(i, "fprop", n)
         return self.K.conv_stats_rows(tile) if s == 1 else 0
 
-    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool, stats: Optional[torch.Tensor] = None) -> int:
+    def _bnin(self, i: int, n: int) -> bool:
+        """Whether layer i's training forward conv applies layer i-1's BatchNorm on load (its input
+        planes are then written by that conv, not by a bn_apply pass)."""
+        key = ("bnin", i, n)
+        v = self._cfg_cache.get(key)
+        if v is None:
+            v = False
+            if self.bn_on_load and i > 0 and self.planes[i] and self.a3[i - 1] is not None:
+                lp = self.spec.convs[i - 1]
+                tile, _, _ = self.conv_config(i, "fprop", n)
+                v = (tile in (17, 19) and lp.cout % 32 == 0 and lp.cout <= 512
+                     and not (i == 1 and self.l0_recompute))  # (that path stores no z for layer 0)
+            self._cfg_cache[key] = v
+        return v
+
+    def _bnin_bwd(self, i: int, n: int) -> bool:
+        """Whether layer i's data-gradient conv applies layer i's BatchNorm backward on load (x3
+        planes, a halo tile, the three-kernel BN backward, kernel-start signals available)."""
+        key = ("bnin_bwd", i, n)
+        v = self._cfg_cache.get(key)
+        if v is None:
+            v = False
+            if (self.bn_bwd_on_load and i > 0 and self.planes[i] and self.np == 3
+                    and self.ksignal and self.free_signal and not self._fused(i, n, True)):
+                l = self.spec.convs[i]
+                tile, _, _ = self.conv_config(i, "dgrad", n)
+                v = tile in (17, 19, 20, 21) and l.cout % 32 == 0 and l.cout <= 512 and (not l.pool or l.hw % 2 == 0)
+            self._cfg_cache[key] = v
+        return v
+
+    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool, stats: Optional[torch.Tensor] = None,
+                  bnin: bool = False) -> int:
         """Forward conv of layer i into z[i] (or split-K slabs); returns the split count left
-        UNREDUCED in self.slab (1 = result is in z[i]).  stats: BN partials from the epilogue."""
+        UNREDUCED in self.slab (1 = result is in z[i]).  stats: BN partials from the epilogue.
+        bnin: apply layer i-1's BN on load (``_bnin``; training forward, slabs never reduced)."""
         l = self.spec.convs[i]
         tile, s, pm = self.conv_config(i, "fprop", n)
         self._ensure_slab(self._slab_need(i, "fprop", n))
         z = self.z[i][:n]
         slab = self.slab if s > 1 else None
+        if bnin:
+            lp, sp = self.spec.convs[i - 1], self.stats[i - 1]
+            self.K.conv_x3_fprop_bnin(self.z[i - 1][:n], lp.pool, sp["scale"], sp["shift"], self.a3[i - 1][:, :n],
+                                      self.w3[i], z, slab, s, tile, stats)
+            return s
         if self.planes[i]:
             self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm, stats)
         else:
@@ -641,6 +691,12 @@ class VGGEngine:
         self._ensure_slab(self._slab_need(i, "dgrad", n))
         slab = self.slab if s > 1 else None
         out = self.g[i - 1][:n]
+        if sig_val > 0 and self._bnin_bwd(i, n):
+            l, st = self.spec.convs[i], self.stats[i]
+            self.K.conv_x3_dgrad_bnin(self.g[i][:n], self.z[i][:n], l.pool, st["scale"], st["shift"], self.coef,
+                                      self.dz3[i][:, :n], self.w3[i], out, slab, s, tile, sig=self.ksig[i:i + 1],
+                                      sig_val=sig_val)
+            return s
         if self.planes[i]:
             if sig_val > 0:
                 self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm,
@@ -729,10 +785,12 @@ class VGGEngine:
                             P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
                             self.buffers[f"{l.bn_key}.running_var"], self.nbt[i:i + 1], st["mean"], st["invstd"],
                             st["scale"], st["shift"], self.bn_momentum, self.bn_eps)
-                K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
+                if not self._bnin(i + 1, n):
+                    K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
             erows = self._epi_rows(i, n)
-            ns = self._conv_fwd(i, x, n, reduce=False, stats=self.epart if erows else None)
+            nxt_bnin = i + 1 < len(L) and self._bnin(i + 1, n)  # the next conv applies this BN on load
+            ns = self._conv_fwd(i, x, n, reduce=False, stats=self.epart if erows else None, bnin=self._bnin(i, n))
             if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
                 buffers_wait()
                 buffers_wait = None
@@ -743,11 +801,12 @@ class VGGEngine:
                               self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                               self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
                               self.bn_momentum, self.bn_eps)
-                if not (i == len(L) - 1 and self.fused_head):
+                if not (i == len(L) - 1 and self.fused_head) and not nxt_bnin:
                     K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
             if self._fused(i, n, False):
-                head = i == len(L) - 1 and self.fused_head  # the head kernel applies it
+                # the head kernel, or the next conv, applies it: statistics and coefficients only
+                head = (i == len(L) - 1 and self.fused_head) or nxt_bnin
                 K.bn_fused_fwd(self.slab if ns > 1 else z, ns, z, l.pool, self.bn_fused_rmax, self.fpart, self.fcnt,
                                P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
                                self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
@@ -760,8 +819,8 @@ class VGGEngine:
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                            self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"], self.bn_momentum,
                            self.bn_eps)
-            if i == len(L) - 1 and self.fused_head:
-                continue  # applied inside the head kernel below
+            if (i == len(L) - 1 and self.fused_head) or nxt_bnin:
+                continue  # applied inside the head kernel below / by the next conv on load
             K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
         feat = self.a[-1][:n].view(n, -1)
         bn_in = (dict(bn_z=self.z[-1][:n], bn_scale=self.stats[-1]["scale"], bn_shift=self.stats[-1]["shift"])
@@ -797,7 +856,10 @@ class VGGEngine:
 
         def side_work(j: int, nm: List[str]):
             with torch.cuda.stream(ws):
-                K.wait_signal(self.ksig[j:j + 1], epoch, self.ksig_timeout_us, self.ksig_tmo)
+                # dz planes written by the data-gradient conv itself (BN backward on load): wait until
+                # it has ENDED, i.e. the next BN backward (layer j-1) has started
+                sig = self.bsig[j - 1:j] if self._bnin_bwd(j, n) else self.ksig[j:j + 1]
+                K.wait_signal(sig, epoch, self.ksig_timeout_us, self.ksig_tmo)
                 self._conv_wgrad(j, x, n)
                 if grad_ready is not None:
                     grad_ready(nm)
@@ -872,6 +934,10 @@ class VGGEngine:
                                self.fcnt, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
                                G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf,
                                self.bn_tmo, self.bn_fused_timeout_us, **bsig)
+            elif epoch and self._bnin_bwd(i, n):  # dz is formed on load by dgrad(i)
+                K.bn_bwd_stats(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
+                               st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
+                               G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], l.pool, **bsig)
             else:
                 K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                          st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],

@@ -268,14 +268,17 @@ def test_comm_plans_per_mode():
     import bench
 
     p = bench.comm_plans(bench.parse(["--mode", "ddp"]))
-    assert p[0] == (10.0, 2.0, False, 0) and len(p) == 5 and len(set(p)) == 5
-    assert {b for b, _, _, _ in p} == {10.0, 25.0, 5.0} and any(f for _, _, f, _ in p)
-    assert any(t < 2 for _, t, _, _ in p) and all(c == 0 for *_, c in p)
+    assert p[0] == (10.0, 2.0, False, 0, False) and len(p) == 5 and len(set(p)) == 5
+    assert {q[0] for q in p} == {10.0, 25.0, 5.0} and any(q[2] for q in p)
+    assert any(q[1] < 2 for q in p) and all(q[3] == 0 and not q[4] for q in p)
     p = bench.comm_plans(bench.parse(["--mode", "ddp", "--bucket-mb", "8"]))
-    assert {b for b, _, _, _ in p} == {8.0} and p[0] == (8.0, 2.0, False, 0)
-    assert bench.comm_plans(bench.parse(["--mode", "allreduce"])) == [(None, 2.0, False, 0), (None, 2.0, True, 0)]
+    assert {q[0] for q in p} == {8.0} and p[0] == (8.0, 2.0, False, 0, False)
+    assert bench.comm_plans(bench.parse(["--mode", "allreduce"])) == [(None, 2.0, False, 0, False),
+                                                                      (None, 2.0, True, 0, False)]
     assert bench.comm_plans(bench.parse(["--mode", "gather"])) == []
     assert bench.comm_plans(bench.parse(["--mode", "zero1"])) == []
+    p = bench.comm_plans(bench.parse(["--mode", "ddp"]), ipc=True)
+    assert p[-1] == (10.0, 2.0, False, 0, True) and len(p) == 6
 
 
 def test_comm_plans_rccl_channel_budgets(monkeypatch):
@@ -286,9 +289,10 @@ def test_comm_plans_rccl_channel_budgets(monkeypatch):
 
     monkeypatch.delenv("DPA_RCCL_CHANNELS", raising=False)
     p = bench.comm_plans(bench.parse(["--mode", "ddp"]), rccl=True)
-    assert p[0] == (10.0, 2.0, False, 0) and p[-2:] == [(10.0, 2.0, False, 16), (10.0, 2.0, False, 8)]
+    assert p[0] == (10.0, 2.0, False, 0, False)
+    assert p[-2:] == [(10.0, 2.0, False, 16, False), (10.0, 2.0, False, 8, False)]
     p = bench.comm_plans(bench.parse(["--mode", "allreduce", "--rccl-channels", "4"]), rccl=True)
-    assert p == [(None, 2.0, False, 0), (None, 2.0, True, 0), (None, 2.0, False, 4)]
+    assert p == [(None, 2.0, False, 0, False), (None, 2.0, True, 0, False), (None, 2.0, False, 4, False)]
     assert len(bench.comm_plans(bench.parse(["--mode", "ddp", "--rccl-channels", "off"]), rccl=True)) == 5
     monkeypatch.setenv("DPA_RCCL_CHANNELS", "12")
     assert len(bench.comm_plans(bench.parse(["--mode", "ddp"]), rccl=True)) == 5

@@ -117,3 +117,37 @@ def test_main_ddp_training_two_ranks(tmp_path):
     assert out.count("Epoch: 1, Iteration: 1-20, Average Loss:") == 2, out[-3000:]  # 20 iterations per rank
     assert out.count("Test set: Average loss:") == 2 and "/1024 (" in out, out[-3000:]
     assert (ck / "rank0.pt").exists() and (ck / "rank1.pt").exists()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_allreduce_ranks_share_one_gpu(world):
+    """the peer-memory all-reduce (HIP IPC mappings + one two-shot kernel per
+    collective) between 2 / 4 processes on one GPU: bitwise the rank-order fp32 sum, slices with
+    odd tails, nothing outside the slice touched, no wait timed out (tests/ipc_worker.py)."""
+    from distributed_pytorch_amd.parallel.spawn import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "tests", "ipc_worker.py")]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPA_STORE_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["world"] == world and d["bitwise_ok"] and not d["timeout"] and d["ipc_ops"] >= 5, d
+
+
+def test_ipc_ddp_matches_gloo(runs):
+    """Bucketed DDP with the bucket all-reduces on the peer-memory kernel (--ipc on, 2 ranks on one
+    GPU): replicas identical and -- a sum of two is exact in any order -- bitwise the parameters of
+    the gloo run of the same mode."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc",
+           "on", "--steps", "3", "--warmup", "2", "--solo-steps", "0", "--diag-steps", "1", "--launch-timeout", "100"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["replicas_identical"] is True and d["ipc_allreduce_ops"] and d["ipc_allreduce_ops"] > 0, d
+    if "ddp" in runs:
+        assert d["param_checksum"] == runs["ddp"]["param_checksum"], (d["param_checksum"], runs["ddp"]["param_checksum"])
