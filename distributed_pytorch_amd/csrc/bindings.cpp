@@ -1165,6 +1165,10 @@ class PyRcclComm {
     track(t);
     comm_.all_reduce(t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), cur_stream());
   }
+  void all_reduce_here(Tensor t, const std::string& op) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce_here: contiguous GPU tensor expected");
+    comm_.all_reduce_here(t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), cur_stream());
+  }
   void broadcast(Tensor t, int root) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "broadcast: contiguous GPU tensor expected");
     track(t);
@@ -1421,6 +1425,7 @@ PYBIND11_MODULE(_C, m) {
       .def("ops_issued", &PyRcclComm::ops_issued)
       .def("comm_count", &PyRcclComm::comm_count)
       .def("all_reduce", &PyRcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
+      .def("all_reduce_here", &PyRcclComm::all_reduce_here, py::arg("t"), py::arg("op") = "sum")
       .def("broadcast", &PyRcclComm::broadcast)
       .def("gather", &PyRcclComm::gather)
       .def("reduce_scatter", &PyRcclComm::reduce_scatter, py::arg("send"), py::arg("recv"), py::arg("op") = "sum")

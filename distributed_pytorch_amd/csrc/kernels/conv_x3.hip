@@ -1201,7 +1201,10 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   // j + 1 (one tap of latency; only one group's raw values live in registers), with the coefficients
   // from LDS ----
   constexpr int ZQ = BPOOL ? 4 : 1;
-  float4 rz[ZQ][2], rg[BWD ? 2 : 1];
+  // raw register sets: one per slot group when a group's raw values are small (no pooling window),
+  // so a chunk's loads are all in flight from its first tap on; one set (group by group) otherwise
+  constexpr int NZB = 1;  // (one set per group measured: spills to scratch in the 256x128 tile)
+  float4 rz[NZB][ZQ][2], rg[NZB][BWD ? 2 : 1];
   int z_off[BNIN ? NCA : 1];  // (fp32 z maps are < 2^31 elements: zbytes is a 32-bit range)
   int g_off[BWD ? NCA : 1];
   int z_u[BNIN == 4 ? NCA : 1];  // BNIN 4: the slot pixel's position in its pool window (scan order)
@@ -1238,14 +1241,15 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   auto load_zj = [&](int j, int c0) {
     if constexpr (BNIN != 0) {
       zc0 = c0;
+      const int b = j % NZB;
 #pragma unroll
       for (int qq = 0; qq < ZQ; ++qq)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-          rz[qq][h] = bload_f4(rzr, z_off[j] + (qq & 1) * a.C + (qq >> 1) * zrow + c0 + 4 * h, a_ok[j]);
+          rz[b][qq][h] = bload_f4(rzr, z_off[j] + (qq & 1) * a.C + (qq >> 1) * zrow + c0 + 4 * h, a_ok[j]);
       if constexpr (BWD) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) rg[h] = bload_f4(rgr, g_off[j] + c0 + 4 * h, a_ok[j]);
+        for (int h = 0; h < 2; ++h) rg[b][h] = bload_f4(rgr, g_off[j] + c0 + 4 * h, a_ok[j]);
       }
     }
   };
@@ -1275,12 +1279,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
         const float sc = k == 0 ? sc4[h].x : k == 1 ? sc4[h].y : k == 2 ? sc4[h].z : sc4[h].w;
         const float sh = k == 0 ? sh4[h].x : k == 1 ? sh4[h].y : k == 2 ? sh4[h].z : sh4[h].w;
         auto zq = [&](int qq) {
-          const float4& v = rz[qq][h];
+          const float4& v = rz[j % NZB][qq][h];
           return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
         };
         float y;
         if constexpr (BWD) {  // bn_bwd_apply_kernel: dy (route1 / the ReLU mask), then fma(k1, dy, fma(k2, z, k3))
-          const float gg = f4k(rg[h], k), k1 = f4k(k14[h], k), k2 = f4k(k24[h], k), k3 = f4k(k34[h], k);
+          const float gg = f4k(rg[j % NZB][h], k), k1 = f4k(k14[h], k), k2 = f4k(k24[h], k), k3 = f4k(k34[h], k);
           float dy, zz;
           if constexpr (BNIN == 4) {
             const float y00 = fmaxf(fmaf(zq(0), sc, sh), 0.f), y01 = fmaxf(fmaf(zq(1), sc, sh), 0.f);
@@ -1436,16 +1440,25 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   const int cb = blockIdx.y * a.cps, ce = min(nch, cb + a.cps);
   const int nsteps = max(0, ce - cb) * 9;
   if (BNIN != 0 && nsteps > 0) {
-    // Same steps and barriers as below with the 9 taps unrolled: slot group j of the next chunk is
-    // loaded at tap j and converted at tap j + 1, in the same straight-line code as those taps'
-    // MFMAs, so the conversion's VALU work fills MFMA gaps instead of a barrier-bound phase.
+    // Same steps and barriers as below with the 9 taps unrolled.  The next chunk's raw z (and g) is
+    // loaded after tap 0's MFMAs were issued (all slot groups at once when the raw values are small;
+    // otherwise group j after tap j's), and slot group j is converted after tap j + 1's MFMAs: the
+    // waits for those loads and the conversion's VALU work sit behind queued matrix work, in the same
+    // straight-line code as that tap.
     static_assert(NCA < 9, "BNIN pipeline");
     load_b(0, cb * BC);
     __syncthreads();  // bnc
+    if constexpr (NZB == NCA) {
 #pragma unroll
-    for (int j = 0; j < NCA; ++j) {
-      load_zj(j, cb * BC);
-      convert(j, true);
+      for (int j = 0; j < NCA; ++j) load_zj(j, cb * BC);
+#pragma unroll
+      for (int j = 0; j < NCA; ++j) convert(j, true);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NCA; ++j) {
+        load_zj(j, cb * BC);
+        convert(j, true);
+      }
     }
     store_a();
     store_b(0);
@@ -1457,9 +1470,18 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int st = st0 + tap;
-        if (tap >= 1 && tap <= NCA) convert(tap - 1, nxt);  // (no next chunk: unused, not stored)
-        if (tap < NCA && nxt) load_zj(tap, (ch + 1) * BC);
         compute(tap, st & 1);
+        if (tap >= 1 && tap <= NCA) convert(tap - 1, nxt);  // (no next chunk: unused, not stored)
+        if (nxt) {
+          if constexpr (NZB == NCA) {
+            if (tap == 0) {
+#pragma unroll
+              for (int j = 0; j < NCA; ++j) load_zj(j, (ch + 1) * BC);
+            }
+          } else if (tap < NCA) {
+            load_zj(tap, (ch + 1) * BC);
+          }
+        }
         if (st + 1 < nsteps) {
           store_b((st + 1) & 1);
           if (st + 2 < nsteps) load_b(tap == 8 ? 1 : (tap == 7 ? 0 : tap + 2), (tap >= 7 ? ch + 1 : ch) * BC);

@@ -158,10 +158,11 @@ int RcclComm::comm_count() {
   return n;
 }
 
-void RcclComm::end_op(const char* what) {
+void RcclComm::end_op(const char* what, hipStream_t on) {
   ops_issued_++;
+  if (on == nullptr) on = stream_;
   if (wd_.debug_sync) {  // host-synchronous op: surfaces ordering bugs and errors at the call site
-    hip_check(hipStreamSynchronize(stream_), what);
+    hip_check(hipStreamSynchronize(on), what);
     const std::string e = async_error();
     if (!e.empty()) throw std::runtime_error(std::string("RCCL error after ") + what + ": " + e);
     return;
@@ -177,7 +178,7 @@ void RcclComm::end_op(const char* what) {
       hip_check(hipEventCreateWithFlags(&ev, event_flags()), "hipEventCreate");
     }
   }
-  hip_check(hipEventRecord(ev, stream_), "hipEventRecord");
+  hip_check(hipEventRecord(ev, on), "hipEventRecord");
   std::lock_guard<std::mutex> g(mu_);
   ops_.push_back(Op{ev, std::chrono::steady_clock::now(), what});
 }
@@ -293,6 +294,15 @@ void RcclComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_
     check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
   }
   end_op("all_reduce");
+}
+
+void RcclComm::all_reduce_here(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t stream) {
+  {
+    Lock g(comm_mu_);
+    require_healthy_locked();
+    check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream), "ncclAllReduce");
+  }
+  end_op("all_reduce", stream);
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t after) {

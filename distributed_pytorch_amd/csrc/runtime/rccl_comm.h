@@ -63,6 +63,10 @@ class RcclComm {
   // All ops: comm stream waits for everything already queued on `after` (the compute stream),
   // then runs the collective.  Returns immediately.
   void all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t after);
+  // the same collective issued on `stream` itself (no comm-stream hop): the caller orders it after
+  // every earlier collective of this communicator (a join with the comm stream) -- the last bucket
+  // of a backward, whose update follows on that stream
+  void all_reduce_here(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t stream);
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t after);
   // Rank `root` receives world*count elements into recv (its own contribution copied in place).
   void gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t after);
@@ -89,7 +93,9 @@ class RcclComm {
   void check(ncclResult_t r, const char* what);
   // throws if the communicator is not healthy; caller holds comm_mu_
   void require_healthy_locked();
-  void end_op(const char* what);  // track completion (or sync in debug mode); caller does NOT hold comm_mu_
+  // track completion (or sync in debug mode) of an op issued on `on` (default: the comm stream);
+  // caller does NOT hold comm_mu_
+  void end_op(const char* what, hipStream_t on = nullptr);
   void watchdog_loop();
   void fail(const std::string& msg);  // watchdog thread only
   void release_locked(bool abort);    // caller holds comm_mu_

@@ -43,6 +43,14 @@ class Comm:
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         raise NotImplementedError
 
+    def all_reduce_here(self, t: torch.Tensor, op: str = "sum"):
+        """The collective ordered on the CURRENT stream: after everything issued on it so far and
+        every earlier collective, before what follows on it.  Generic form: a region + a wait;
+        RcclComm issues it on the current stream itself (no comm-stream hop)."""
+        with self.region():
+            self.all_reduce(t, op)
+        self.wait()
+
     def broadcast(self, t: torch.Tensor, root: int = 0):
         raise NotImplementedError
 
@@ -266,6 +274,10 @@ class RcclComm(Comm):
 
     def all_reduce(self, t, op="sum"):
         self._c.all_reduce(t, op)
+
+    def all_reduce_here(self, t, op="sum"):
+        self.wait()  # every earlier collective of this communicator first (one hop: comm -> current)
+        self._c.all_reduce_here(t, op)
 
     def broadcast(self, t, root=0):
         self._c.broadcast(t, root)

@@ -108,6 +108,14 @@ class IpcComm(Comm):
         self._c.all_reduce(rid, off, t.numel(), self.blocks, int(self.timeout_s * 1e6))
         self.ipc_ops += 1
 
+    def all_reduce_here(self, t: torch.Tensor, op: str = "sum"):
+        if not self.ipc_eligible(t, op):
+            return self.inner.all_reduce_here(t, op)
+        self.inner.wait()  # earlier collectives (RCCL or peer kernels on the comm stream) first
+        rid, off = self._region_of(t)
+        self._c.all_reduce(rid, off, t.numel(), self.blocks, int(self.timeout_s * 1e6))
+        self.ipc_ops += 1
+
     def broadcast(self, t, root=0):
         self.inner.broadcast(t, root)
 
