@@ -215,6 +215,20 @@ def ipc_comm(ctx, dev, engine, cache: dict):
     return cache["ipc"]
 
 
+def ipc_agrees(ipc, flat: torch.Tensor, dev) -> bool:
+    """All-reduce the gradient arena (as the last tuning step left it) through the peer kernel and,
+    from a copy, through the wrapped communicator; True when they agree to rounding."""
+    ref = flat.clone()
+    with ipc.region():
+        ipc.inner.all_reduce(ref)
+        ipc.all_reduce(flat)
+    ipc.wait()
+    torch.cuda.synchronize(dev)
+    err = (flat - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    return err <= 1e-5 * max(scale, 1e-30) and not ipc._c.take_timeout()
+
+
 def tune_comm(a, engine, sync, ctx, dev, batches):
     """Warmup-phase choice among ``comm_plans``: each plan runs ``--comm-tune-steps`` steps per
     repetition (2 repetitions, interleaved); the score of a plan is its best repetition's time,
@@ -261,11 +275,14 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
             benchlib.device_barrier(ctx, dev)
             el = ctx.all_max(time.perf_counter() - t0) / n * 1e3
             score[p] = min(score.get(p, el), el)
-    # a plan whose peer-memory waits timed out (any rank) is disqualified
+    # a plan whose peer-memory waits timed out (any rank), or whose all-reduce of the real gradient
+    # arena disagrees with the communicator's (beyond summation-order rounding), is disqualified
     if "ipc" in comms:
         bad = ctx.all_max(1.0 if comms["ipc"]._c.take_timeout() else 0.0) > 0
+        if not bad:
+            bad = ctx.all_max(0.0 if ipc_agrees(comms["ipc"], engine.grads.flat, dev) else 1.0) > 0
         if bad:
-            print(f"[rank {ctx.rank}] comm tuner: IPC all-reduce timed out; plan dropped", flush=True)
+            print(f"[rank {ctx.rank}] comm tuner: IPC all-reduce timed out or disagreed; plan dropped", flush=True)
             plans = [p for p in plans if not p[4]]
     # the first plan is the default: another one must beat it by 1 % (run-to-run noise of a few
     # steps), so the choice does not flap between equivalent plans
