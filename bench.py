@@ -418,7 +418,10 @@ def main(argv=None):
             "hip_graph": graphed is not None and graphed.graph is not None,
             "data": "synthetic (CIFAR-10-shaped uint8 on device, random-crop/flip/normalize each step)",
             "config": {"model": a.model, "global_batch": a.batch * ctx.world, "seq_len": None, "image_size": 32,
-                       "parallelism": f"dp{ctx.world}", "sync_mode": a.mode, "comm": ctx.comm.name,
+                       "parallelism": f"dp{ctx.world}",
+                       # one rank without a communicator runs no collective at all
+                       "sync_mode": a.mode if sync.active else f"none (1 rank, no collectives; {a.mode} requested)",
+                       "comm": ctx.comm.name,
                        "bucket_mb": [round(4 * b.numel / 2 ** 20, 3) for b in sync.buckets] if sync.active else None,
                        "per_bucket_update": bool(sync.fuse_step), "comm_tune": tune_report,
                        "overlap": not a.no_overlap, "launcher": launcher,
