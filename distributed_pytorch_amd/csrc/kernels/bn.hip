@@ -30,6 +30,14 @@
 #include <cstdlib>
 #include <type_traits>
 
+extern "C" {  // bn_wide.hip: bf16 apply passes with 16-byte lanes (return 1: not applicable)
+int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,
+                      const float* scale, const float* shift, long M, int C, int act, hipStream_t st);
+int dpa_bn_bwd_apply_wide(const unsigned short* g, const unsigned short* g2, const unsigned short* z,
+                          unsigned short* dz, const float* scale, const float* shift, const float* coef, long M, int C,
+                          int act, hipStream_t st);
+}
+
 namespace {
 
 constexpr int RT = 1024;  // forward-statistics block size
@@ -837,6 +845,12 @@ void bn_apply_launch(int act, int grid, hipStream_t st, const TZ* z, float* a, u
 template <typename TZ>
 int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H, int W,
                   int C, int pool, int act, const TZ* res, hipStream_t st, unsigned char* mask = nullptr) {
+  if constexpr (sizeof(TZ) == 2) {  // bf16 in, one bf16 plane out: 16-byte lanes (bn_wide.hip)
+    if (!pool && np == 1) {
+      const int rc = dpa_bn_apply_wide(z, res, a3, mask, scale, shift, (long)N * H * W, C, act, st);
+      if (rc != 1) return rc;
+    }
+  }
   const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   const long ps = total * 4;
   const int grid = grid_ch(total, C / 4);
@@ -1078,6 +1092,12 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
                                                                         // by its consumer (conv_x3.hip BNIN 3/4)
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
+  if constexpr (sizeof(TZ) == 2) {  // bf16 in, one bf16 plane out: 16-byte lanes (bn_wide.hip)
+    if (!pool && np == 1 && act != 2) {
+      const int rc = dpa_bn_bwd_apply_wide(gg, g2, z, dz3, scale, shift, coef, (long)Mo, C, act, st);
+      if (rc != 1) return rc;
+    }
+  }
   const long total = (long)Mo * (C / 4);
   const long ps = (long)N * H * W * C;
   const int grid = grid_ch(total, C / 4);

@@ -29,9 +29,10 @@
 // dispatcher places them in order, so the rendezvous can only stall while other kernels (the
 // weight-gradient stream, RCCL) hold the CUs it needs -- they never wait for this kernel, so the
 // stall ends when they do.  The geometry query refuses (the engine then runs the three-kernel BN)
-// any grid above 512 blocks or above half of the chip's co-resident capacity for this kernel
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs, or DPA_BN_FUSED_CAP blocks when set: tests
-// force the fallback with it).  A block that waits longer than `ticks` of the wall clock (the
+// any grid above 512 blocks and any slice of R blocks above half of the chip's co-resident capacity
+// for this kernel (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs, or DPA_BN_FUSED_CAP blocks
+// when set: tests force the fallback with it) -- half, so a slice still fits while the other
+// stream's kernels hold the rest of the chip.  A block that waits longer than `ticks` of the wall clock (the
 // engine's own short bound, DPA_BN_FUSED_TIMEOUT_US, 2 s by default) sets tmo[0] = 1 and continues
 // (garbage, never a hang; the engine raises on the word after the step).
 #include "common.h"
@@ -613,7 +614,7 @@ constexpr int GRID_MAX = 512;
 bool pick_geo_resident(int Mo, int C, bool pool, bool bwd, int rmax, Geo& g) {
   if (!pick_geo(Mo, C, pool, bwd, rmax, g)) return false;
   const long grid = (long)g.slices * g.R;
-  return grid <= GRID_MAX && 2 * grid <= resident_capacity(bwd, pool, g);
+  return grid <= GRID_MAX && 2L * g.R <= resident_capacity(bwd, pool, g);
 }
 
 template <int CL>
