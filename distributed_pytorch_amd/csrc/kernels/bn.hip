@@ -36,6 +36,10 @@ int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsign
 int dpa_bn_bwd_apply_wide(const unsigned short* g, const unsigned short* g2, const unsigned short* z,
                           unsigned short* dz, const float* scale, const float* shift, const float* coef, long M, int C,
                           int act, hipStream_t st);
+int dpa_bn_bwd_reduce_wide(const unsigned short* g, const unsigned short* g2, const unsigned short* z,
+                           const unsigned short* res, const unsigned char* mask, unsigned short* dyout,
+                           const float* scale, const float* shift, const float* mean, const float* invstd,
+                           float* part, int Mo, int C, int act, int rpb, int* sig, int sig_val, hipStream_t st);
 }
 
 namespace {
@@ -897,16 +901,24 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = bwd_rows_per_block(Mo, C);
-  const int nblk = (Mo + rpb - 1) / rpb;
+  int nblk = (Mo + rpb - 1) / rpb;
   const bool wide = bwd_wide(Mo, C);
-#define RED(P, A)                                                                                                 \
+  int nw = 0;  // bf16 in the 1024-thread geometry: 16-byte lanes (bn_wide.hip)
+  if constexpr (sizeof(TZ) == 2) {
+    if (wide && !pool && nsplit == 1)
+      nw = dpa_bn_bwd_reduce_wide(gsrc, g2, z, res, mask, dyout, scale, shift, mean, invstd, part, Mo, C, act, rpb,
+                                  sig, sig_val, st);
+  }
+#define RED(P, A)                                                                                               \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
                                                             N, H, W, C, rpb, sig, sig_val, g2, mask, dyout);            \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
                                                               part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout)
-  if (pool) {
+  if (nw > 0) {
+    nblk = nw;
+  } else if (pool) {
     RED(true, 0);
   } else if (act == 0) {
     RED(false, 0);

@@ -135,6 +135,104 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_wide_kernel(const uint4* __r
   for (; i < total8; i += stride) body(g[i], g2 ? g2[i] : make_uint4(0u, 0u, 0u, 0u), z[i], i);
 }
 
+// Backward reduce (bn.hip bn_bwd_reduce_kernel's 1024-thread geometry, bf16, unpooled, unsplit):
+// per (row block, channel) sums of dy, dy*xhat and xhat, with dy = g (+ g2) through the ReLU of
+// ACT 0, as is (ACT 1), or through the add+ReLU of ACT 2 (mask from the forward, or the residual),
+// dy stored to dyout for ACT 2 (the residual's gradient).  C/8 threads per row, 1024/(C/8) rows per
+// iteration, two rows' loads in flight; rows summed in order, then the fixed-order LDS tree (the
+// row partition differs from bn.hip's, so sums agree to rounding, not bitwise).  part: [block][3][C]
+// as bn.hip's, finalized by the same kernel.
+constexpr int RTW = 1024;
+
+__device__ __forceinline__ float4 f4sum(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int ACT, bool MK>
+__global__ __launch_bounds__(RTW) void bn_bwd_reduce_wide_kernel(
+    const uint4* __restrict__ g, const uint4* __restrict__ g2, const uint4* __restrict__ z,
+    const uint4* __restrict__ res, const unsigned short* __restrict__ mask, uint4* __restrict__ dyout,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float* __restrict__ part, int Mo, int C8, int rpb, int* sig, int sig_val) {
+  start_signal(sig, sig_val);
+  const int t = threadIdx.x;
+  const int RPI = RTW / C8;
+  const int lane_c = t % C8, lane_r = t / C8;
+  const bool active = lane_r < RPI;
+  const int r0 = blockIdx.x * rpb, r1 = min(Mo, r0 + rpb);
+  float sdy[8] = {}, sdx[8] = {}, sx[8] = {};
+  if (active) {
+    float sc[8], sh[8], mu[8], is[8];
+    coef8(scale, lane_c, sc);
+    coef8(shift, lane_c, sh);
+    coef8(mean, lane_c, mu);
+    coef8(invstd, lane_c, is);
+    constexpr bool mk = ACT == 2 && MK;  // ReLU mask of the forward (else the residual)
+    auto row = [&](uint4 gv, uint4 hv, uint4 zv, uint4 rv, unsigned m, long gi) {
+      float gf[8], zf[8], rf[8], dyv[8];
+      unpack8(gv, gf);
+      unpack8(zv, zf);
+      if (g2) {
+        float hf[8];
+        unpack8(hv, hf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gf[e] += hf[e];
+      }
+      if (ACT == 2 && !mk) unpack8(rv, rf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float dy;
+        if (ACT == 2 && mk) {
+          dy = ((m >> (e < 4 ? e : e + 4)) & 1u) ? gf[e] : 0.f;
+        } else {
+          const float u = fmaf(zf[e], sc[e], sh[e]);
+          dy = ACT == 0 ? (u > 0.f ? gf[e] : 0.f) : ACT == 1 ? gf[e] : ((u + rf[e]) > 0.f ? gf[e] : 0.f);
+        }
+        const float xh = (zf[e] - mu[e]) * is[e];
+        sdy[e] += dy;
+        sdx[e] = fmaf(dy, xh, sdx[e]);
+        sx[e] += xh;
+        dyv[e] = dy;
+      }
+      if (ACT == 2 && dyout) dyout[gi] = pack8(dyv);
+    };
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    int r = r0 + lane_r;
+    for (; r + RPI < r1; r += 2 * RPI) {
+      const long i0 = (long)r * C8 + lane_c, i1 = i0 + (long)RPI * C8;
+      const uint4 ga = g[i0], gb = g[i1];
+      const uint4 ha = g2 ? g2[i0] : zero, hb = g2 ? g2[i1] : zero;
+      const uint4 za = z[i0], zb = z[i1];
+      const uint4 ra = ACT == 2 && !mk ? res[i0] : zero, rb = ACT == 2 && !mk ? res[i1] : zero;
+      const unsigned ma = mk ? mask[i0] : 0u, mb = mk ? mask[i1] : 0u;
+      row(ga, ha, za, ra, ma, i0);
+      row(gb, hb, zb, rb, mb, i1);
+    }
+    for (; r < r1; r += RPI) {
+      const long i0 = (long)r * C8 + lane_c;
+      row(g[i0], g2 ? g2[i0] : zero, z[i0], ACT == 2 && !mk ? res[i0] : zero, mk ? mask[i0] : 0u, i0);
+    }
+  }
+  __shared__ float4 shb[RTW];
+  float* o = part + (long)blockIdx.x * 3 * (8 * C8) + lane_c * 8;
+  const int C = 8 * C8;
+  int p2 = 1;
+  while (p2 < RPI) p2 <<= 1;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {  // (sum dy, sum dy*xhat, sum xhat) x (channels 0-3, 4-7 of the group)
+    const float* v = q < 2 ? sdy : q < 4 ? sdx : sx;
+    const int h = (q & 1) * 4;
+    shb[t] = make_float4(v[h], v[h + 1], v[h + 2], v[h + 3]);
+    __syncthreads();
+    for (int off = p2 >> 1; off >= 1; off >>= 1) {
+      if (active && lane_r < off && lane_r + off < RPI) shb[t] = f4sum(shb[t], shb[t + off * C8]);
+      __syncthreads();
+    }
+    if (active && lane_r == 0) *reinterpret_cast<float4*>(o + (q >> 1) * C + h) = shb[t];
+    __syncthreads();
+  }
+}
+
 // grid: <= 8192 blocks of 256 threads, the stride a multiple of C8 (one channel group per thread)
 int grid_wide(long total8, int C8) {
   long g = (total8 + 255) / 256;
@@ -155,9 +253,46 @@ bool wide_on() {
   return !(e && e[0] == '0');
 }
 
+bool wide_red_on() {
+  const char* e = getenv("DPA_BN_WIDE_RED");  // read per call: tests switch it in-process
+  return wide_on() && !(e && e[0] == '0');
+}
+
 }  // namespace
 
 extern "C" {
+// Backward reduce for bf16, unpooled, unsplit tensors in bn.hip's 1024-thread geometry: rpb is
+// bn.hip's rows per block (rounded up here to whole iterations, so the grid never exceeds its and
+// the partial workspace fits).  Returns the number of blocks launched (the finalize's partial
+// rows), 0 when not applicable (the caller runs bn.hip's kernel), or -(HIP error).
+int dpa_bn_bwd_reduce_wide(const unsigned short* g, const unsigned short* g2, const unsigned short* z,
+                           const unsigned short* res, const unsigned char* mask, unsigned short* dyout,
+                           const float* scale, const float* shift, const float* mean, const float* invstd,
+                           float* part, int Mo, int C, int act, int rpb, int* sig, int sig_val, hipStream_t st) {
+  if (!wide_red_on() || C % 8 || C / 8 > RTW || act < 0 || act > 2 || (act == 2 && !mask && !res)) return 0;
+  if ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(g2) | reinterpret_cast<uintptr_t>(z) |
+       reinterpret_cast<uintptr_t>(res) | reinterpret_cast<uintptr_t>(dyout)) & 15 ||
+      reinterpret_cast<uintptr_t>(mask) & 1)
+    return 0;
+  const int C8 = C / 8, RPI = RTW / C8;
+  const int rw = (rpb + RPI - 1) / RPI * RPI;
+  const int nblk = (Mo + rw - 1) / rw;
+  const uint4 *gg = reinterpret_cast<const uint4*>(g), *hh = reinterpret_cast<const uint4*>(g2),
+              *zz = reinterpret_cast<const uint4*>(z), *rr = reinterpret_cast<const uint4*>(res);
+  const unsigned short* mm = reinterpret_cast<const unsigned short*>(mask);
+  uint4* dd = reinterpret_cast<uint4*>(dyout);
+#define LAUNCH(A, M)                                                                                               \
+  bn_bwd_reduce_wide_kernel<A, M><<<nblk, RTW, 0, st>>>(gg, hh, zz, rr, mm, dd, scale, shift, mean, invstd, part, Mo, \
+                                                     C8, rw, sig, sig_val)
+  if (act == 0) LAUNCH(0, false);
+  else if (act == 1) LAUNCH(1, false);
+  else if (mask) LAUNCH(2, true);
+  else LAUNCH(2, false);
+#undef LAUNCH
+  const int e = (int)hipGetLastError();
+  return e ? -e : nblk;
+}
+
 // bf16 [M][C] -> bf16 [M][C] (+ mask [M*C/4] bytes for act 2); returns 1 when not applicable (the
 // caller runs bn.hip's kernel), else a HIP error code
 int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,

@@ -290,7 +290,7 @@ __device__ __forceinline__ void epi_col_stats(const f32x16 (&acc)[TM][TN], int r
       const float* o = sh + (r * BNC + c) * 3;
       w = ew_merge(w, EWelford{o[0], o[1], o[2]});
     }
-    if (c < ncols) part[(long)c * nblk + bm] = make_float2(w.mean, w.m2);
+    if (c < ncols) part[c * nblk + bm] = make_float2(w.mean, w.m2);  // < BNC * nblk: 32-bit index
   }
 }
 

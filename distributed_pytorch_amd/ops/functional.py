@@ -261,6 +261,56 @@ def clear_deferred():
     """Drop deferred contributions of an abandoned backward (called at every training forward)."""
     _DEFERRED.clear()
     _STATS.clear()
+    _SIDE_STATE["armed"] = False  # an abandoned backward's end-of-pass join never ran
+
+
+# Weight gradients on a second stream (the VGG engine's two-stream backward, for autograd): a conv's
+# wgrad reads only its saved input and dz, and nothing in the backward reads dW, so it runs on a
+# per-device side stream behind an event of the compute stream while the compute stream continues
+# with the data gradient, the BatchNorm backwards and the next layers (bandwidth-bound BN passes
+# beside MFMA-bound weight gradients).  Joins: the compute stream waits for the side stream at the
+# end of every backward pass (an autograd engine callback, so plain ``loss.backward()`` users see
+# final .grad), and a collective that reads gradients mid-backward (parallel/ddp.py) joins it into
+# the communicator's stream first (``wgrad_join``).  Tensors the side stream reads are
+# ``record_stream``-ed, so the caching allocator cannot hand their memory to the compute stream early.
+# DPA_WGRAD_STREAM=0: every wgrad on the compute stream (A/B).
+WGRAD_STREAM = os.environ.get("DPA_WGRAD_STREAM", "1") == "1"
+_SIDE: Dict[torch.device, torch.cuda.Stream] = {}
+_SIDE_STATE = {"armed": False, "pending": set()}
+
+
+def _wgrad_side(dev: torch.device) -> Optional["torch.cuda.Stream"]:
+    if not (WGRAD_STREAM and dev.type == "cuda") or _AUTOTUNE["on"]:
+        return None
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def wgrad_join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
+    """Order ``stream`` (default: the current stream) after every weight gradient queued so far on
+    the side stream of ``device`` (default: every device with pending side work)."""
+    devs = [torch.device(device)] if device is not None else list(_SIDE_STATE["pending"])
+    for d in devs:
+        s = _SIDE.get(d)
+        if s is not None and d in _SIDE_STATE["pending"]:
+            (stream or torch.cuda.current_stream(d)).wait_stream(s)
+
+
+def _arm_end_join(main: "torch.cuda.Stream", dev: torch.device):
+    """Once per backward pass: the compute stream joins the side stream when the pass ends."""
+    _SIDE_STATE["pending"].add(dev)
+    if _SIDE_STATE["armed"]:
+        return
+
+    def join():
+        _SIDE_STATE["armed"] = False
+        main.wait_stream(_SIDE[dev])
+        _SIDE_STATE["pending"].discard(dev)
+
+    _SIDE_STATE["armed"] = True
+    torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 class GradJoin:
@@ -452,14 +502,25 @@ class Conv2dNHWC(torch.autograd.Function):
             dw = grad_slot(ctx.w_param)
             if dw is None:
                 dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
+            side = _wgrad_side(dz.device)
+            skey = "slab" if side is None else "wslab"  # the side stream's own split-K slab
 
             def run_w(tile, s, pm):
-                slab = WS.get("slab", s * K * R * S * C, dz.device) if s > 1 else None
+                slab = WS.get(skey, s * K * R * S * C, dz.device) if s > 1 else None
                 Kx.conv_x3_wgrad(xp, dzp, dw, slab, stride, pad, s, tile, pm)
 
             cfg = choose_config(ctx.impl, "wgrad", geom, N * P * Q, K, R * S * C, P * Q <= 16, run_w,
                                 lambda s: 4 * s * K * R * S * C)
-            run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
+            if side is None:
+                run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
+            else:
+                main = torch.cuda.current_stream(dz.device)
+                side.wait_stream(main)
+                _arm_end_join(main, dz.device)
+                with torch.cuda.stream(side):
+                    run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
+                for t in (xp, dzp, dw):
+                    t.record_stream(side)
         if dx is not None and ctx.cx != C:
             dx = dx[..., :ctx.cx].contiguous()
         if join is not None and dx is not None and addend is None:

@@ -266,14 +266,14 @@ def test_bn_fused_residency_guard_falls_back(monkeypatch):
 
     C_ = _C()
     assert C_.bn_fused_geo(256 * 4, 512, True, False, 64) is not None
-    monkeypatch.setenv("DPA_BN_FUSED_CAP", "8")
+    monkeypatch.setenv("DPA_BN_FUSED_CAP", "1")
     assert C_.bn_fused_geo(256 * 4, 512, True, False, 64) is None
     torch.manual_seed(0)
     x = torch.zeros(64, 32, 32, 4, device="cuda")
     x[..., :3] = torch.randn(64, 32, 32, 3, device="cuda")
     t = torch.randint(0, 10, (64,), device="cuda")
     res = []
-    for cap in ("8", None):
+    for cap in ("1", None):
         if cap is None:
             monkeypatch.delenv("DPA_BN_FUSED_CAP")
         eng = VGGEngine("VGG11", "cuda", max_batch=64, impl="x3")

@@ -506,3 +506,51 @@ def test_resnet_staged_epilogue_bitwise(monkeypatch, impl):
     assert torch.equal(out[0][0], out[1][0])
     for n in out[0][1]:
         assert torch.equal(out[0][1][n], out[1][1][n]), n
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_wgrad_side_stream_bitwise(monkeypatch, graph):
+    """Weight gradients on the side stream (functional.WGRAD_STREAM) give bitwise the gradients of
+    the one-stream backward, eager and replayed as a captured HIP graph (bench_resnet.py's step),
+    and the compute stream has joined the side stream when backward returns."""
+    from distributed_pytorch_amd.models.resnet import ResNet
+    from distributed_pytorch_amd.ops import functional as Fn
+    from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel, FlatSGD
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(16, 64, 64, 3, device="cuda", generator=g)
+    t = torch.randint(0, 10, (16,), device="cuda", generator=g)
+    out = []
+    for side in (False, True):
+        monkeypatch.setattr(Fn, "WGRAD_STREAM", side)
+        torch.manual_seed(0)
+        m = ResNet([1, 1, 1, 1], 10, impl="bf16").cuda()
+        ddp = DistributedDataParallel(m)
+        opt = FlatSGD(ddp, lr=0.01, momentum=0.9)
+        one = torch.ones((), device="cuda")
+
+        def step():
+            opt.zero_grad()
+            loss = F.cross_entropy(ddp(x), t)
+            loss.backward(one)
+            opt.step(ddp.finish())
+            return loss
+
+        for _ in range(2):
+            step()
+        if graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                step()
+            gr.replay()
+        else:
+            step()
+        torch.cuda.synchronize()
+        out.append((ddp.flat_grads.clone(), ddp.flat_params.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])

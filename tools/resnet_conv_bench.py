@@ -73,9 +73,13 @@ def main():
         ins_t = (wt,) if stem else (xt, wt)
         th_b = timeit(lambda: torch.autograd.grad(F.conv2d(xt, wt, stride=s, padding=p), ins_t, dzt),
                       a.iters) - th_f
+        xw = x.detach()  # weight gradient alone (no data gradient requested)
+        ours_w = timeit(lambda: torch.autograd.grad(Fn.conv2d_nhwc(xw, w, s, p, "bf16"), (w,), dz), a.iters) - ours_f
         row = {"shape": [N, H, W, C, K, R, s, p], "count": cnt, "ours_fwd": round(ours_f, 1),
-               "ours_bwd": round(ours_b, 1), "miopen_fwd": round(th_f, 1), "miopen_bwd": round(th_b, 1)}
+               "ours_bwd": round(ours_b, 1), "ours_wgrad": round(ours_w, 1), "miopen_fwd": round(th_f, 1),
+               "miopen_bwd": round(th_b, 1)}
         tot["ours"] += cnt * (ours_f + ours_b)
+        tot["ours_wgrad"] += cnt * ours_w
         tot["miopen"] += cnt * (th_f + th_b)
         best_gemm = None
         if R == 1 and s == 1:
@@ -86,6 +90,7 @@ def main():
             g_f = timeit(lambda: x2 @ w2.t(), a.iters)
             g_b = timeit(lambda: (dz2 @ w2, dz2.t() @ x2), a.iters)
             row["gemm_fwd"], row["gemm_bwd"] = round(g_f, 1), round(g_b, 1)
+            row["gemm_wgrad"] = round(timeit(lambda: dz2.t() @ x2, a.iters), 1)
             best_gemm = g_f + g_b
         tot["best"] += cnt * min(ours_f + ours_b, th_f + th_b, best_gemm or 1e18)
         print(json.dumps(row), flush=True)
