@@ -262,6 +262,7 @@ def clear_deferred():
     _DEFERRED.clear()
     _STATS.clear()
     _SIDE_STATE["armed"] = False  # an abandoned backward's end-of-pass join never ran
+    _SIDE_STATE["queue"] = []
 
 
 # Weight gradients on a second stream (the VGG engine's two-stream backward, for autograd): a conv's
@@ -273,14 +274,26 @@ def clear_deferred():
 # final .grad), and a collective that reads gradients mid-backward (parallel/ddp.py) joins it into
 # the communicator's stream first (``wgrad_join``).  Tensors the side stream reads are
 # ``record_stream``-ed, so the caching allocator cannot hand their memory to the compute stream early.
-# DPA_WGRAD_STREAM=0: every wgrad on the compute stream (A/B).
-WGRAD_STREAM = os.environ.get("DPA_WGRAD_STREAM", "1") == "1"
+# Only a weight whose gradient autograd adopts without a kernel takes this path (no .grad yet, one
+# use in the forward): an accumulation or a multi-use sum would read dW on the compute stream.
+# DPA_WGRAD_STREAM=1 turns it on (default off); DPA_WGRAD_BATCH=k: the side stream forks from the
+# compute stream once per k weight gradients (they queue until then; fewer cross-stream edges in a
+# captured graph), default 1.  Measured on ResNet-50 (bench_resnet.py, HIP-graph replay, same box,
+# interleaved): one stream 9,175-9,201 img/s; side stream 8,950-8,988; batched forks k = 3 / 8:
+# 8,896-8,942 / 8,917-8,929 (an earlier box: 8,982-8,990 vs 8,966-9,061).  The replayed graph
+# leaves ~0.9 ms per step idle around the cross-stream edges and the overlapped kernels slow each
+# other (kernel time 14.2 -> 16.5 ms); the eager step overlaps better but is host-bound and erratic
+# (9,467 and 7,402 img/s).  docs/PERF_NOTES.md, round 4.
+WGRAD_STREAM = os.environ.get("DPA_WGRAD_STREAM", "0") == "1"
+WGRAD_BATCH = max(1, int(os.environ.get("DPA_WGRAD_BATCH", "1")))
 _SIDE: Dict[torch.device, torch.cuda.Stream] = {}
-_SIDE_STATE = {"armed": False, "pending": set()}
+_SIDE_STATE = {"armed": False, "pending": set(), "queue": []}
 
 
-def _wgrad_side(dev: torch.device) -> Optional["torch.cuda.Stream"]:
+def _wgrad_side(dev: torch.device, w: torch.Tensor) -> Optional["torch.cuda.Stream"]:
     if not (WGRAD_STREAM and dev.type == "cuda") or _AUTOTUNE["on"]:
+        return None
+    if w.grad is not None or getattr(w, "_dpa_uses", 1) != 1:
         return None
     s = _SIDE.get(dev)
     if s is None:
@@ -288,9 +301,28 @@ def _wgrad_side(dev: torch.device) -> Optional["torch.cuda.Stream"]:
     return s
 
 
+def _flush_side():
+    """Launch the queued weight gradients on their side streams, behind their compute streams."""
+    q = _SIDE_STATE["queue"]
+    if not q:
+        return
+    _SIDE_STATE["queue"] = []
+    forked = set()
+    for main, dev, run, keep in q:
+        side = _SIDE[dev]
+        if (main, dev) not in forked:
+            side.wait_stream(main)
+            forked.add((main, dev))
+        with torch.cuda.stream(side):
+            run()
+        for t in keep:
+            t.record_stream(side)
+
+
 def wgrad_join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
     """Order ``stream`` (default: the current stream) after every weight gradient queued so far on
     the side stream of ``device`` (default: every device with pending side work)."""
+    _flush_side()
     devs = [torch.device(device)] if device is not None else list(_SIDE_STATE["pending"])
     for d in devs:
         s = _SIDE.get(d)
@@ -298,14 +330,19 @@ def wgrad_join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> Non
             (stream or torch.cuda.current_stream(d)).wait_stream(s)
 
 
-def _arm_end_join(main: "torch.cuda.Stream", dev: torch.device):
-    """Once per backward pass: the compute stream joins the side stream when the pass ends."""
+def _side_submit(main: "torch.cuda.Stream", dev: torch.device, run: Callable[[], None], keep) -> None:
+    """Queue one weight gradient for the side stream (launched at once when WGRAD_BATCH is 1) and
+    arm the end-of-backward join."""
     _SIDE_STATE["pending"].add(dev)
+    _SIDE_STATE["queue"].append((main, dev, run, keep))
+    if len(_SIDE_STATE["queue"]) >= WGRAD_BATCH:
+        _flush_side()
     if _SIDE_STATE["armed"]:
         return
 
     def join():
         _SIDE_STATE["armed"] = False
+        _flush_side()
         main.wait_stream(_SIDE[dev])
         _SIDE_STATE["pending"].discard(dev)
 
@@ -502,7 +539,7 @@ class Conv2dNHWC(torch.autograd.Function):
             dw = grad_slot(ctx.w_param)
             if dw is None:
                 dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
-            side = _wgrad_side(dz.device)
+            side = _wgrad_side(dz.device, ctx.w_param)
             skey = "slab" if side is None else "wslab"  # the side stream's own split-K slab
 
             def run_w(tile, s, pm):
@@ -514,13 +551,9 @@ class Conv2dNHWC(torch.autograd.Function):
             if side is None:
                 run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
             else:
-                main = torch.cuda.current_stream(dz.device)
-                side.wait_stream(main)
-                _arm_end_join(main, dz.device)
-                with torch.cuda.stream(side):
-                    run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
-                for t in (xp, dzp, dw):
-                    t.record_stream(side)
+                sk = Kx.x3_splits(N * P * Q, cfg[1])
+                _side_submit(torch.cuda.current_stream(dz.device), dz.device,
+                             lambda: run_w(cfg[0], sk, cfg[2]), (xp, dzp, dw))
         if dx is not None and ctx.cx != C:
             dx = dx[..., :ctx.cx].contiguous()
         if join is not None and dx is not None and addend is None:
