@@ -34,7 +34,8 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val,
-               const void* g2, const unsigned char* mask);
+               const void* g2, const unsigned char* mask, unsigned* tick);
+long dpa_bn_tick_words(int M, int C);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -465,9 +466,19 @@ void conv_x3_dgrad_bnin(Tensor g, Tensor z, bool pool, Tensor scale, Tensor shif
 
 // BN backward statistics only (reduce + finalize: dgamma, dbeta, dbias, coef); dz is formed on load
 // by the data-gradient conv (conv_x3_dgrad_bnin).  fp32, ReLU activation.
+// tick (optional): int32 counter words, zeroed once, for the backward reduce's ticketed finalize
+// (bn.hip TICK: no separate finalize launch); they re-arm themselves after every launch
+unsigned* tick_ptr(const OptT& tick, int Mo, int C, const char* what) {
+  if (!tick.has_value() || !tick->defined()) return nullptr;
+  TORCH_CHECK(tick->is_cuda() && tick->is_contiguous() && tick->scalar_type() == torch::kInt32 &&
+                  tick->numel() >= dpa_bn_tick_words(Mo, C),
+              what, ": tick must be a contiguous int32 CUDA tensor of bn_tick_words(M, C) zeroed words");
+  return reinterpret_cast<unsigned*>(tick->data_ptr<int32_t>());
+}
+
 void bn_bwd_stats(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean,
                   Tensor invstd, Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias,
-                  bool pool, OptT sig, int64_t sig_val) {
+                  bool pool, OptT sig, int64_t sig_val, OptT tick) {
   need(gsrc, "gsrc");
   need(g, "g");
   need(z, "z");
@@ -479,7 +490,8 @@ void bn_bwd_stats(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale,
   TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd_stats: coef too small");
   chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
                  fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), nullptr, nullptr, 0, N, H, W, C, pool ? 1 : 0, 0, nullptr,
-                 nullptr, 0, cur_stream(), opt_signal(sig, "bn_bwd_stats"), (int)sig_val, nullptr, nullptr),
+                 nullptr, 0, cur_stream(), opt_signal(sig, "bn_bwd_stats"), (int)sig_val, nullptr, nullptr,
+                 tick_ptr(tick, Mo, C, "bn_bwd_stats")),
       "bn_bwd_stats");
 }
 
@@ -878,7 +890,7 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask, OptT tick) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
@@ -928,7 +940,8 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   }
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp),
+                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp,
+                 tick_ptr(tick, Mo, C, "bn_bwd")),
       "bn_bwd");
 }
 
@@ -1273,7 +1286,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_stats", &bn_bwd_stats, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
         py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("pool"),
-        py::arg("sig") = py::none(), py::arg("sig_val") = 0);
+        py::arg("sig") = py::none(), py::arg("sig_val") = 0, py::arg("tick") = py::none());
   m.def("conv_x3_fprop_bnin", &conv_x3_fprop_bnin, py::arg("zin"), py::arg("pool"), py::arg("scale"),
         py::arg("shift"), py::arg("a3w"), py::arg("w3"), py::arg("out"), py::arg("slab"), py::arg("splits"),
         py::arg("tile"), py::arg("stats") = py::none());
@@ -1302,7 +1315,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
-        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none());
+        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none(),
+        py::arg("tick") = py::none());
+  m.def("bn_tick_words", [](int64_t M, int64_t C) { return (int64_t)dpa_bn_tick_words((int)M, (int)C); });
   m.def("bn_fused_geo", &bn_fused_geo, py::arg("Mo"), py::arg("C"), py::arg("pool"), py::arg("bwd"),
         py::arg("rmax"));
   m.def("bn_fused_fwd", &bn_fused_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),

@@ -505,8 +505,98 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // dyout (ACT 2, optional): the gradient through the add+ReLU, dy = relu'(u + r) * (g + g2), is
 // stored here (it is the residual's gradient dres); the apply pass then reads dy alone (ACT 1)
 // instead of g, g2 and the mask again.
+// Ticketed finalize (TICK): the reduce kernel finishes the statistics itself instead of a separate
+// bn_bwd_finalize launch, in bn_bwd_finalize_kernel<8>'s exact summation order (bitwise the same
+// coefficients).  Each block stores its partial row device-coherently (agent-scope stores, written
+// through the XCD's L2) and takes a ticket on the counter of its residue group (block % TG); the
+// group's last block sums the group's rows in ascending block order (the finalize's per-thread
+// strided sum) into a level-2 row and takes a ticket on the kernel's counter; the last of those
+// combines the TG group sums with the finalize's LDS tree order and writes dgamma, dbeta, dbias and the
+// apply coefficients.  No block waits for another (no residency assumption); counters re-arm
+// themselves (the next launch is stream-ordered behind this one).
+constexpr int TG = 32;  // = 256 / 8: bn_bwd_finalize_kernel<8>'s row groups
+struct FinArgs {
+  unsigned* tick;  // [1 + TG] zeroed words
+  float* part2;    // [TG][3][C]
+  const float* gamma;
+  float *dgamma, *dbeta, *dbias, *coef;
+  float Mfull;
+};
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st4_agent(float* p, float4 v) {
+  st_agent(p, v.x);
+  st_agent(p + 1, v.y);
+  st_agent(p + 2, v.z);
+  st_agent(p + 3, v.w);
+}
+// thread 0 takes a ticket on *ctr (n takers); true in every thread of the block that drew the last
+__device__ __forceinline__ bool last_ticket(unsigned* ctr, unsigned n, unsigned* flag) {
+  typedef __attribute__((address_space(1))) unsigned gu32;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's device-coherent stores are acked
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned v = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = v == n - 1;
+    if (last) {
+      __hip_atomic_store((gu32*)ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0u;
+}
+template <int NT>
+__device__ void ticket_finalize(const FinArgs& f, const float* part, int nblk, int C, const float* mean,
+                                const float* invstd, unsigned* flag) {
+  const int grp = blockIdx.x % TG, ng = nblk < TG ? nblk : TG;
+  if (!last_ticket(f.tick + 1 + grp, (unsigned)((nblk - 1 - grp) / TG + 1), flag)) return;
+  for (int q = threadIdx.x; q < 3 * C; q += NT) {  // level 1: rows grp, grp + TG, ... in order
+    float a = 0.f;
+    int k = grp;
+    for (; k + 7 * TG < nblk; k += 8 * TG) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(k + u * TG) * 3 * C + q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; k < nblk; k += TG) a += part[(long)k * 3 * C + q];
+    st_agent(f.part2 + (long)grp * 3 * C + q, a);
+  }
+  if (!last_ticket(f.tick, (unsigned)ng, flag)) return;
+  for (int c = threadIdx.x; c < C; c += NT) {  // level 2: bn_bwd_finalize_kernel<8>'s LDS tree order
+    float r[3];
+#pragma unroll 1
+    for (int j = 0; j < 3; ++j) {  // one quantity at a time: 32 live values, not 96
+      float v[TG];
+#pragma unroll
+      for (int g = 0; g < TG; ++g) v[g] = g < ng ? f.part2[((long)g * 3 + j) * C + c] : 0.f;
+#pragma unroll
+      for (int h = TG / 2; h >= 1; h >>= 1)
+#pragma unroll
+        for (int g = 0; g < h; ++g) v[g] += v[g + h];
+      r[j] = v[0];
+    }
+    const float sdy = r[0], sdx = r[1], sx = r[2];
+    const float iv = invstd[c], gm = f.gamma[c];
+    const float k1 = gm * iv;
+    const float k2x = -k1 * sdx / f.Mfull;
+    const float k3 = -k1 * sdy / f.Mfull;
+    f.dgamma[c] = sdx;
+    f.dbeta[c] = sdy;
+    if (f.dbias) f.dbias[c] = k2x * sx;
+    f.coef[c] = k1;
+    f.coef[C + c] = k2x * iv;
+    f.coef[2 * C + c] = k3 - k2x * iv * mean[c];
+  }
+}
+
 // part layout: [block][3][C]
-template <bool POOL, int ACT, typename TZ, int RTB>
+template <bool POOL, int ACT, typename TZ, int RTB, bool TICK = false>
 __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
                                                             int nsplit, const TZ* __restrict__ z,
                                                             const TZ* __restrict__ res,
@@ -518,7 +608,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             int rpb, int* sig, int sig_val,
                                                             const TZ* __restrict__ g2,
                                                             const unsigned char* __restrict__ mask,
-                                                            TZ* __restrict__ dyout) {
+                                                            TZ* __restrict__ dyout, FinArgs fin = FinArgs{}) {
   start_signal(sig, sig_val);
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
@@ -637,9 +727,18 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
       sh[0][t] = vals[q];
       __syncthreads();
       tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-      if (cval && lane_r == 0) *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
+      if (cval && lane_r == 0) {
+        if constexpr (TICK)
+          st4_agent(o + q * C, sh[0][t]);
+        else
+          *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
+      }
       __syncthreads();
     }
+  }
+  if constexpr (TICK) {
+    __shared__ unsigned flag;
+    ticket_finalize<RTB>(fin, part, gridDim.x, C, mean, invstd, &flag);
   }
 }
 
@@ -897,12 +996,17 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
                   const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                   float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
                   hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
-                  const unsigned char* mask = nullptr, TZ* dyout = nullptr) {
+                  const unsigned char* mask = nullptr, TZ* dyout = nullptr, unsigned* tick = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   const int rpb = bwd_rows_per_block(Mo, C);
   int nblk = (Mo + rpb - 1) / rpb;
   const bool wide = bwd_wide(Mo, C);
+  // ticketed finalize inside the reduce (256-thread geometry; part holds the level-2 rows after the
+  // block rows, dpa_bn_part_floats; its order is the 8-channel finalize's)
+  const bool ticked = tick != nullptr && !wide && fin_cpb() == 8;
+  FinArgs fin{};
+  if (ticked) fin = FinArgs{tick, part + (long)nblk * 3 * C, gamma, dgamma, dbeta, dbias, coef, (float)N * H * W};
   int nw = 0;  // bf16 in the 1024-thread geometry: 16-byte lanes (bn_wide.hip)
   if constexpr (sizeof(TZ) == 2) {
     if (wide && !pool && nsplit == 1)
@@ -913,6 +1017,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
                                                             N, H, W, C, rpb, sig, sig_val, g2, mask, dyout);            \
+  else if (ticked)                                                                                                \
+    bn_bwd_reduce_kernel<P, A, TZ, RTB, true><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean,    \
+                                                                    invstd, part, N, H, W, C, rpb, sig, sig_val, g2, \
+                                                                    mask, dyout, fin);                               \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
                                                               part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout)
@@ -928,6 +1036,7 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
     RED(false, 2);
   }
 #undef RED
+  if (ticked && nw <= 0) return;  // the reduce finalized
   if (fin_cpb() == 8)
     bn_bwd_finalize_kernel<8><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
                                                           dgamma, dbeta, dbias, coef);
@@ -1083,7 +1192,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                 const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2,
-                const unsigned char* mask) {
+                const unsigned char* mask, unsigned* tick) {
   if (nsplit < 1) nsplit = 1;
   // add+ReLU: the reduce pass stores dy (= dres) and the apply pass reads it alone as an identity
   // activation (DPA_BN_DY_PASS=0: the apply re-reads g, g2 and the mask / residual)
@@ -1091,7 +1200,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
   const bool dy_pass = !(dy_env && dy_env[0] == '0');
   const bool dyp = dy_pass && act == 2 && nsplit == 1 && !pool && dres != nullptr;
   bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
-                   C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr);
+                   C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr, tick);
   if (dyp) {
     act = 1;
     gsrc = dres;
@@ -1135,7 +1244,15 @@ extern "C" {
 long dpa_bn_part_floats(int M, int C, int bwd) {
   const int rpb = bwd ? bwd_rows_per_block(M, C) : red_rows_per_block(M, C);
   const long nblk = (M + rpb - 1) / rpb;
-  return nblk * C * (bwd ? 3 : 2);
+  // backward: the block rows, then the ticketed finalize's level-2 rows (bn_bwd_reduce_kernel TICK)
+  return bwd ? (nblk + TG) * C * 3 : nblk * C * 2;
+}
+
+// counter words the ticketed backward finalize needs (zeroed once; they re-arm themselves)
+long dpa_bn_tick_words(int M, int C) {
+  (void)M;
+  (void)C;
+  return 1 + TG;
 }
 
 // z [M][C] (or nsplit fp32 slabs of it in src; then z is written) -> partials -> finalize.
@@ -1198,7 +1315,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2,
-               const unsigned char* mask) {
+               const unsigned char* mask, unsigned* tick) {
   bn_unroll_init();
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && ((!res && !mask) || !dres))) return -2;
   if (mask && act != 2) return -2;
@@ -1207,10 +1324,10 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask);
+                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask, tick);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st, sig, sig_val, (const float*)g2, mask);
+                            (float*)dres, st, sig, sig_val, (const float*)g2, mask, tick);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.

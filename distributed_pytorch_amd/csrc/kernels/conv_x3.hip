@@ -1085,6 +1085,7 @@ struct HArgs {
   const float* gin;
   unsigned gbytes;
   const float* bcoef;  // k1 [C], k2 [C], k3 [C]
+  int dbg;  // EXPERIMENT: bit 0 skip B stores, 1 skip B loads, 2 skip A stores, 3 skip A loads
 };
 
 // staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
@@ -1502,17 +1503,18 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
     if (cb + 1 < ce) load_a((cb + 1) * BC);
     __syncthreads();
     int tap = 0, ch = cb;
+    const int dbg = a.dbg;
     for (int st = 0; st < nsteps; ++st) {
       compute(tap, st & 1);
       const bool last_tap = tap == 8;
       const int tap1 = last_tap ? 0 : tap + 1, ch1 = last_tap ? ch + 1 : ch;  // step st + 1
       if (st + 1 < nsteps) {
-        store_b((st + 1) & 1);
-        if (st + 2 < nsteps) load_b(tap1 == 8 ? 0 : tap1 + 1, (tap1 == 8 ? ch1 + 1 : ch1) * BC);
+        if (!(dbg & 1)) store_b((st + 1) & 1);
+        if (st + 2 < nsteps && !(dbg & 2)) load_b(tap1 == 8 ? 0 : tap1 + 1, (tap1 == 8 ? ch1 + 1 : ch1) * BC);
         if (last_tap) {  // every wave is done with this chunk's image before it is replaced
           __syncthreads();
-          store_a();
-          if (ch + 2 < ce) load_a((ch + 2) * BC);
+          if (!(dbg & 4)) store_a();
+          if (ch + 2 < ce && !(dbg & 8)) load_a((ch + 2) * BC);
         }
       }
       __syncthreads();
@@ -2247,6 +2249,10 @@ int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
 }
 
 // -6: the conv does not fit the halo tile (channels, or rows wider than BM/4 - 1 pixels)
+inline int halo_dbg() {  // EXPERIMENT (staging cost bounds): DPA_HALO_DBG bit mask, read per call
+  const char* e = getenv("DPA_HALO_DBG");
+  return e ? atoi(e) : 0;
+}
 template <bool DG>
 int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st,
              const void* add = nullptr) {
@@ -2257,6 +2263,7 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
   a.gm = cdiv(a.M, BM);
   a.gn = cdiv(a.Nout, halo_bn(tile));
   a.sepi = ob_epi();
+  a.dbg = halo_dbg();
   a.cps = cdiv(a.C / BC, splits);
   a.out = splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;

@@ -202,6 +202,7 @@ class VGGEngine:
         self.stats = []  # per layer dict(mean, invstd, scale, shift)
         self.eval_ss = []
         part_need = 1
+        tick_need = 0
         for i, l in enumerate(L):
             hw, ho = l.hw, (l.hw // 2 if l.pool else l.hw)
             nxt_planes = i + 1 < len(L) and self.planes[i + 1]
@@ -221,6 +222,7 @@ class VGGEngine:
             M, Mo = N * hw * hw, N * ho * ho
             part_need = max(part_need, self.K.bn_part_floats(M, l.cout, False),
                             self.K.bn_part_floats(Mo, l.cout, True))
+            tick_need = max(tick_need, self.K.bn_tick_words(Mo, l.cout) if hasattr(self.K, "bn_tick_words") else 0)
         # Weight gradients run on a second HIP stream (DPA_WGRAD_STREAM=0: one stream): wgrad(i) needs
         # only dz(i) and the stored forward activation, so it runs beside dgrad(i) and the BN
         # backward of layer i-1, whose reduce/finalize kernels leave most CUs idle.  It has its own
@@ -346,6 +348,11 @@ class VGGEngine:
                                and hasattr(self.K, "conv_x3_dgrad_bnin"))
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
+        # Ticketed BN-backward finalize (bn.hip TICK): the reduce kernel's last blocks finalize the
+        # statistics, so the main stream runs no separate finalize launch per layer (DPA_BN_TICK=0:
+        # bn_bwd_finalize as before).  Counter words zeroed once; they re-arm themselves.
+        self.bn_tick = (torch.zeros(max(tick_need, 1), device=dev, dtype=torch.int32)
+                        if dev.type == "cuda" and tick_need and os.environ.get("DPA_BN_TICK", "1") == "1" else None)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
         self.loss_row = torch.zeros(N, **f32)
         self.dlogits = torch.zeros(N, num_classes, **f32)
@@ -937,11 +944,11 @@ class VGGEngine:
             elif epoch and self._bnin_bwd(i, n):  # dz is formed on load by dgrad(i)
                 K.bn_bwd_stats(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                                st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                               G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], l.pool, **bsig)
+                               G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], l.pool, tick=self.bn_tick, **bsig)
             else:
                 K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                          st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig)
+                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, tick=self.bn_tick, **bsig)
             after_bn(i)
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.

@@ -276,7 +276,7 @@ def clear_deferred():
 # ``record_stream``-ed, so the caching allocator cannot hand their memory to the compute stream early.
 # Only a weight whose gradient autograd adopts without a kernel takes this path (no .grad yet, one
 # use in the forward): an accumulation or a multi-use sum would read dW on the compute stream.
-# DPA_WGRAD_STREAM=1 turns it on (default off); DPA_WGRAD_BATCH=k: the side stream forks from the
+# DPA_GENERIC_WGRAD_STREAM=1 turns it on (default off); DPA_WGRAD_BATCH=k: the side stream forks from the
 # compute stream once per k weight gradients (they queue until then; fewer cross-stream edges in a
 # captured graph), default 1.  Measured on ResNet-50 (bench_resnet.py, HIP-graph replay, same box,
 # interleaved): one stream 9,175-9,201 img/s; side stream 8,950-8,988; batched forks k = 3 / 8:
@@ -284,7 +284,7 @@ def clear_deferred():
 # leaves ~0.9 ms per step idle around the cross-stream edges and the overlapped kernels slow each
 # other (kernel time 14.2 -> 16.5 ms); the eager step overlaps better but is host-bound and erratic
 # (9,467 and 7,402 img/s).  docs/PERF_NOTES.md, round 4.
-WGRAD_STREAM = os.environ.get("DPA_WGRAD_STREAM", "0") == "1"
+WGRAD_STREAM = os.environ.get("DPA_GENERIC_WGRAD_STREAM", "0") == "1"
 WGRAD_BATCH = max(1, int(os.environ.get("DPA_WGRAD_BATCH", "1")))
 _SIDE: Dict[torch.device, torch.cuda.Stream] = {}
 _SIDE_STATE = {"armed": False, "pending": set(), "queue": []}

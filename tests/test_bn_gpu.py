@@ -110,9 +110,13 @@ def test_bn_three_kernel_forward(shape):
     assert int(nbt_d.item()) == 1
 
 
-@pytest.mark.parametrize("shape", BN_SHAPES)
+@pytest.mark.parametrize("shape", BN_SHAPES + [(256, 16, 16, 128, True), (256, 8, 8, 256, False)])
 @pytest.mark.parametrize("nsplit", [1, 2])
-def test_bn_three_kernel_backward(shape, nsplit):
+@pytest.mark.parametrize("ticked", [False, True])
+def test_bn_three_kernel_backward(shape, nsplit, ticked):
+    """ticked: the reduce kernel finalizes the statistics itself (bn.hip TICK, two levels of
+    tickets, the finalize kernel's summation order): run twice on the same counters, which must be
+    re-armed (zero) after each launch, and bitwise equal to the separate finalize launch."""
     C_ = _C()
     N, H, W, C, pool = shape
     g, z, gamma, beta, bias, rm, rv, gout = _inputs(shape, 1)
@@ -130,9 +134,22 @@ def test_bn_three_kernel_backward(shape, nsplit):
     else:
         half = torch.randn(gout.shape, generator=g)
         src, gbuf = d(torch.stack([half, gout - half]).reshape(-1)), torch.empty(gout.shape, device="cuda")
-    C_.bn_bwd(src, nsplit, gbuf, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, out[0], out[1],
-              out[2], dz, pool)
+    tick = (torch.zeros(C_.bn_tick_words(N * Ho * Wo, C), dtype=torch.int32, device="cuda") if ticked else None)
+    for _ in range(2 if ticked else 1):
+        coef.fill_(float("nan"))
+        C_.bn_bwd(src, nsplit, gbuf, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, out[0],
+                  out[1], out[2], dz, pool, tick=tick)
     torch.cuda.synchronize()
+    if ticked:
+        assert int(tick.abs().sum().item()) == 0, "ticket counters not re-armed"
+        assert torch.isfinite(coef).all()
+        ref_out = [torch.zeros(C, device="cuda") for _ in range(3)]
+        ref_coef, ref_dz = torch.empty(3 * C, device="cuda"), torch.empty(z.shape, device="cuda")
+        C_.bn_bwd(src, nsplit, gbuf, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, ref_coef,
+                  ref_out[0], ref_out[1], ref_out[2], ref_dz, pool)
+        torch.cuda.synchronize()
+        assert torch.equal(coef, ref_coef) and torch.equal(dz, ref_dz)
+        assert all(torch.equal(a_, b_) for a_, b_ in zip(out, ref_out))
     close(gbuf, gout, 1e-5, "g")
     close(dz, ref["dz"], 2e-5, "dz")
     close(out[0], ref["dgamma"], 2e-5, "dgamma")
