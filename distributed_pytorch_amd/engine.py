@@ -348,11 +348,14 @@ class VGGEngine:
                                and hasattr(self.K, "conv_x3_dgrad_bnin"))
         # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
         self.part = torch.zeros(part_need, **f32)
-        # Ticketed BN-backward finalize (bn.hip TICK): the reduce kernel's last blocks finalize the
-        # statistics, so the main stream runs no separate finalize launch per layer (DPA_BN_TICK=0:
-        # bn_bwd_finalize as before).  Counter words zeroed once; they re-arm themselves.
+        # Ticketed BN-backward finalize (bn.hip TICK, DPA_BN_TICK=1): the reduce kernel's last blocks
+        # finalize the statistics (bitwise the finalize kernel's result), so the main stream runs no
+        # separate finalize launch per layer.  Off by default: same-box A/B 176.0k (finalize launch)
+        # vs 170.5k img/s (ticketed) -- the serial two-level tail inside the reduce, behind
+        # device-coherent stores and an agent-scope acquire, outlasts the launch it saves
+        # (docs/PERF_NOTES.md, round 4).  Counter words zeroed once; they re-arm themselves.
         self.bn_tick = (torch.zeros(max(tick_need, 1), device=dev, dtype=torch.int32)
-                        if dev.type == "cuda" and tick_need and os.environ.get("DPA_BN_TICK", "1") == "1" else None)
+                        if dev.type == "cuda" and tick_need and os.environ.get("DPA_BN_TICK", "0") == "1" else None)
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
         self.loss_row = torch.zeros(N, **f32)
         self.dlogits = torch.zeros(N, num_classes, **f32)
