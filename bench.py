@@ -81,6 +81,11 @@ def parse(argv=None):
     ap.add_argument("--rccl-channels", default="16,8",
                     help="N>1 with the native RCCL communicator: channel (workgroup) budgets the comm tuner also "
                          "tries, each on its own communicator (comma list; 'off' = RCCL's default only)")
+    ap.add_argument("--defer-update", default="auto", choices=["auto", "on", "off"],
+                    help="run each step's SGD at the start of the next step on the weight-gradient stream, idle "
+                         "during the forward (engine.defer_update; bitwise the same updates; the timed region ends "
+                         "with the last step's update).  auto = DPA_DEFER_UPDATE=1 (default 0: same-box A/B 172.0k immediate vs 163.5k "
+                         "deferred img/s, docs/PERF_NOTES.md); never with a HIP graph")
     ap.add_argument("--profile", action="store_true",
                     help="re-run this command under rocprofv3 --kernel-trace --stats (prints the command)")
     ap.add_argument("--profile-dir", default="gpurun_out/prof")
@@ -247,6 +252,7 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     if ctx.world <= 1 or a.comm_tune == "off" or len(plans) < 2 or a.no_overlap:
         return sync, None
     it = batches()
+    engine.flush_update()
     snap = [t.clone() for t in (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt,
                                 engine.loss_accum)]
     steps_taken = engine.steps_taken
@@ -371,7 +377,12 @@ def main(argv=None):
     it = batches()
     graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
                if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
-    el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev)
+    engine.defer_update = (a.defer_update == "on" or (a.defer_update == "auto" and
+                                                      os.environ.get("DPA_DEFER_UPDATE", "0") == "1")) \
+        and graphed is None and dev.type == "cuda"
+    # the flush after the timed loop keeps the last step's (deferred) update inside the timed region
+    el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev,
+                              flush=engine.flush_update)
     engine.check_signals()
     loss = float(engine.loss.item())
     ms = el / a.steps * 1e3
@@ -392,6 +403,7 @@ def main(argv=None):
         sync.__dict__.pop("finish", None)  # drop make_step's probe wrapper
         diag = step_comm_report(samples, len(sync.buckets))
         diag["exposed_comm_ms"] = ctx.all_max(diag["exposed_comm_ms"] or 0.0)
+    engine.flush_update()
     benchlib.device_barrier(ctx, dev)
     pdiff = benchlib.replicas_max_diff(ctx.comm, engine.params.flat)
     if dev.type == "cuda":
@@ -425,6 +437,7 @@ def main(argv=None):
                        "bucket_mb": [round(4 * b.numel / 2 ** 20, 3) for b in sync.buckets] if sync.active else None,
                        "per_bucket_update": bool(sync.fuse_step), "comm_tune": tune_report,
                        "overlap": not a.no_overlap, "launcher": launcher,
+                       "deferred_update": bool(engine.defer_update),
                        "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
             "per_gpu_img_s": round(per_gpu, 1),
             "solo_img_s": round(solo_img_s, 1) if solo_img_s else None,

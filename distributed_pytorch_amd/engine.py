@@ -356,6 +356,23 @@ class VGGEngine:
         # (docs/PERF_NOTES.md, round 4).  Counter words zeroed once; they re-arm themselves.
         self.bn_tick = (torch.zeros(max(tick_need, 1), device=dev, dtype=torch.int32)
                         if dev.type == "cuda" and tick_need and os.environ.get("DPA_BN_TICK", "0") == "1" else None)
+        # Deferred optimizer step (``defer_update``, set by the caller, e.g. bench.py): the update of
+        # step k runs at the start of step k+1 on the weight-gradient stream -- idle during the forward
+        # -- instead of at the end of step k on the main stream.  Layer 0's slice still runs at once
+        # (its conv is the next kernel to read parameters); the main stream waits for layers 1-3 before
+        # conv 1 and for the rest (layers 4.., the classifier) before conv 4, long after they finished.
+        # Same kernels, same slices of the same element-wise update: results are bitwise those of the
+        # immediate step.  Measured slower (VGG-11 x3: 172.0k immediate vs 163.5k img/s deferred, same
+        # box): the update's 184 MB stream competes with the forward's BatchNorm passes and the two
+        # cross-stream waits sit on the main stream -- off unless the caller sets it.  Anything that reads the parameters or momenta from outside the step calls
+        # ``flush_update()`` first (state_dict, evaluation, loading, broadcast, the bench's timed region).
+        self.defer_update = False
+        self._pending_upd = None  # (grad_scale, first) of a deferred update not yet issued
+        self._upd_ev = [DevEvent(), DevEvent(), DevEvent()] if dev.type == "cuda" else None
+        self._upd_wait: Dict[int, DevEvent] = {}
+        los = [self.params.offsets[f"{l.conv_key}.weight"] for l in L]
+        nl = len(L)
+        self._upd_cut = (los[min(1, nl - 1)], los[min(4, nl - 1)], self.params.flat.numel())
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
         self.loss_row = torch.zeros(N, **f32)
         self.dlogits = torch.zeros(N, num_classes, **f32)
@@ -394,6 +411,7 @@ class VGGEngine:
 
     @torch.no_grad()
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        self.flush_update()
         sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
         seen = set()
         for l in self.spec.convs:
@@ -422,12 +440,14 @@ class VGGEngine:
         """Re-split the parameter arena into the bf16 operand planes (one launch).  Needed after
         parameters change outside ``sgd_step`` (load, broadcast); the SGD kernel refreshes them
         itself."""
+        self.flush_update()
         if self.wplanes is not None:
             self.K.split_planes(self.params.flat, self.wplanes)
 
     @torch.no_grad()
     def state_dict(self, prefix: str = "") -> "OrderedDict[str, torch.Tensor]":
         """Reference-layout state_dict (58 keys for VGG-11, OIHW fp32, CPU tensors)."""
+        self.flush_update()
         out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         for i, l in enumerate(self.spec.convs):
             out[prefix + f"{l.conv_key}.weight"] = (
@@ -459,6 +479,7 @@ class VGGEngine:
     @torch.no_grad()
     def optimizer_state_dict(self) -> dict:
         """torch.optim.SGD-format state_dict (momentum buffers in OIHW)."""
+        self.flush_update()
         names = self.spec.param_names()
         state = {}
         if self.steps_taken > 0:
@@ -472,6 +493,7 @@ class VGGEngine:
 
     @torch.no_grad()
     def load_optimizer_state_dict(self, osd: dict):
+        self.flush_update()
         names = self.spec.param_names()
         pg = osd["param_groups"][0]
         self.lr, self.momentum, self.weight_decay = pg["lr"], pg["momentum"], pg["weight_decay"]
@@ -774,8 +796,12 @@ class VGGEngine:
             epoch = self._sig_epoch
         if self.x0p is not None and not (self.fused_conv0 and self.fused_wgrad0):  # plane kernels read x0p
             K.pad_split8(x, self.x0p[:, :n])
+        self._issue_deferred_update()
+        main = torch.cuda.current_stream(self.device) if self._upd_wait else None
         for i, l in enumerate(L):
             z, st = self.z[i][:n], self.stats[i]
+            if self._upd_wait and i in self._upd_wait:  # this layer's (and later) parameters updated
+                self._upd_wait.pop(i).wait(main)
             if i == 0 and self.l0_recompute:
                 if buffers_wait is not None:
                     buffers_wait()
@@ -832,6 +858,9 @@ class VGGEngine:
             if (i == len(L) - 1 and self.fused_head) or nxt_bnin:
                 continue  # applied inside the head kernel below / by the next conv on load
             K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
+        for ev in self._upd_wait.values():  # (networks too short for the layer-indexed waits)
+            ev.wait(main)
+        self._upd_wait = {}
         feat = self.a[-1][:n].view(n, -1)
         bn_in = (dict(bn_z=self.z[-1][:n], bn_scale=self.stats[-1]["scale"], bn_shift=self.stats[-1]["shift"])
                  if self.fused_head else {})
@@ -1010,10 +1039,62 @@ class VGGEngine:
         self._eval_dirty = True
         return self.loss
 
-    def sgd_step(self, grad_scale: float = 1.0, offset: int = 0, count: int = -1):
+    def sgd_step(self, grad_scale: float = 1.0, offset: int = 0, count: int = -1, first: Optional[bool] = None):
         """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
+        self.flush_update()
+        self._sgd(grad_scale, offset, count, self.steps_taken == 0 if first is None else first)
+
+    def _sgd(self, grad_scale: float, offset: int, count: int, first: bool):
         self.K.sgd_flat(self.params.flat, self.grads.flat, self.mom.flat, self.lr, self.momentum, self.weight_decay,
-                        grad_scale, self.steps_taken == 0, offset, count, self.wplanes)
+                        grad_scale, first, offset, count, self.wplanes)
+
+    def sgd_step_deferred(self, grad_scale: float = 1.0):
+        """The whole-arena SGD of this step, deferred (see ``defer_update``): layer 0's slice now, the
+        rest at the start of the next ``forward_backward`` (or at ``flush_update``)."""
+        if not (self.defer_update and self._upd_ev is not None and self.wstream is not None
+                and not torch.cuda.is_current_stream_capturing()):
+            self.sgd_step(grad_scale)
+            return
+        self.flush_update()
+        first = self.steps_taken == 0
+        c1 = self._upd_cut[0]
+        self._sgd(grad_scale, 0, c1, first)
+        self._upd_ev[0].record(torch.cuda.current_stream(self.device))
+        self._pending_upd = (grad_scale, first)
+
+    def _issue_deferred_update(self):
+        """Start of a step: the pending update on the weight-gradient stream, behind the end of the
+        previous step; the forward waits for its two halves before conv 1 and conv 4."""
+        if self._pending_upd is None:
+            return
+        scale, first = self._pending_upd
+        self._pending_upd = None
+        c1, c4, end = self._upd_cut
+        s = self.wstream
+        self._upd_ev[0].wait(s)
+        with torch.cuda.stream(s):
+            self._sgd(scale, c1, c4 - c1, first)
+            self._upd_ev[1].record(s)
+            self._sgd(scale, c4, end - c4, first)
+            self._upd_ev[2].record(s)
+        nl = len(self.spec.convs)
+        self._upd_wait = {min(1, nl - 1): self._upd_ev[1], min(4, nl - 1): self._upd_ev[2]}
+        if min(1, nl - 1) == min(4, nl - 1):
+            self._upd_wait = {min(1, nl - 1): self._upd_ev[2]}
+
+    def flush_update(self):
+        """Run a deferred update now, on the current stream (callers that read parameters or momenta
+        outside the step).  Also makes the current stream wait for an issued one."""
+        if self._pending_upd is not None:
+            scale, first = self._pending_upd
+            self._pending_upd = None
+            c1, _, end = self._upd_cut
+            self._sgd(scale, c1, end - c1, first)
+        if self._upd_wait:
+            cur = torch.cuda.current_stream(self.device)
+            for ev in self._upd_wait.values():
+                ev.wait(cur)
+            self._upd_wait = {}
 
     def wait_signal(self, signal):
         """The current stream waits (one polling wave, bounded) for a ``(flag, value)`` signal."""
@@ -1036,6 +1117,7 @@ class VGGEngine:
 
     # ------------------------------------------------------------------ evaluation
     def begin_eval(self):
+        self.flush_update()
         for i, l in enumerate(self.spec.convs):
             self.K.bn_eval_params(self.params[f"{l.bn_key}.weight"], self.params[f"{l.bn_key}.bias"],
                                   self.params[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],

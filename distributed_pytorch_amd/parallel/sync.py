@@ -161,6 +161,7 @@ class GradSync:
     # -- state broadcast (DDP ctor semantics; torch distributed.py:862-871) --
     def broadcast_state(self):
         e = self.engine
+        e.flush_update()
         with self.comm.region():
             self.comm.broadcast(e.params.flat, 0)
             if self.shared_buffers:
@@ -173,7 +174,8 @@ class GradSync:
 
     def prepare_checkpoint(self):
         """Collective hook before every rank writes its checkpoint: make the local optimizer state
-        complete (a no-op except for sharded optimizer state)."""
+        complete (a no-op except for sharded optimizer state and a deferred update)."""
+        self.engine.flush_update()
 
     def pre_forward(self):
         """Called before the training forward.  May return a callable that the engine invokes
@@ -306,7 +308,7 @@ class GradSync:
         """Apply the optimizer step to the synchronised gradients (the whole arena by default;
         with the fused step only slices whose update was not already queued during backward)."""
         if not self.fuse_step:
-            self.engine.sgd_step(grad_scale)
+            self.engine.sgd_step_deferred(grad_scale)  # (immediate unless engine.defer_update)
             return
         for b in self.buckets:
             if not b.stepped:
@@ -460,6 +462,7 @@ class ZeroSync(DDPSync):
         rank holds the complete momentum arena already (``prepare_checkpoint`` all-gathers the
         shards before each save)."""
         e = self.engine
+        e.flush_update()
         with self.comm.region():
             self.comm.broadcast(e.params.flat, 0)
             if self.shared_buffers:
@@ -471,6 +474,7 @@ class ZeroSync(DDPSync):
     def prepare_checkpoint(self):
         """All-gather every bucket's owned momentum shards so each rank's arena (and checkpoint)
         holds the full, current SGD state."""
+        self.engine.flush_update()
         if not self.active:
             return
         e = self.engine
