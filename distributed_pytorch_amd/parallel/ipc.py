@@ -52,6 +52,8 @@ class IpcComm(Comm):
         self.tag = tag
         self.blocks = int(blocks or os.environ.get("DPA_IPC_BLOCKS", "32"))
         self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("DPA_IPC_TIMEOUT", "60"))
+        # elements one collective can carry: each rank stages a 1/W slice (multiple of 4 elements)
+        self.max_elems = (int(stage_floats) // 4 * 4) * self.world
         self._nreg = 0
         self._regions: Dict[Tuple[int, int], int] = {}  # (data ptr, elements) -> region id
         with torch.cuda.device(self.device):
@@ -101,20 +103,27 @@ class IpcComm(Comm):
         return (op == "sum" and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
                 and t.data_ptr() % 16 == 0 and self._region_of(t) is not None)
 
+    def _peer_all_reduce(self, t: torch.Tensor):
+        """One peer-kernel collective per staging-buffer-sized piece (pieces are multiples of 4*W
+        elements, so every piece stays 16-byte aligned)."""
+        rid, off = self._region_of(t)
+        n, done = t.numel(), 0
+        while done < n:
+            k = min(self.max_elems, n - done)
+            self._c.all_reduce(rid, off + done, k, self.blocks, int(self.timeout_s * 1e6))
+            self.ipc_ops += 1
+            done += k
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         if not self.ipc_eligible(t, op):
             return self.inner.all_reduce(t, op)
-        rid, off = self._region_of(t)
-        self._c.all_reduce(rid, off, t.numel(), self.blocks, int(self.timeout_s * 1e6))
-        self.ipc_ops += 1
+        self._peer_all_reduce(t)
 
     def all_reduce_here(self, t: torch.Tensor, op: str = "sum"):
         if not self.ipc_eligible(t, op):
             return self.inner.all_reduce_here(t, op)
         self.inner.wait()  # earlier collectives (RCCL or peer kernels on the comm stream) first
-        rid, off = self._region_of(t)
-        self._c.all_reduce(rid, off, t.numel(), self.blocks, int(self.timeout_s * 1e6))
-        self.ipc_ops += 1
+        self._peer_all_reduce(t)
 
     def broadcast(self, t, root=0):
         self.inner.broadcast(t, root)

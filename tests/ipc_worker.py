@@ -21,7 +21,8 @@ def main():
     dev = ctx.device
     W, r = ctx.world, ctx.rank
     store = torch.distributed.distributed_c10d._get_default_store()
-    c = IpcComm(ctx.comm, store, dev, blocks=int(os.environ.get("DPA_IPC_BLOCKS", "16")), timeout_s=30.0)
+    c = IpcComm(ctx.comm, store, dev, blocks=int(os.environ.get("DPA_IPC_BLOCKS", "16")), timeout_s=30.0,
+                stage_floats=int(os.environ.get("DPA_IPC_TEST_STAGE", str(1 << 22))))
     N = 1 << 21
     data = [torch.randn(N, generator=torch.Generator().manual_seed(100 + q)) for q in range(W)]
     arena = data[r].to(dev)

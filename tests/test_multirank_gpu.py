@@ -119,16 +119,19 @@ def test_main_ddp_training_two_ranks(tmp_path):
     assert (ck / "rank0.pt").exists() and (ck / "rank1.pt").exists()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_ipc_allreduce_ranks_share_one_gpu(world):
+@pytest.mark.parametrize("world,stage", [(2, None), (4, None), (2, 65536)])
+def test_ipc_allreduce_ranks_share_one_gpu(world, stage):
     """the peer-memory all-reduce (HIP IPC mappings + one two-shot kernel per
     collective) between 2 / 4 processes on one GPU: bitwise the rank-order fp32 sum, slices with
-    odd tails, nothing outside the slice touched, no wait timed out (tests/ipc_worker.py)."""
+    odd tails, nothing outside the slice touched, no wait timed out (tests/ipc_worker.py).  stage: a
+    staging buffer smaller than a collective's slice (the collective runs as several pieces)."""
     from distributed_pytorch_amd.parallel.spawn import free_port
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "tests", "ipc_worker.py")]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if stage:
+        env["DPA_IPC_TEST_STAGE"] = str(stage)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPA_STORE_PORT"):
         env.pop(k, None)
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
