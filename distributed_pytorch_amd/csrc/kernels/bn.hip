@@ -98,7 +98,11 @@ inline int bwd_blocks(long M, int C) {
     const char* e = std::getenv("DPA_BN_BWD_BLOCKS");
     return e ? std::atoi(e) : BWD_BLOCKS;
   }();
-  return bwd_wide(M, C) ? 256 : nb;
+  static const int nw = [] {  // 1024-thread geometry (A/B: DPA_BN_BWD_WIDE_BLOCKS)
+    const char* e = std::getenv("DPA_BN_BWD_WIDE_BLOCKS");
+    return e ? std::atoi(e) : 256;
+  }();
+  return bwd_wide(M, C) ? nw : nb;
 }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
