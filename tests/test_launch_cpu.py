@@ -297,3 +297,34 @@ def test_comm_plans_rccl_channel_budgets(monkeypatch):
     monkeypatch.setenv("DPA_RCCL_CHANNELS", "12")
     assert len(bench.comm_plans(bench.parse(["--mode", "ddp"]), rccl=True)) == 5
     assert bench.comm_plans(bench.parse(["--mode", "gather"]), rccl=True) == []
+
+
+def test_ipc_collective_pieces_cover_the_tensor():
+    """parallel/ipc.py: a collective larger than the staging buffer runs as consecutive pieces of at
+    most stage * world elements (multiples of 4 * world: 16-byte aligned offsets) that cover it
+    exactly; a small one is one piece."""
+    import torch
+
+    from distributed_pytorch_amd.parallel.ipc import IpcComm
+
+    calls = []
+
+    class FakeNative:
+        def all_reduce(self, rid, off, n, blocks, tmo):
+            calls.append((rid, off, n))
+
+    for world, stage, n in ((2, 1000, 4099), (8, 65536, 9_225_000), (4, 1 << 22, 12345)):
+        c = object.__new__(IpcComm)
+        c.world, c.blocks, c.timeout_s, c.ipc_ops = world, 16, 1.0, 0
+        c.max_elems = (stage // 4 * 4) * world
+        c._c = FakeNative()
+        t = torch.zeros(n + 64)
+        c._regions = {(t.data_ptr(), t.numel()): 3}
+        calls.clear()
+        c._peer_all_reduce(t[16:16 + n])
+        assert sum(k for _, _, k in calls) == n and c.ipc_ops == len(calls)
+        pos = 16
+        for rid, off, k in calls:
+            assert rid == 3 and off == pos and k <= c.max_elems and off % 4 == 0
+            pos += k
+        assert len(calls) == -(-n // c.max_elems)
