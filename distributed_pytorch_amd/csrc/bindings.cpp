@@ -95,6 +95,15 @@ int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short*
                       int sig_val);
 int dpa_wait_signal(const int* sig, int val, long long timeout_us, int* tmo, hipStream_t st);
 int dpa_bn_fused_geo(int Mo, int C, int pool, int bwd, int rmax, long* part_floats, long* cnt_words, int* blocks);
+int dpa_bn_cols_bwd(const float* gsrc, int nsplit, const float* z, int N, int H, int W, int C, int pool,
+                    const float* scale, const float* shift, const float* mean, const float* invstd,
+                    const float* gamma, float* dgamma, float* dbeta, float* dbias, float* dz, unsigned short* dz3,
+                    int np, long ps, int* sig, int sig_val, hipStream_t st);
+int dpa_bn_cols_ok(int units, int C, int pool);
+int dpa_bn_cols_fwd(const float* src, int nsplit, float* zw, int N, int H, int W, int C, int pool,
+                    const float* gamma, const float* beta, const float* bias, float* rmean, float* rvar,
+                    long long* nbt, float* mean, float* invstd, float* scale, float* shift, float* out,
+                    unsigned short* out3, int np, long ps, float momentum, float eps, hipStream_t st);
 int dpa_bn_fused_fwd(const float* src, int nsplit, float* zw, int N, int H, int W, int C, int pool, int rmax,
                      float* part, unsigned* cnt, const float* gamma, const float* beta, const float* bias,
                      float* rmean, float* rvar, long long* nbt, float* mean, float* invstd, float* scale,
@@ -1013,6 +1022,48 @@ void bn_fused_fwd(Tensor src, int64_t nsplit, Tensor z, bool pool, int64_t rmax,
       "bn_fused_fwd");
 }
 
+// Column-block forward BN (bn_cols.hip): one launch, no cross-block hand-off, for small layers.
+bool bn_cols_ok(int64_t units, int64_t C, bool pool) { return dpa_bn_cols_ok((int)units, (int)C, pool ? 1 : 0) != 0; }
+
+void bn_cols_fwd(Tensor src, int64_t nsplit, Tensor z, bool pool, Tensor gamma, Tensor beta, OptT bias, OptT rmean,
+                 OptT rvar, OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, OptT out,
+                 double momentum, double eps) {
+  need(src, "src");
+  need(z, "z");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
+  TORCH_CHECK(dpa_bn_cols_ok(Mo, C, pool ? 1 : 0), "bn_cols_fwd: layer too large for the column-block BN");
+  TORCH_CHECK(src.numel() >= nsplit * z.numel(), "bn_cols_fwd: src too small");
+  TORCH_CHECK(nsplit == 1 || src.data_ptr() != z.data_ptr(), "bn_cols_fwd: slabs and z must differ");
+  long long* nb_p = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    need(*nbt, "nbt", at::kLong);
+    nb_p = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  const OutPtrs o = out_ptrs(out, (int64_t)Mo * C, "bn_cols_fwd");
+  chk(dpa_bn_cols_fwd(fp(src), (int)nsplit, fp(z), N, H, W, C, pool ? 1 : 0, fp(gamma), fp(beta), ofp(bias),
+                      ofp(rmean), ofp(rvar), nb_p, fp(mean), fp(invstd), fp(scale), fp(shift), o.f, o.b, o.np, o.ps,
+                      (float)momentum, (float)eps, cur_stream()),
+      "bn_cols_fwd");
+}
+
+void bn_cols_bwd(Tensor gsrc, int64_t nsplit, Tensor z, bool pool, Tensor scale, Tensor shift, Tensor mean,
+                 Tensor invstd, Tensor gamma, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, OptT sig,
+                 int64_t sig_val) {
+  need(gsrc, "gsrc");
+  need(z, "z");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
+  TORCH_CHECK(dpa_bn_cols_ok(Mo, C, pool ? 1 : 0), "bn_cols_bwd: layer too large for the column-block BN");
+  TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_cols_bwd: gsrc too small");
+  const OutPtrs o = out_ptrs(dz, z.numel(), "bn_cols_bwd");
+  TORCH_CHECK(o.f || o.b, "bn_cols_bwd: dz required");
+  chk(dpa_bn_cols_bwd(fp(gsrc), (int)nsplit, fp(z), N, H, W, C, pool ? 1 : 0, fp(scale), fp(shift), fp(mean),
+                      fp(invstd), fp(gamma), fp(dgamma), fp(dbeta), ofp(dbias), o.f, o.b, o.np, o.ps,
+                      opt_signal(sig, "bn_cols_bwd"), (int)sig_val, cur_stream()),
+      "bn_cols_bwd");
+}
+
 void bn_fused_bwd(Tensor gsrc, int64_t nsplit, Tensor z, bool pool, int64_t rmax, Tensor part, Tensor cnt,
                   Tensor scale, Tensor shift, Tensor mean, Tensor invstd, Tensor gamma, Tensor dgamma, Tensor dbeta,
                   OptT dbias, Tensor dz, Tensor tmo, int64_t timeout_us, OptT sig, int64_t sig_val) {
@@ -1320,6 +1371,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_tick_words", [](int64_t M, int64_t C) { return (int64_t)dpa_bn_tick_words((int)M, (int)C); });
   m.def("bn_fused_geo", &bn_fused_geo, py::arg("Mo"), py::arg("C"), py::arg("pool"), py::arg("bwd"),
         py::arg("rmax"));
+  m.def("bn_cols_ok", &bn_cols_ok, py::arg("units"), py::arg("C"), py::arg("pool"));
+  m.def("bn_cols_fwd", &bn_cols_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
+        py::arg("gamma"), py::arg("beta"), py::arg("bias"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"),
+        py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("out"), py::arg("momentum"),
+        py::arg("eps"));
+  m.def("bn_cols_bwd", &bn_cols_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
+        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
   m.def("bn_fused_fwd", &bn_fused_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
         py::arg("rmax"), py::arg("part"), py::arg("cnt"), py::arg("gamma"), py::arg("beta"), py::arg("bias"),
         py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("mean"), py::arg("invstd"), py::arg("scale"),

@@ -308,6 +308,15 @@ class VGGEngine:
         # (layers 4-7 at batch 256), backward only for the 2x2 layers (<= 0.6M; beside the weight-
         # gradient convs the 4x4 layers' rendezvous waits for CUs and loses to the three kernels).
         self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", "2200000")) if dev.type == "cuda" else 0
+        # BN of those small layers as ONE column-block launch instead (bn_cols.hip: a block owns 4
+        # channels over all rows, no rendezvous between blocks; DPA_BN_COLS=1 forward,
+        # DPA_BN_COLS_BWD=1 backward).  Off: same box, 175.1k (bn_fused / three kernels) vs 160.1k
+        # (forward) vs 143.9k img/s (both) -- the 16-byte-per-row loads of a 4-channel column touch
+        # one cache line per lane, and C/4 blocks leave half the CUs idle (docs/PERF_NOTES.md).
+        self.bn_cols = (dev.type == "cuda" and hasattr(self.K, "bn_cols_fwd")
+                        and os.environ.get("DPA_BN_COLS", "0") == "1")
+        self.bn_cols_bwd = (dev.type == "cuda" and hasattr(self.K, "bn_cols_bwd")
+                            and os.environ.get("DPA_BN_COLS_BWD", "0") == "1")
         self.bn_fused_bwd_max = (int(os.environ.get("DPA_BN_FUSED_BWD_MAX", "600000"))
                                  if dev.type == "cuda" else 0)
         self.bn_fused_rmax = int(os.environ.get("DPA_BN_FUSED_RMAX", "64"))
@@ -520,6 +529,21 @@ class VGGEngine:
             return None  # layer 0: conv0_fwd / bn_bwd_wgrad0 fuse its BN with the convolution instead
         ho = l.hw // 2 if l.pool else l.hw
         return self.K.bn_fused_geo(n * ho * ho, l.cout, l.pool, bwd, self.bn_fused_rmax)
+
+    def _cols(self, i: int, n: int, bwd: bool = False) -> bool:
+        """Layer i's BN as the column-block kernel (bn_cols.hip): layers up to the one-launch BN's
+        size bound whose register tile fits (DPA_BN_COLS=0 / DPA_BN_COLS_BWD=0: never)."""
+        key = ("cols", i, n, bwd)
+        v = self._fgeo.get(key)
+        if v is None:
+            l = self.spec.convs[i]
+            ho = l.hw // 2 if l.pool else l.hw
+            on = self.bn_cols_bwd if bwd else self.bn_cols
+            v = bool(on and i > 0 and 0 < n * l.hw * l.hw * l.cout <= self.bn_fused_max
+                     and self.K.bn_cols_ok(n * ho * ho, l.cout, l.pool)
+                     and not (bwd and self._bnin_bwd(i, n)))  # (BN on load forms dz in the dgrad instead)
+            self._fgeo[key] = v
+        return v
 
     def _fused(self, i: int, n: int, bwd: bool) -> bool:
         key = (i, n, bwd)
@@ -840,6 +864,14 @@ class VGGEngine:
                 if not (i == len(L) - 1 and self.fused_head) and not nxt_bnin:
                     K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
+            if self._cols(i, n):  # one launch, no cross-block hand-off (bn_cols.hip)
+                head = (i == len(L) - 1 and self.fused_head) or nxt_bnin
+                K.bn_cols_fwd(self.slab if ns > 1 else z, ns, z, l.pool, P[f"{l.bn_key}.weight"],
+                              P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
+                              self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
+                              self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
+                              None if head else self._act_out(i, n), self.bn_momentum, self.bn_eps)
+                continue
             if self._fused(i, n, False):
                 # the head kernel, or the next conv, applies it: statistics and coefficients only
                 head = (i == len(L) - 1 and self.fused_head) or nxt_bnin
@@ -968,7 +1000,11 @@ class VGGEngine:
                 if params_free is not None:
                     params_free(names)
                 continue
-            if self._fused(i, n, True):
+            if self._cols(i, n, True):  # one launch, no cross-block hand-off (bn_cols.hip)
+                K.bn_cols_bwd(self.slab if gsplit > 1 else g, gsplit, z, l.pool, st["scale"], st["shift"], st["mean"],
+                              st["invstd"], P[f"{l.bn_key}.weight"], G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"],
+                              G[f"{l.conv_key}.bias"], dzbuf, **bsig)
+            elif self._fused(i, n, True):
                 K.bn_fused_bwd(self.slab if gsplit > 1 else g, gsplit, z, l.pool, self.bn_fused_rmax, self.fpart,
                                self.fcnt, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
                                G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf,
