@@ -2200,12 +2200,14 @@ int xsplits(int Kred, int splits) {
 //   FPROP / DGRAD: 16 = 256x128 with 16-channel chunks (8 waves), 17 = 256x128 / 32,
 //                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32,
 //                  20 = 256x64 / 32 (8 waves of 64x32), 21 = 128x64 / 32 (4 waves of 64x32) for
-//                  64-channel outputs (e.g. the data gradient into a 64-channel layer)
+//                  64-channel outputs (e.g. the data gradient into a 64-channel layer),
+//                  22 = 256x128 / 32 with 16 waves of 64x32, 23 = 128x128 / 32 with 8 waves of
+//                  64x32 (four / two waves per SIMD beside the one-block-per-CU LDS footprint)
 //   WGRAD:         16 = 64-pixel chunks, 17 = 32-pixel chunks
-bool is_halo(int tile) { return tile >= 16 && tile <= 21; }
-int halo_bm(int tile) { return (tile <= 17 || tile == 20) ? 256 : 128; }
-int halo_bn(int tile) { return tile >= 20 ? 64 : 128; }
-int halo_bc(int tile) { return (tile & 1) || tile == 20 ? 32 : 16; }
+bool is_halo(int tile) { return tile >= 16 && tile <= 23; }
+int halo_bm(int tile) { return (tile <= 17 || tile == 20 || tile == 22) ? 256 : 128; }
+int halo_bn(int tile) { return tile == 20 || tile == 21 ? 64 : 128; }
+int halo_bc(int tile) { return (tile & 1) || tile == 20 || tile == 22 ? 32 : 16; }
 
 template <int BM, int BN, int WM, int WN, bool DG, int NP, int BC, bool OB>
 int launch_halo(const HArgs& a, int splits, hipStream_t st) {
@@ -2244,6 +2246,8 @@ int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
     case 18: return launch_halo<128, 128, 2, 2, DG, NP, 16, OB>(a, splits, st);
     case 20: return launch_halo<256, 64, 4, 2, DG, NP, 32, OB>(a, splits, st);
     case 21: return launch_halo<128, 64, 2, 2, DG, NP, 32, OB>(a, splits, st);
+    case 22: return launch_halo<256, 128, 4, 4, DG, NP, 32, OB>(a, splits, st);
+    case 23: return launch_halo<128, 128, 2, 4, DG, NP, 32, OB>(a, splits, st);
     default: return launch_halo<128, 128, 2, 2, DG, NP, 32, OB>(a, splits, st);
   }
 }

@@ -99,8 +99,9 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
 
 # Halo-staged 3x3/s1/p1 tiles of conv_x3.hip (ids after the 16 implicit-GEMM tiles): the block's
 # input pixels are staged once per channel chunk and the 9 taps read shifted views of them.
-HALO_TILES = (16, 17, 18, 19, 20, 21)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19) or 64 (20, 21)
-                                       # output channels, 16 or 32-channel chunks
+HALO_TILES = (16, 17, 18, 19, 20, 21, 22, 23)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19, 22, 23)
+                                               # or 64 (20, 21) output channels, 16 or 32-channel
+                                               # chunks; 22 / 23: 17 / 19 with twice the waves
 HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
 POS_TILES = (24, 25, 26, 27, 28, 29)  # fprop / dgrad of small images: position-major rows, padding taps
                                       # skipped (conv_x3.hip conv_pos_kernel)
@@ -115,7 +116,7 @@ def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
         return p is not None and cred % 8 == 0 and cout % 8 == 0 and p + 2 * w + 2 <= 2 * p + 3
     if tile not in HALO_TILES:
         return False
-    bm, bc = (256 if tile in (16, 17, 20) else 128), (32 if tile & 1 or tile == 20 else 16)
+    bm, bc = (256 if tile in (16, 17, 20, 22) else 128), (32 if tile & 1 or tile in (20, 22) else 16)
     return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= bm + bm // 2
 
 

@@ -381,11 +381,11 @@ def _halo_ok(kind, tile, w, cred, cout):
 
 @pytest.mark.parametrize("shape", HALO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21, 22, 23])
 @pytest.mark.parametrize("np_", [3, 1])
 @pytest.mark.parametrize("dgrad", [False, True])
 def test_conv_halo(shape, splits, tile, np_, dgrad):
-    """Halo-staged 3x3 fprop / data gradient (tiles 16-21) against fp64: partial blocks, blocks
+    """Halo-staged 3x3 fprop / data gradient (tiles 16-23) against fp64: partial blocks, blocks
     across image boundaries, bands of rows, partial column tiles (128- and 64-column tiles) and
     split-K."""
     C = _C()
