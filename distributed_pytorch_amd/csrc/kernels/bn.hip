@@ -77,11 +77,13 @@ inline int bwd_force() {
   }();
   return f;
 }
-inline bool bwd_wide(long M, int C) {
+// bf: bf16 tensors (the generic path, its 16-byte-lane reduce): the 1024-thread geometry at every
+// size (ResNet-50 A/B: 9,240 -> 9,330 img/s); fp32 (the VGG engine) by size as above.
+inline bool bwd_wide(long M, int C, bool bf = false) {
   const int f = bwd_force();
   if (f == 1024) return true;
   if (f == 256) return false;
-  return M * (long)(C >> 2) > WIDE_MIN_F4;
+  return bf || M * (long)(C >> 2) > WIDE_MIN_F4;
 }
 // channels per backward-finalize block: 8 (32 partial rows of each in flight) or 4 (64 rows;
 // DPA_BN_FIN_CPB=4).  Equal within noise in the step (158.5k vs 158.2k img/s), 8 is kept.
@@ -92,8 +94,8 @@ inline int fin_cpb() {
   }();
   return v;
 }
-inline int bwd_rt(long M, int C) { return bwd_wide(M, C) ? RT : RTB; }
-inline int bwd_blocks(long M, int C) {
+inline int bwd_rt(long M, int C, bool bf = false) { return bwd_wide(M, C, bf) ? RT : RTB; }
+inline int bwd_blocks(long M, int C, bool bf = false) {
   static const int nb = [] {
     const char* e = std::getenv("DPA_BN_BWD_BLOCKS");
     return e ? std::atoi(e) : BWD_BLOCKS;
@@ -102,7 +104,7 @@ inline int bwd_blocks(long M, int C) {
     const char* e = std::getenv("DPA_BN_BWD_WIDE_BLOCKS");
     return e ? std::atoi(e) : 256;
   }();
-  return bwd_wide(M, C) ? nw : nb;
+  return bwd_wide(M, C, bf) ? nw : nb;
 }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
@@ -142,7 +144,10 @@ __host__ inline int red_rows_per_block(int M, int C, int rt = RT, int blocks = 2
   return rpb < g.RPI ? g.RPI : rpb;
 }
 
-inline int bwd_rows_per_block(int M, int C) { return red_rows_per_block(M, C, bwd_rt(M, C), bwd_blocks(M, C)); }
+// (the fp32 rule sizes dpa_bn_part_floats: the bf16 geometry never needs more partial rows)
+inline int bwd_rows_per_block(int M, int C, bool bf = false) {
+  return red_rows_per_block(M, C, bwd_rt(M, C, bf), bwd_blocks(M, C, bf));
+}
 
 // In-block tree over the RPI row lanes of each channel lane (fixed order): on return sh[t] for
 // lane_r == 0 holds the block sum.  Caller has stored sh[t] and synchronised.
@@ -1003,9 +1008,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
                   const unsigned char* mask = nullptr, TZ* dyout = nullptr, unsigned* tick = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
-  const int rpb = bwd_rows_per_block(Mo, C);
+  constexpr bool bf = sizeof(TZ) == 2;
+  const int rpb = bwd_rows_per_block(Mo, C, bf);
   int nblk = (Mo + rpb - 1) / rpb;
-  const bool wide = bwd_wide(Mo, C);
+  const bool wide = bwd_wide(Mo, C, bf);
   // ticketed finalize inside the reduce (256-thread geometry; part holds the level-2 rows after the
   // block rows, dpa_bn_part_floats; its order is the 8-channel finalize's)
   const bool ticked = tick != nullptr && !wide && fin_cpb() == 8;
