@@ -289,27 +289,23 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
                                                           float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float momentum, float eps) {
-  // 4 channels per block, 64 partial rows of each in flight (one batch of loads per thread for the
-  // ~256 partial rows of the statistics pass), fixed-order Chan merges
+  // 4 channels per block, 64 partial-row groups of each, fixed-order Chan merges
   constexpr int CPB = 4, G = 256 / CPB;
   const int cl = threadIdx.x % CPB, grp = threadIdx.x / CPB;
   const int c = blockIdx.x * CPB + cl;
   Welford acc{0.f, 0.f, 0.f};
   if (c < C) {
-    int k = grp;
-    for (; k + 3 * G < nblk; k += 4 * G) {
-      float2 p[4];
+    // 16 partial rows per thread in flight (conv0's ~1024 epilogue partials: one memory latency
+    // instead of four), merged in the same order
+    for (int k = grp; k < nblk; k += 16 * G) {
+      float2 p[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) p[u] = part[(long)(k + G * u) * C + c];
+      for (int u = 0; u < 16; ++u) p[u] = k + G * u < nblk ? part[(long)(k + G * u) * C + c] : make_float2(0.f, 0.f);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const int kk = k + G * u;
-        acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
+        if (kk < nblk) acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
       }
-    }
-    for (; k < nblk; k += G) {
-      const float2 p = part[(long)k * C + c];
-      acc = merge(acc, Welford{(float)min(rpb, M - k * rpb), p.x, p.y});
     }
   }
   __shared__ Welford sh[256];
@@ -754,7 +750,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
 // Per channel: sum the block partials (fixed order -> deterministic), emit dgamma, dbeta, dbias and
 // the dz coefficients: dz = k1*dy + k2*z + k3.   8 channels x 32 groups per block.
 // Backward finalize: BF_CPB channels per 256-thread block, 256/BF_CPB partial rows of each in
-// flight (a thread's loads are issued 8 rows at a time), fixed-order LDS tree.
+// flight (a thread's loads are issued 16 rows at a time), fixed-order LDS tree.
 template <int BF_CPB>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                               float Mfull, const float* __restrict__ gamma,
@@ -767,28 +763,24 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   const int c = blockIdx.x * BF_CPB + cl;
   float a = 0.f, b = 0.f, x = 0.f;
   if (c < C) {
-    int k = grp;
-    for (; k + 7 * G < nblk; k += 8 * G) {
-      float pa[8], pb[8], px[8];
+    // 16 partial rows per thread in flight (one memory latency for the engine's 512-row partials
+    // instead of two); out-of-range rows add +0.f (exact: the sums start at +0), same order
+    for (int k = grp; k < nblk; k += 16 * G) {
+      float pa[16], pb[16], px[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float* p = part + (long)(k + G * u) * 3 * C + c;
-        pa[u] = p[0];
-        pb[u] = p[C];
-        px[u] = p[2 * C];
+      for (int u = 0; u < 16; ++u) {
+        const bool v = k + G * u < nblk;
+        const float* p = part + (long)(v ? k + G * u : 0) * 3 * C + c;
+        pa[u] = v ? p[0] : 0.f;
+        pb[u] = v ? p[C] : 0.f;
+        px[u] = v ? p[2 * C] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         a += pa[u];
         b += pb[u];
         x += px[u];
       }
-    }
-    for (; k < nblk; k += G) {
-      const float* p = part + (long)k * 3 * C + c;
-      a += p[0];
-      b += p[C];
-      x += p[2 * C];
     }
   }
   __shared__ float sh[3][256];

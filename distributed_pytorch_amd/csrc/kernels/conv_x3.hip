@@ -2104,10 +2104,37 @@ __global__ __launch_bounds__(256) void pad_split_kernel(const float* __restrict_
   }
 }
 
+// DPA_WGRAD_BPC=b (b >= 1; read per call): a weight-gradient launch reserves unused dynamic LDS so
+// that at most b of its blocks share a CU.  The VGG engine runs these convs on its second stream
+// beside the critical path's BatchNorm passes; packed 3 blocks per CU (e.g. 148 VGPRs x 3 waves per
+// SIMD) they leave no registers for those passes' waves until conv blocks retire.
+int wgrad_bpc() {
+  const char* e = getenv("DPA_WGRAD_BPC");
+  return e ? atoi(e) : 0;
+}
+constexpr int LDS_PER_CU = 160 * 1024;
+
 template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK, int NS, bool OB>
 int launch_x3(const Args& a, hipStream_t st) {
   dim3 grid(a.gm * a.gn, a.splits, a.nph > 1 ? a.nph : 1);
-  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS, OB><<<grid, WM * WN * 64, 0, st>>>(a);
+  auto kern = conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS, OB>;
+  size_t dyn = 0;
+  if (MODE == XM_WGRAD) {
+    const int b = wgrad_bpc();
+    if (b > 0) {
+      static int stat = -1;  // this instantiation's static LDS bytes
+      if (stat < 0) {
+        hipFuncAttributes fa;
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) != hipSuccess) return 1;
+        stat = (int)fa.sharedSizeBytes;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_PER_CU - stat);
+      }
+      const int want = LDS_PER_CU / (b + 1) + 256 - stat;  // b + 1 blocks no longer fit
+      if (want > 0) dyn = (size_t)std::min(want, LDS_PER_CU - stat);
+    }
+  }
+  kern<<<grid, WM * WN * 64, dyn, st>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -37,12 +37,19 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
                                                          float* __restrict__ logits_out, int B, int Cin, int J,
                                                          BnIn bn = BnIn{nullptr, nullptr, nullptr}) {
   extern __shared__ float w_s[];  // [J][Cin]
-  for (int i = threadIdx.x * 4; i < J * Cin; i += blockDim.x * 4)
-    *reinterpret_cast<float4*>(w_s + i) = *reinterpret_cast<const float4*>(w + i);
-  __syncthreads();
+  // All of the block's W loads are issued together, then the row's loads, and only then is the LDS
+  // image written: one memory latency for both instead of one per 4 KB of W plus one for the row
+  // (the rolled copy loop cost ~5 dependent round trips on the VGG step's critical path).
+  constexpr int WIT = (MAXJ * 64 * MAXCL + 1023) / 1024;  // float4 per thread (256 threads)
+  float4 wt[WIT];
+#pragma unroll
+  for (int u = 0; u < WIT; ++u) {
+    const int i = threadIdx.x * 4 + u * 1024;
+    wt[u] = i < J * Cin ? *reinterpret_cast<const float4*>(w + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
+  const int row = min(blockIdx.x * 4 + (threadIdx.x >> 6), B - 1);  // tail waves load a valid row
+  const bool rv = blockIdx.x * 4 + (threadIdx.x >> 6) < B;
   const float* xr = x + (long)row * Cin;
   float xv[MAXCL];
   if constexpr (BNIN) {
@@ -57,7 +64,7 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
         const float v00 = fmaxf(fmaf(zr[c], sc, sh), 0.f), v01 = fmaxf(fmaf(zr[Cin + c], sc, sh), 0.f);
         const float v10 = fmaxf(fmaf(zr[2 * Cin + c], sc, sh), 0.f), v11 = fmaxf(fmaf(zr[3 * Cin + c], sc, sh), 0.f);
         v = fmaxf(fmaxf(v00, v01), fmaxf(v10, v11));
-        xo[c] = v;
+        if (rv) xo[c] = v;
       }
       xv[k] = v;
     }
@@ -68,6 +75,13 @@ __global__ __launch_bounds__(256) void fc_ce_rows_kernel(const float* __restrict
       xv[k] = c < Cin ? xr[c] : 0.f;
     }
   }
+#pragma unroll
+  for (int u = 0; u < WIT; ++u) {
+    const int i = threadIdx.x * 4 + u * 1024;
+    if (i < J * Cin) *reinterpret_cast<float4*>(w_s + i) = wt[u];
+  }
+  __syncthreads();
+  if (!rv) return;
   float logit[MAXJ];
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
