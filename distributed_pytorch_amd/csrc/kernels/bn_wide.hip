@@ -298,7 +298,8 @@ int dpa_bn_bwd_reduce_wide(const unsigned short* g, const unsigned short* g2, co
 int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,
                       const float* scale, const float* shift, long M, int C, int act, hipStream_t st) {
   if (!wide_on() || C % 8 || act < 0 || act > 2 || (act == 2 && !res)) return 1;
-  if ((reinterpret_cast<uintptr_t>(z) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(res)) & 15)
+  if ((reinterpret_cast<uintptr_t>(z) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(res)) & 15 ||
+      reinterpret_cast<uintptr_t>(mask) & 1)  // the mask is stored as 2-byte words
     return 1;
   const long total8 = M * (C / 8);
   const int grid = grid_wide(total8, C / 8);
