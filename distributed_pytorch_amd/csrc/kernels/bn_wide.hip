@@ -139,16 +139,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_wide_kernel(const uint4* __r
 // per (row block, channel) sums of dy, dy*xhat and xhat, with dy = g (+ g2) through the ReLU of
 // ACT 0, as is (ACT 1), or through the add+ReLU of ACT 2 (mask from the forward, or the residual),
 // dy stored to dyout for ACT 2 (the residual's gradient).  C/8 threads per row, 1024/(C/8) rows per
-// iteration, two rows' loads in flight; rows summed in order, then the fixed-order LDS tree (the
-// row partition differs from bn.hip's, so sums agree to rounding, not bitwise).  part: [block][3][C]
-// as bn.hip's, finalized by the same kernel.
+// iteration, U = 2 rows' loads in flight (4 measured no faster); rows summed in order, then the
+// fixed-order LDS tree (the row partition differs from bn.hip's, so sums agree to rounding, not
+// bitwise).  part: [block][3][C] as bn.hip's, finalized by the same kernel.
 constexpr int RTW = 1024;
 
 __device__ __forceinline__ float4 f4sum(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int ACT, bool MK>
+template <int ACT, bool MK, int U = 2>
 __global__ __launch_bounds__(RTW) void bn_bwd_reduce_wide_kernel(
     const uint4* __restrict__ g, const uint4* __restrict__ g2, const uint4* __restrict__ z,
     const uint4* __restrict__ res, const unsigned short* __restrict__ mask, uint4* __restrict__ dyout,
@@ -198,15 +198,22 @@ __global__ __launch_bounds__(RTW) void bn_bwd_reduce_wide_kernel(
     };
     const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
     int r = r0 + lane_r;
-    for (; r + RPI < r1; r += 2 * RPI) {
-      const long i0 = (long)r * C8 + lane_c, i1 = i0 + (long)RPI * C8;
-      const uint4 ga = g[i0], gb = g[i1];
-      const uint4 ha = g2 ? g2[i0] : zero, hb = g2 ? g2[i1] : zero;
-      const uint4 za = z[i0], zb = z[i1];
-      const uint4 ra = ACT == 2 && !mk ? res[i0] : zero, rb = ACT == 2 && !mk ? res[i1] : zero;
-      const unsigned ma = mk ? mask[i0] : 0u, mb = mk ? mask[i1] : 0u;
-      row(ga, ha, za, ra, ma, i0);
-      row(gb, hb, zb, rb, mb, i1);
+    // U rows' loads in flight per thread (rows still summed in ascending order: any U, same sums)
+    for (; r + (U - 1) * RPI < r1; r += U * RPI) {
+      uint4 gv[U], hv[U], zv[U], rv[U];
+      unsigned mv[U];
+      long iv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        iv[u] = (long)(r + u * RPI) * C8 + lane_c;
+        gv[u] = g[iv[u]];
+        hv[u] = g2 ? g2[iv[u]] : zero;
+        zv[u] = z[iv[u]];
+        rv[u] = ACT == 2 && !mk ? res[iv[u]] : zero;
+        mv[u] = mk ? mask[iv[u]] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) row(gv[u], hv[u], zv[u], rv[u], mv[u], iv[u]);
     }
     for (; r < r1; r += RPI) {
       const long i0 = (long)r * C8 + lane_c;

@@ -107,3 +107,4 @@ def _bwd_compare(monkeypatch, shape, act, with_g2, use_mask, exact):
         else:
             rel = ((x - y).abs().max() / x.abs().max().clamp_min(1e-30)).item()
             assert rel < 1e-4, (name, rel)
+
