@@ -22,12 +22,40 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                    help="diagnostic: busy the GPU with matmuls this long after the build, before the warmup "
+                         "steps (does the transient follow the clock, or the process?)")
+    ap.add_argument("--prewarm-kind", default="mfma", choices=["mfma", "mem"],
+                    help="mfma: fp32 matmuls; mem: 1 GiB device copies (memory / fabric clocks)")
+    ap.add_argument("--prelaunch", type=int, default=0,
+                    help="diagnostic: this many tiny kernel launches before the warmup steps (launch-path state)")
+    ap.add_argument("--lr", type=float, default=None, help="diagnostic: override the SGD learning rate (0: frozen)")
     a = ap.parse_args()
     args = bench.parse([])
     dev = torch.device("cuda", 0)
     t0 = time.perf_counter()
     engine, sync, it = bench.build(args, dev, 0, 1, NullComm())
     step = bench.make_step(engine, sync, it)
+    if a.lr is not None:
+        engine.lr = a.lr
+    if a.prelaunch > 0:
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        for i in range(a.prelaunch):
+            engine.K.set_signal(flag, i)
+        torch.cuda.synchronize()
+    if a.prewarm_ms > 0:
+        big = a.prewarm_kind == "mem"
+        x = torch.randn((1 << 28) if big else 4096 * 4096, device=dev)
+        y = torch.empty_like(x) if big else None
+        t1 = time.perf_counter()
+        while (time.perf_counter() - t1) * 1e3 < a.prewarm_ms:
+            for _ in range(8):
+                if big:
+                    y.copy_(x)
+                else:
+                    x = torch.tanh(x.view(4096, 4096) @ x.view(4096, 4096)).view(-1)
+            torch.cuda.synchronize()
+        del x, y
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
