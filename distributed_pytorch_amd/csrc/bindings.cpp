@@ -117,7 +117,7 @@ int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H
 
 int dpa_set_signal(int* sig, int val, hipStream_t st);
 int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
-                    int bf, hipStream_t st);
+                    int bf, hipStream_t st, const float* scale, const float* shift);
 int dpa_maxpool_bwd(const void* dy, const unsigned char* arg, void* dx, int N, int H, int W, int C, int k, int s,
                     int p, int bf, hipStream_t st);
 int dpa_augment(const unsigned char* img, const long long* idx, const long long* labels, float* out,
@@ -1157,16 +1157,24 @@ void maxpool_check(const Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, name, " must be fp32 or bf16");
 }
 
-void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t k, int64_t s, int64_t p) {
+// scale / shift (optional, fp32 [C]): x is a BatchNorm input, pooled as relu(x*scale + shift)
+void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t k, int64_t s, int64_t p, OptT scale, OptT shift) {
   maxpool_check(x, "x");
   maxpool_check(y, "y");
+  const bool bn = scale.has_value() && scale->defined();
+  TORCH_CHECK(bn == (shift.has_value() && shift->defined()), "maxpool_fwd: scale and shift go together");
+  if (bn) {
+    need(*scale, "scale");
+    need(*shift, "shift");
+    TORCH_CHECK(scale->numel() == x.size(3) && shift->numel() == x.size(3), "maxpool_fwd: scale/shift size");
+  }
   TORCH_CHECK(y.scalar_type() == x.scalar_type() && arg.scalar_type() == at::kByte && arg.sizes() == y.sizes() &&
                   arg.is_contiguous(), "maxpool_fwd: y/arg shape or dtype");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(y.size(0) == N && y.size(1) == (H + 2 * p - k) / s + 1 && y.size(2) == (W + 2 * p - k) / s + 1 &&
                   y.size(3) == C, "maxpool_fwd: output shape");
   chk(dpa_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)s, (int)p,
-                      x.scalar_type() == at::kBFloat16 ? 1 : 0, cur_stream()),
+                      x.scalar_type() == at::kBFloat16 ? 1 : 0, cur_stream(), ofp(scale), ofp(shift)),
       "maxpool_fwd");
 }
 
@@ -1422,7 +1430,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("parts") = 3);
   m.def("fc_ce_eval", &fc_ce_eval);
   m.def("augment", &augment);
-  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("y"), py::arg("arg"), py::arg("k"), py::arg("s"),
+        py::arg("p"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("maxpool_bwd", &maxpool_bwd);
   // A HIP stream with an explicit priority (lower number = higher priority; HIP's range is reported
   // by stream_priority_range()).  Owned by the caller; lives until stream_destroy.

@@ -51,9 +51,14 @@ struct PoolGeom {
   int N, H, W, C8, P, Q, k, s, p;
 };
 
-template <typename T, typename IT>
+// BN (BatchNorm + ReLU on load, `bn`): x is the BN input z and every window element is first mapped
+// to relu(z * scale + shift), rounded to T as bn_apply stores it -- the same max and positions as
+// pooling bn_apply's output, without writing or re-reading that tensor (the ResNet stem).
+template <typename T, typename IT, bool BN = false>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                          unsigned char* __restrict__ arg, PoolGeom g) {
+                                                          unsigned char* __restrict__ arg, PoolGeom g,
+                                                          const float* __restrict__ scale = nullptr,
+                                                          const float* __restrict__ shift = nullptr) {
   // IT: 32-bit index arithmetic when the element count allows (64-bit divisions dominated the
   // kernel: 2.5 TB/s on the ResNet-50 stem)
   const IT total = (IT)g.N * g.P * g.Q * g.C8;
@@ -64,12 +69,16 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
     r /= (IT)g.Q;
     const int oh = (int)(r % (IT)g.P);
     const int n = (int)(r / (IT)g.P);
-    float m[8];
+    float m[8], sc[8], sh[8];
     unsigned char a[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       m[k] = -INFINITY;
       a[k] = 0;
+    }
+    if constexpr (BN) {
+      V8<float>::load(scale + c8 * 8, sc);
+      V8<float>::load(shift + c8 * 8, sh);
     }
     bool first = true;  // the first in-image tap initialises (pad < k: every window has one)
     for (int kh = 0; kh < g.k; ++kh) {
@@ -80,6 +89,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
         if ((unsigned)w >= (unsigned)g.W) continue;
         float v[8];
         V8<T>::load(x + (((long)n * g.H + h) * g.W + w) * (g.C8 * 8) + c8 * 8, v);
+        if constexpr (BN) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float u = fmaxf(fmaf(v[k], sc[k], sh[k]), 0.f);
+            v[k] = sizeof(T) == 2 ? bf16_f(bf16_rne(u)) : u;
+          }
+        }
         const unsigned char pos = (unsigned char)(kh * g.k + kw);
 #pragma unroll
         for (int k = 0; k < 8; ++k)
@@ -147,21 +163,28 @@ int grid_for(long n) {
 
 extern "C" {
 
-// x [N,H,W,C] (C % 8 == 0) fp32 (bf=0) or bf16 (bf=1) -> y [N,P,Q,C], arg uint8 [N,P,Q,C]
+// x [N,H,W,C] (C % 8 == 0) fp32 (bf=0) or bf16 (bf=1) -> y [N,P,Q,C], arg uint8 [N,P,Q,C].
+// scale / shift (both or neither, [C] fp32): x is a BatchNorm input, pooled as relu(x*scale + shift).
 int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
-                    int bf, hipStream_t st) {
-  if (C % 8 || k < 1 || k * k > 255 || s < 1 || p < 0 || p >= k) return -2;
+                    int bf, hipStream_t st, const float* scale, const float* shift) {
+  if (C % 8 || k < 1 || k * k > 255 || s < 1 || p < 0 || p >= k || (scale == nullptr) != (shift == nullptr))
+    return -2;
   PoolGeom g{N, H, W, C / 8, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
   const long total = (long)g.N * g.P * g.Q * g.C8;
   const bool small = total + 8192L * 256 < (1L << 32);  // (the strided index stays below 2^32)
-  if (bf && small)
-    maxpool_fwd_kernel<u16, unsigned><<<grid_for(total), 256, 0, st>>>((const u16*)x, (u16*)y, arg, g);
-  else if (bf)
-    maxpool_fwd_kernel<u16, unsigned long><<<grid_for(total), 256, 0, st>>>((const u16*)x, (u16*)y, arg, g);
-  else if (small)
-    maxpool_fwd_kernel<float, unsigned><<<grid_for(total), 256, 0, st>>>((const float*)x, (float*)y, arg, g);
-  else
-    maxpool_fwd_kernel<float, unsigned long><<<grid_for(total), 256, 0, st>>>((const float*)x, (float*)y, arg, g);
+  const int grid = grid_for(total);
+#define POOL_FWD(T, IT)                                                                                   \
+  do {                                                                                                    \
+    if (scale)                                                                                            \
+      maxpool_fwd_kernel<T, IT, true><<<grid, 256, 0, st>>>((const T*)x, (T*)y, arg, g, scale, shift);    \
+    else                                                                                                  \
+      maxpool_fwd_kernel<T, IT><<<grid, 256, 0, st>>>((const T*)x, (T*)y, arg, g);                        \
+  } while (0)
+  if (bf && small) POOL_FWD(u16, unsigned);
+  else if (bf) POOL_FWD(u16, unsigned long);
+  else if (small) POOL_FWD(float, unsigned);
+  else POOL_FWD(float, unsigned long);
+#undef POOL_FWD
   return (int)hipGetLastError();
 }
 

@@ -92,7 +92,8 @@ class ResNet(nn.Module):
                     m.weight[..., :m.cin].copy_(w.permute(0, 2, 3, 1))
 
     def features(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        mp = self.maxpool
+        x = self.bn1(self.conv1(x), pool=(mp.k, mp.stride, mp.padding))  # BN + ReLU + max-pool, one pass on GPU
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))
 
     def forward(self, x, target=None):

@@ -573,7 +573,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0,
 class BnActNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, gamma, beta, res, rmean, rvar, nbt, training: bool, momentum: float, eps: float, act: int,
-                res_join: Optional[GradJoin] = None):
+                res_join: Optional[GradJoin] = None, pool: Optional[Tuple[int, int, int]] = None):
         N, H, W, C = z.shape
         dev = z.device
         K = _ext.require() if _native(z) else cpu_ref
@@ -591,31 +591,48 @@ class BnActNHWC(torch.autograd.Function):
                            eps)
         else:
             K.bn_eval_params(gamma, beta, None, rmean, rvar, scale, shift, eps)
-        a = torch.empty_like(z)
-        # add+ReLU in training on GPU: the kernel also writes the ReLU mask (1 byte per 4 channels),
-        # which the backward reads instead of the residual
-        mask = (torch.empty(z.numel() // 4, dtype=torch.uint8, device=dev)
-                if act == 2 and training and _native(z) and BN_RELU_MASK else None)
-        K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None, mask=mask)
-        ctx.act, ctx.training = act, training
+        arg = None
+        mask = None
+        if pool is not None:
+            # BN + ReLU applied inside the max-pool's loads (the ResNet stem): the BN output is never
+            # stored; the pool's window positions route the backward
+            k, st_, pd = pool
+            a = torch.empty(N, conv_out(H, k, st_, pd), conv_out(W, k, st_, pd), C, device=dev, dtype=z.dtype)
+            arg = torch.empty(a.shape, device=dev, dtype=torch.uint8)
+            K.maxpool_fwd(z, a, arg, k, st_, pd, scale=scale, shift=shift)
+        else:
+            a = torch.empty_like(z)
+            # add+ReLU in training on GPU: the kernel also writes the ReLU mask (1 byte per 4 channels),
+            # which the backward reads instead of the residual
+            mask = (torch.empty(z.numel() // 4, dtype=torch.uint8, device=dev)
+                    if act == 2 and training and _native(z) and BN_RELU_MASK else None)
+            K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None, mask=mask)
+        ctx.act, ctx.training, ctx.pool = act, training, pool
         ctx.res_join = res_join
         ctx.params = (gamma, beta)
         if training:
             note_use(gamma)
             note_use(beta)
-        ctx.save_for_backward(z, res if act == 2 and mask is None else None, mask, gamma, mean, invstd, scale, shift)
+        ctx.save_for_backward(z, res if act == 2 and mask is None else None, mask, gamma, mean, invstd, scale, shift,
+                              arg)
         return a
 
     @staticmethod
     def backward(ctx, da):
-        z, res, mask, gamma, mean, invstd, scale, shift = ctx.saved_tensors
+        z, res, mask, gamma, mean, invstd, scale, shift, arg = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("bn_act_nhwc backward is only defined in training mode")
-        ent = _DEFERRED.pop(da.data_ptr(), None)  # a deferred second contribution to da (GradJoin.register)
+        # a deferred second contribution to da (GradJoin.register; never for the pooled form)
+        ent = _DEFERRED.pop(da.data_ptr(), None) if ctx.pool is None else None
         da = da.contiguous()
         N, H, W, C = z.shape
         native = _native(z)
         K = _ext.require() if native else cpu_ref
+        if ctx.pool is not None:  # the pool's gather first: the gradient of the (never stored) BN output
+            k, st_, pd = ctx.pool
+            dpre = torch.empty_like(z)
+            K.maxpool_bwd(da, arg, dpre, k, st_, pd)
+            da = dpre
         f32 = dict(device=z.device, dtype=torch.float32 if native else z.dtype)
         dz = torch.empty_like(z)
         dgamma, dbeta = (grad_slot(p) for p in ctx.params)
@@ -637,14 +654,28 @@ class BnActNHWC(torch.autograd.Function):
                  res, dres, g2=g2, mask=mask)
         if ctx.res_join is not None and dres is not None:
             dres = ctx.res_join.contribute(dres)
-        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+
+
+# BN + ReLU + max-pool as one forward pass (bn_act_nhwc ``pool``); A/B switch (0: apply pass + pool)
+FUSE_BN_POOL = os.environ.get("DPA_FUSE_BN_POOL", "1") == "1"
 
 
 def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, training: bool = True,
                 momentum: float = 0.1, eps: float = 1e-5, act: str = "relu", residual: Optional[torch.Tensor] = None,
-                res_join: Optional[GradJoin] = None):
-    """``res_join``: the residual's gradient is one contribution of a GradJoin (ResNet identity)."""
+                res_join: Optional[GradJoin] = None, pool: Optional[Tuple[int, int, int]] = None):
+    """``res_join``: the residual's gradient is one contribution of a GradJoin (ResNet identity).
+    ``pool`` = (k, stride, pad): the output is max-pooled as well (ResNet stem); on GPU with ReLU the
+    pool applies BN + ReLU to its window loads and the BN output is never stored."""
     a = ACT[act]
+    if pool is not None:
+        if not (FUSE_BN_POOL and a == 0 and _native(z) and z.shape[-1] % 8 == 0
+                and z.dtype in (torch.float32, torch.bfloat16)):
+            out = bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, training, momentum, eps,
+                              act)
+            return max_pool_nhwc(out, *pool)
+        return BnActNHWC.apply(z.contiguous(), gamma, beta, None, running_mean, running_var, num_batches_tracked,
+                               bool(training), float(momentum), float(eps), a, None, tuple(int(v) for v in pool))
     if a == 2 and residual is None:
         raise ValueError("act='add_relu' needs a residual")
     res = residual.to(z.dtype).contiguous() if residual is not None else None

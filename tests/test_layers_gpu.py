@@ -185,6 +185,40 @@ def test_maxpool_nhwc_matches_torch(shape, k, s, p, dtype):
     assert (dx.cpu().double() - dxr.permute(0, 2, 3, 1)).abs().max() <= tol * dxr.abs().max()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,pool", [((4, 16, 16, 64), (3, 2, 1)), ((2, 15, 17, 16), (3, 2, 1)),
+                                        ((2, 8, 8, 8), (2, 2, 0))])
+def test_bn_relu_maxpool_fused_bitwise(monkeypatch, shape, pool, dtype):
+    """BN + ReLU applied in the max-pool's loads (bn_act_nhwc ``pool``, the ResNet stem) == the BN
+    apply pass followed by the pool: output, running statistics and every gradient bitwise."""
+    from distributed_pytorch_amd.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(5)
+    C = shape[-1]
+    z0 = (torch.randn(shape, generator=g) * 2 + 0.3).round(decimals=1).to(dtype).cuda()  # ties are common
+    gm0, bt0 = (torch.rand(C, generator=g) + 0.5).cuda(), (torch.randn(C, generator=g) * 0.2).cuda()
+    dy = None
+
+    def run(fused):
+        nonlocal dy
+        monkeypatch.setattr(Fn, "FUSE_BN_POOL", fused)
+        z = z0.clone().requires_grad_(True)
+        gm, bt = gm0.clone().requires_grad_(True), bt0.clone().requires_grad_(True)
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        nbt = torch.zeros(1, dtype=torch.long, device="cuda")
+        y = Fn.bn_act_nhwc(z, gm, bt, rm, rv, nbt, True, 0.1, 1e-5, "relu", pool=pool)
+        if dy is None:
+            dy = torch.randn(y.shape, generator=g).to(dtype).cuda()
+        y.backward(dy)
+        torch.cuda.synchronize()
+        return y, z.grad, gm.grad, bt.grad, rm, rv
+
+    ref, fused = run(False), run(True)
+    for a, b in zip(ref, fused):
+        assert a.shape == b.shape and torch.equal(a.view(-1).view(torch.int16) if a.dtype == torch.bfloat16 else a,
+                                                  b.view(-1).view(torch.int16) if b.dtype == torch.bfloat16 else b)
+
+
 def test_head_kernels_match_torch():
     """GAP + Linear + softmax-CE head (head.hip + hipBLASLt GEMMs) vs torch fp64: loss, dx (bf16),
     dW, db; and the logits head's backward."""
