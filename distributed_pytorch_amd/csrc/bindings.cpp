@@ -116,6 +116,9 @@ int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H
                      int sig_val);
 
 int dpa_set_signal(int* sig, int val, hipStream_t st);
+int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,
+                      const float* scale, const float* shift, long M, int C, int act, hipStream_t st,
+                      const float* rscale, const float* rshift);
 int dpa_maxpool_fwd(const void* x, void* y, unsigned char* arg, int N, int H, int W, int C, int k, int s, int p,
                     int bf, hipStream_t st, const float* scale, const float* shift);
 int dpa_maxpool_bwd(const void* dy, const unsigned char* arg, void* dx, int N, int H, int W, int C, int k, int s,
@@ -665,6 +668,28 @@ unsigned char* mask_ptr(const OptT& mask, const Tensor& z, const char* what) {
                   mask->numel() == z.numel() / 4,
               what, ": mask must be a contiguous uint8 CUDA tensor of z.numel() / 4 bytes");
   return mask->data_ptr<unsigned char>();
+}
+
+// BN + add + ReLU whose residual is another BatchNorm's INPUT rz (ResNet downsample branch): out =
+// relu(z*scale + shift + bf16(rz*rscale + rshift)), plus the ReLU mask; bf16 [N,H,W,C], C % 8 == 0.
+// Returns false when the 16-byte-lane kernel cannot run it (the caller applies the two BNs separately).
+bool bn_apply_rbn(Tensor z, Tensor out, Tensor scale, Tensor shift, Tensor rz, Tensor rscale, Tensor rshift,
+                  Tensor mask) {
+  for (const Tensor* t : {&z, &out, &rz}) need(*t, "bn_apply_rbn: z/out/rz", at::kBFloat16);
+  for (const Tensor* t : {&scale, &shift, &rscale, &rshift}) need(*t, "bn_apply_rbn: coefficients");
+  need(mask, "bn_apply_rbn: mask", at::kByte);
+  const int64_t C = z.size(-1);
+  TORCH_CHECK(out.numel() == z.numel() && rz.numel() == z.numel() && mask.numel() == z.numel() / 4 &&
+                  scale.numel() == C && shift.numel() == C && rscale.numel() == C && rshift.numel() == C,
+              "bn_apply_rbn: shapes");
+  const int rc = dpa_bn_apply_wide(reinterpret_cast<const unsigned short*>(z.data_ptr<at::BFloat16>()),
+                                   reinterpret_cast<const unsigned short*>(rz.data_ptr<at::BFloat16>()),
+                                   reinterpret_cast<unsigned short*>(out.data_ptr<at::BFloat16>()),
+                                   mask.data_ptr<uint8_t>(), fp(scale), fp(shift), z.numel() / C, (int)C, 2,
+                                   cur_stream(), fp(rscale), fp(rshift));
+  if (rc == 1) return false;
+  chk(rc, "bn_apply_rbn");
+  return true;
 }
 
 void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t act, OptT res, OptT mask) {
@@ -1368,6 +1393,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
   m.def("bn_eval_params", &bn_eval_params);
+  m.def("bn_apply_rbn", &bn_apply_rbn, py::arg("z"), py::arg("out"), py::arg("scale"), py::arg("shift"),
+        py::arg("rz"), py::arg("rscale"), py::arg("rshift"), py::arg("mask"));
   m.def("bn_apply", &bn_apply, py::arg("z"), py::arg("a"), py::arg("scale"), py::arg("shift"), py::arg("pool"),
         py::arg("act") = 0, py::arg("res") = py::none(), py::arg("mask") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"), py::arg("scale"),

@@ -32,7 +32,8 @@
 
 extern "C" {  // bn_wide.hip: bf16 apply passes with 16-byte lanes (return 1: not applicable)
 int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,
-                      const float* scale, const float* shift, long M, int C, int act, hipStream_t st);
+                      const float* scale, const float* shift, long M, int C, int act, hipStream_t st,
+                      const float* rscale, const float* rshift);
 int dpa_bn_bwd_apply_wide(const unsigned short* g, const unsigned short* g2, const unsigned short* z,
                           unsigned short* dz, const float* scale, const float* shift, const float* coef, long M, int C,
                           int act, hipStream_t st);
@@ -951,7 +952,7 @@ int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, co
                   int C, int pool, int act, const TZ* res, hipStream_t st, unsigned char* mask = nullptr) {
   if constexpr (sizeof(TZ) == 2) {  // bf16 in, one bf16 plane out: 16-byte lanes (bn_wide.hip)
     if (!pool && np == 1) {
-      const int rc = dpa_bn_apply_wide(z, res, a3, mask, scale, shift, (long)N * H * W, C, act, st);
+      const int rc = dpa_bn_apply_wide(z, res, a3, mask, scale, shift, (long)N * H * W, C, act, st, nullptr, nullptr);
       if (rc != 1) return rc;
     }
   }

@@ -36,21 +36,34 @@ constexpr int UNR = 4;
 
 // forward: ACT 0 relu(fma(z, sc, sh)); 1 fma(z, sc, sh); 2 relu(fma(z, sc, sh) + res) (+ ReLU mask,
 // one byte per 4 channels: bit k = channel 4*i + k of that group passed the ReLU)
-template <int ACT>
+// RBN (ACT 2): res is itself a BatchNorm input (the downsample branch's conv output); it is mapped
+// to fma(res, rscale, rshift) rounded to bf16 -- the value that BN's own apply pass (ACT 1) would
+// have stored -- so that pass and its output tensor go.
+template <int ACT, bool RBN = false>
 __global__ __launch_bounds__(256) void bn_apply_wide_kernel(const uint4* __restrict__ z, const uint4* __restrict__ res,
                                                             uint4* __restrict__ out, unsigned short* __restrict__ mask,
                                                             const float* __restrict__ scale,
-                                                            const float* __restrict__ shift, long total8, int C8) {
+                                                            const float* __restrict__ shift, long total8, int C8,
+                                                            const float* __restrict__ rscale = nullptr,
+                                                            const float* __restrict__ rshift = nullptr) {
   const long stride = (long)gridDim.x * blockDim.x;
   const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c8 = (int)(i0 % C8);
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   coef8(scale, c8, sc);
   coef8(shift, c8, sh);
+  if constexpr (RBN) {
+    coef8(rscale, c8, rsc);
+    coef8(rshift, c8, rsh);
+  }
   auto body = [&](uint4 zv, uint4 rv, long i) {
     float zf[8], rf[8], o[8];
     unpack8(zv, zf);
     if constexpr (ACT == 2) unpack8(rv, rf);
+    if constexpr (RBN) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rf[e] = __uint_as_float((unsigned)bf16_rne(fmaf(rf[e], rsc[e], rsh[e])) << 16);
+    }
     unsigned m = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -301,9 +314,12 @@ int dpa_bn_bwd_reduce_wide(const unsigned short* g, const unsigned short* g2, co
 }
 
 // bf16 [M][C] -> bf16 [M][C] (+ mask [M*C/4] bytes for act 2); returns 1 when not applicable (the
-// caller runs bn.hip's kernel), else a HIP error code
+// caller runs bn.hip's kernel), else a HIP error code.  rscale / rshift (act 2 only): the residual is a
+// BatchNorm input, added as bf16(fma(res, rscale, rshift)) (bn_apply_wide_kernel RBN).
 int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,
-                      const float* scale, const float* shift, long M, int C, int act, hipStream_t st) {
+                      const float* scale, const float* shift, long M, int C, int act, hipStream_t st,
+                      const float* rscale, const float* rshift) {
+  if ((rscale != nullptr) != (rshift != nullptr) || (rscale && act != 2)) return -2;
   if (!wide_on() || C % 8 || act < 0 || act > 2 || (act == 2 && !res)) return 1;
   if ((reinterpret_cast<uintptr_t>(z) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(res)) & 15 ||
       reinterpret_cast<uintptr_t>(mask) & 1)  // the mask is stored as 2-byte words
@@ -318,6 +334,8 @@ int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsign
     bn_apply_wide_kernel<0><<<grid, 256, 0, st>>>(zz, rr, oo, mm, scale, shift, total8, C / 8);
   else if (act == 1)
     bn_apply_wide_kernel<1><<<grid, 256, 0, st>>>(zz, rr, oo, mm, scale, shift, total8, C / 8);
+  else if (rscale)
+    bn_apply_wide_kernel<2, true><<<grid, 256, 0, st>>>(zz, rr, oo, mm, scale, shift, total8, C / 8, rscale, rshift);
   else
     bn_apply_wide_kernel<2><<<grid, 256, 0, st>>>(zz, rr, oo, mm, scale, shift, total8, C / 8);
   return (int)hipGetLastError();

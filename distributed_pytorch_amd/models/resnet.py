@@ -54,8 +54,8 @@ class Bottleneck(nn.Module):
                 x.register_hook(j.guard)
         out = self.bn1(self.conv1(x, j))
         out = self.bn2(self.conv2(out))
-        if self.downsample is not None:
-            return self.bn3(self.conv3(out), self.downsample[1](self.downsample[0](x, j)))
+        if self.downsample is not None:  # the downsample BN is applied inside bn3's add (one pass on GPU)
+            return self.bn3(self.conv3(out), self.downsample[0](x, j), res_bn=self.downsample[1])
         return self.bn3(self.conv3(out), x, res_join=j)
 
 

@@ -570,30 +570,64 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0,
     return Conv2dNHWC.apply(x.contiguous(), w, int(stride), int(pad), impl, join, torch.is_grad_enabled())
 
 
+def _bn_coefs(K, z, gamma, beta, rmean, rvar, nbt, training: bool, momentum: float, eps: float):
+    """(mean, invstd, scale, shift) of a BatchNorm over z [N,H,W,C]: from the producing conv's
+    epilogue partials when it registered them, else a statistics pass (training), or the running
+    statistics (eval).  Updates the running statistics in training."""
+    N, H, W, C = z.shape
+    dev = z.device
+    # per-channel statistics in fp32 on GPU (bf16 activations too); the CPU oracle also runs fp64
+    f32 = dict(device=dev, dtype=torch.float32 if _native(z) else z.dtype)
+    mean, invstd, scale, shift = (torch.empty(C, **f32) for _ in range(4))
+    st = _STATS.pop(z.data_ptr(), None) if training and _native(z) else None
+    if st is not None and st[3] == (N * H * W, C):  # partials from the producing conv's epilogue
+        K.bn_finalize(st[0], st[1], st[2], N * H * W, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale,
+                      shift, momentum, eps)
+        STATS_USED["epilogue"] += 1
+    elif training:
+        part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), dev, zero=True) if _native(z) else None
+        K.bn_fwd_stats(z, 1, z, part, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale, shift, momentum, eps)
+    else:
+        K.bn_eval_params(gamma, beta, None, rmean, rvar, scale, shift, eps)
+    return mean, invstd, scale, shift
+
+
+def _bn_grad_bufs(params, C: int, f32: dict):
+    """dgamma / dbeta: the optimizer's direct slots when the parameters have them."""
+    out = []
+    for p in params:
+        d = grad_slot(p)
+        out.append(d if d is not None and d.dtype == f32["dtype"] else torch.empty(C, **f32))
+    return out
+
+
 class BnActNHWC(torch.autograd.Function):
+    """Training / eval BatchNorm2d + activation on NHWC.  Optional fusions: ``pool`` (the output is
+    max-pooled inside the pool's loads, ResNet stem) and ``rgamma``/``rbeta``/``rstate`` (act 2 only:
+    ``res`` is the INPUT of a second BatchNorm -- the downsample branch -- whose BN is applied inside
+    the add's loads; its backward runs here after this one's)."""
+
     @staticmethod
     def forward(ctx, z, gamma, beta, res, rmean, rvar, nbt, training: bool, momentum: float, eps: float, act: int,
-                res_join: Optional[GradJoin] = None, pool: Optional[Tuple[int, int, int]] = None):
+                res_join: Optional[GradJoin] = None, pool: Optional[Tuple[int, int, int]] = None,
+                rgamma=None, rbeta=None, rstate=None):
         N, H, W, C = z.shape
         dev = z.device
         K = _ext.require() if _native(z) else cpu_ref
-        # per-channel statistics in fp32 on GPU (bf16 activations too); the CPU oracle also runs fp64
-        f32 = dict(device=dev, dtype=torch.float32 if _native(z) else z.dtype)
-        mean, invstd, scale, shift = (torch.empty(C, **f32) for _ in range(4))
-        st = _STATS.pop(z.data_ptr(), None) if training and _native(z) else None
-        if st is not None and st[3] == (N * H * W, C):  # partials from the producing conv's epilogue
-            K.bn_finalize(st[0], st[1], st[2], N * H * W, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale,
-                          shift, momentum, eps)
-            STATS_USED["epilogue"] += 1
-        elif training:
-            part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), dev, zero=True) if _native(z) else None
-            K.bn_fwd_stats(z, 1, z, part, gamma, beta, None, rmean, rvar, nbt, mean, invstd, scale, shift, momentum,
-                           eps)
-        else:
-            K.bn_eval_params(gamma, beta, None, rmean, rvar, scale, shift, eps)
+        rbn = rgamma is not None
+        if rbn:  # the residual branch's BN first (its statistics come from the downsample conv)
+            rco = _bn_coefs(K, res, rgamma, rbeta, *rstate[:3], training, *rstate[3:])
+        mean, invstd, scale, shift = _bn_coefs(K, z, gamma, beta, rmean, rvar, nbt, training, momentum, eps)
         arg = None
         mask = None
-        if pool is not None:
+        if rbn:
+            a = torch.empty_like(z)
+            mask = torch.empty(z.numel() // 4, dtype=torch.uint8, device=dev)
+            if not K.bn_apply_rbn(z, a, scale, shift, res, rco[2], rco[3], mask):
+                r = torch.empty_like(res)
+                K.bn_apply(res, r, rco[2], rco[3], False, 1)
+                K.bn_apply(z, a, scale, shift, False, 2, r, mask=mask)
+        elif pool is not None:
             # BN + ReLU applied inside the max-pool's loads (the ResNet stem): the BN output is never
             # stored; the pool's window positions route the backward
             k, st_, pd = pool
@@ -607,19 +641,21 @@ class BnActNHWC(torch.autograd.Function):
             mask = (torch.empty(z.numel() // 4, dtype=torch.uint8, device=dev)
                     if act == 2 and training and _native(z) and BN_RELU_MASK else None)
             K.bn_apply(z, a, scale, shift, False, act, res if act == 2 else None, mask=mask)
-        ctx.act, ctx.training, ctx.pool = act, training, pool
+        ctx.act, ctx.training, ctx.pool, ctx.rbn = act, training, pool, rbn
         ctx.res_join = res_join
-        ctx.params = (gamma, beta)
+        ctx.params = (gamma, beta) + ((rgamma, rbeta) if rbn else ())
         if training:
-            note_use(gamma)
-            note_use(beta)
+            for p in ctx.params:
+                note_use(p)
+        rsave = (res, rgamma) + tuple(rco[:4]) if rbn else (None,) * 6
         ctx.save_for_backward(z, res if act == 2 and mask is None else None, mask, gamma, mean, invstd, scale, shift,
-                              arg)
+                              arg, *rsave)
         return a
 
     @staticmethod
     def backward(ctx, da):
-        z, res, mask, gamma, mean, invstd, scale, shift, arg = ctx.saved_tensors
+        z, res, mask, gamma, mean, invstd, scale, shift, arg, rz, rgamma, rmean, rinvstd, rscale, rshift = \
+            ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("bn_act_nhwc backward is only defined in training mode")
         # a deferred second contribution to da (GradJoin.register; never for the pooled form)
@@ -635,11 +671,7 @@ class BnActNHWC(torch.autograd.Function):
             da = dpre
         f32 = dict(device=z.device, dtype=torch.float32 if native else z.dtype)
         dz = torch.empty_like(z)
-        dgamma, dbeta = (grad_slot(p) for p in ctx.params)
-        if dgamma is None or dgamma.dtype != f32["dtype"]:
-            dgamma = torch.empty(C, **f32)
-        if dbeta is None or dbeta.dtype != f32["dtype"]:
-            dbeta = torch.empty(C, **f32)
+        dgamma, dbeta = _bn_grad_bufs(ctx.params[:2], C, f32)
         dres = torch.empty_like(z) if ctx.act == 2 else None
         part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), z.device, zero=True) if native else None
         coef = torch.empty(3 * C, **f32)
@@ -652,22 +684,47 @@ class BnActNHWC(torch.autograd.Function):
                 da = da + ent[1].view_as(da)
         K.bn_bwd(da, 1, da, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, None, dz, False, ctx.act,
                  res, dres, g2=g2, mask=mask)
+        if ctx.rbn:  # dres is the gradient of the residual BN's output: its backward (identity act)
+            drz = torch.empty_like(rz)
+            drg, drb = _bn_grad_bufs(ctx.params[2:], C, f32)
+            K.bn_bwd(dres, 1, dres, rz, rscale, rshift, rmean, rinvstd, rgamma, part, coef, drg, drb, None, drz, False,
+                     1, None, None)
+            return dz, dgamma, dbeta, drz, None, None, None, None, None, None, None, None, None, drg, drb, None
         if ctx.res_join is not None and dres is not None:
             dres = ctx.res_join.contribute(dres)
-        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 # BN + ReLU + max-pool as one forward pass (bn_act_nhwc ``pool``); A/B switch (0: apply pass + pool)
 FUSE_BN_POOL = os.environ.get("DPA_FUSE_BN_POOL", "1") == "1"
+# the downsample branch's BN applied inside the block's add + ReLU (bn_act_nhwc ``res_bn``); A/B switch
+FUSE_RES_BN = os.environ.get("DPA_FUSE_RES_BN", "1") == "1"
 
 
 def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, training: bool = True,
                 momentum: float = 0.1, eps: float = 1e-5, act: str = "relu", residual: Optional[torch.Tensor] = None,
-                res_join: Optional[GradJoin] = None, pool: Optional[Tuple[int, int, int]] = None):
+                res_join: Optional[GradJoin] = None, pool: Optional[Tuple[int, int, int]] = None,
+                res_bn=None):
     """``res_join``: the residual's gradient is one contribution of a GradJoin (ResNet identity).
     ``pool`` = (k, stride, pad): the output is max-pooled as well (ResNet stem); on GPU with ReLU the
-    pool applies BN + ReLU to its window loads and the BN output is never stored."""
+    pool applies BN + ReLU to its window loads and the BN output is never stored.
+    ``res_bn`` (act 'add_relu'): a BatchNorm2d module (act 'none') whose INPUT ``residual`` is; the
+    residual added is res_bn(residual).  In training on GPU (bf16) it is applied inside the add's loads
+    and its output is never stored (ResNet downsample branch)."""
     a = ACT[act]
+    if res_bn is not None:
+        m = res_bn
+        if not (FUSE_RES_BN and BN_RELU_MASK and a == 2 and training and m.act == "none" and _native(z)
+                and z.dtype == torch.bfloat16 and residual is not None and residual.dtype == torch.bfloat16
+                and residual.shape == z.shape and z.shape[-1] % 8 == 0):
+            residual = m(residual)
+        else:
+            rstate = (m.running_mean, m.running_var, m.num_batches_tracked.view(1), float(m.momentum), float(m.eps))
+            out = BnActNHWC.apply(z.contiguous(), gamma, beta, residual.contiguous(), running_mean, running_var,
+                                  num_batches_tracked, bool(training), float(momentum), float(eps), a, None, None,
+                                  m.weight, m.bias, rstate)
+            out._dpa_sum_on_load = out.requires_grad  # (as below: a deferred contribution is summed on load)
+            return out
     if pool is not None:
         if not (FUSE_BN_POOL and a == 0 and _native(z) and z.shape[-1] % 8 == 0
                 and z.dtype in (torch.float32, torch.bfloat16)):

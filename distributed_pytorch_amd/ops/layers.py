@@ -66,11 +66,12 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
-    def forward(self, z, residual=None, res_join=None, pool=None):
-        """``pool`` = (k, stride, pad): also max-pool the output (fused on GPU, see Fn.bn_act_nhwc)."""
+    def forward(self, z, residual=None, res_join=None, pool=None, res_bn=None):
+        """``pool`` = (k, stride, pad): also max-pool the output; ``res_bn``: ``residual`` is the input of
+        that BatchNorm2d module (fused on GPU, see Fn.bn_act_nhwc)."""
         nbt = self.num_batches_tracked.view(1) if self.training else None
         return Fn.bn_act_nhwc(z, self.weight, self.bias, self.running_mean, self.running_var, nbt, self.training,
-                              self.momentum, self.eps, self.act, residual, res_join, pool)
+                              self.momentum, self.eps, self.act, residual, res_join, pool, res_bn)
 
     def extra_repr(self):
         return f"{self.c}, act={self.act}"

@@ -219,6 +219,43 @@ def test_bn_relu_maxpool_fused_bitwise(monkeypatch, shape, pool, dtype):
                                                   b.view(-1).view(torch.int16) if b.dtype == torch.bfloat16 else b)
 
 
+@pytest.mark.parametrize("cin,width,stride,hw", [(64, 64, 1, 14), (256, 128, 2, 14), (64, 32, 2, 9)])
+def test_downsample_bn_fused_into_add_bitwise(monkeypatch, cin, width, stride, hw):
+    """A bottleneck with a downsample branch: its BN applied inside bn3's add + ReLU (bn_act_nhwc
+    ``res_bn``, no stored BN output) == the separate BN pass: output, input gradient, every parameter
+    gradient and the running statistics bitwise."""
+    from distributed_pytorch_amd.models.resnet import Bottleneck
+    from distributed_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(3)
+    ref = Bottleneck(cin, width, stride, True, "bf16").cuda()
+    g = torch.Generator().manual_seed(4)
+    x0 = torch.randn(4, hw, hw, cin, generator=g).to(torch.bfloat16).cuda()
+    dy = None
+
+    def run(fused):
+        nonlocal dy
+        monkeypatch.setattr(Fn, "FUSE_RES_BN", fused)
+        m = Bottleneck(cin, width, stride, True, "bf16").cuda()
+        m.load_state_dict(ref.state_dict())
+        x = x0.clone().requires_grad_(True)
+        y = m(x)
+        if dy is None:
+            dy = torch.randn(y.shape, generator=g).to(torch.bfloat16).cuda()
+        y.backward(dy)
+        torch.cuda.synchronize()
+        grads = [p.grad for _, p in sorted(m.named_parameters())]
+        bufs = [b for _, b in sorted(m.named_buffers())]
+        return [y, x.grad] + grads + bufs
+
+    a, b = run(False), run(True)
+    assert len(a) == len(b)
+    for u, v in zip(a, b):
+        assert u is not None and v is not None and u.shape == v.shape
+        assert torch.equal(u.view(-1).view(torch.int16) if u.dtype == torch.bfloat16 else u,
+                           v.view(-1).view(torch.int16) if v.dtype == torch.bfloat16 else v)
+
+
 def test_head_kernels_match_torch():
     """GAP + Linear + softmax-CE head (head.hip + hipBLASLt GEMMs) vs torch fp64: loss, dx (bf16),
     dW, db; and the logits head's backward."""
