@@ -153,6 +153,77 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// 3x3 / stride 2 / pad 1 backward (the ResNet stem), one thread per 2x2 input block x 8 channels: the
+// block's pixels are covered by exactly the windows (m..m+1, n..n+1); each window's dy and positions
+// are loaded once for the four pixels (the general gather loads them once per covered pixel, 2.25x
+// on average).  Per pixel, windows are summed in the general kernel's ascending (oh, ow) order:
+// bitwise its result.
+template <typename T, typename IT>
+__global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const T* __restrict__ dy,
+                                                               const unsigned char* __restrict__ arg,
+                                                               T* __restrict__ dx, PoolGeom g) {
+  const int Hb = (g.H + 1) / 2, Wb = (g.W + 1) / 2;
+  const IT total = (IT)g.N * Hb * Wb * g.C8;
+  for (IT i = (IT)blockIdx.x * 256u + threadIdx.x; i < total; i += (IT)gridDim.x * 256u) {
+    const int c8 = (int)(i % (IT)g.C8);
+    IT r = i / (IT)g.C8;
+    const int bn = (int)(r % (IT)Wb);
+    r /= (IT)Wb;
+    const int bm = (int)(r % (IT)Hb);
+    const int n = (int)(r / (IT)Hb);
+    float v[2][2][8];
+    unsigned char a[2][2][8];
+#pragma unroll
+    for (int wi = 0; wi < 2; ++wi)
+#pragma unroll
+      for (int wj = 0; wj < 2; ++wj) {
+        const int oh = bm + wi, ow = bn + wj;
+        const bool ok = oh < g.P && ow < g.Q;
+        const long o = (((long)n * g.P + (ok ? oh : 0)) * g.Q + (ok ? ow : 0)) * g.C8 + c8;
+        if (ok) {
+          V8<T>::load(dy + o * 8, v[wi][wj]);
+          const uint2 packed = *reinterpret_cast<const uint2*>(arg + o * 8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            a[wi][wj][k] = (unsigned char)(((k < 4 ? packed.x : packed.y) >> (8 * (k & 3))) & 0xFFu);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            v[wi][wj][k] = 0.f;
+            a[wi][wj][k] = 0xFF;  // matches no window position
+          }
+        }
+      }
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int h = 2 * bm + dh, w = 2 * bn + dw;
+        if (h >= g.H || w >= g.W) continue;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int wi = 0; wi < 2; ++wi)
+#pragma unroll
+          for (int wj = 0; wj < 2; ++wj) {
+            const int kh = h - 2 * (bm + wi) + 1, kw = w - 2 * (bn + wj) + 1;  // position in window
+            if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;
+            const unsigned char pos = (unsigned char)(kh * 3 + kw);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (a[wi][wj][k] == pos) acc[k] += v[wi][wj][k];
+          }
+        V8<T>::store(dx + (((long)n * g.H + h) * g.W + w) * (g.C8 * 8) + c8 * 8, acc);
+      }
+  }
+}
+
+bool k3s2_on() {
+  const char* e = getenv("DPA_POOL_K3S2");  // read per call: tests switch it in-process
+  return !(e && e[0] == '0');
+}
+
 int grid_for(long n) {
   long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -195,6 +266,19 @@ int dpa_maxpool_bwd(const void* dy, const unsigned char* arg, void* dx, int N, i
   PoolGeom g{N, H, W, C / 8, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
   const long total = (long)g.N * g.H * g.W * g.C8;
   const bool small = total + 8192L * 256 < (1L << 32);
+  if (k == 3 && s == 2 && p == 1 && k3s2_on()) {
+    const long tb = (long)g.N * ((H + 1) / 2) * ((W + 1) / 2) * g.C8;
+    if (bf && small)
+      maxpool_bwd_k3s2_kernel<u16, unsigned><<<grid_for(tb), 256, 0, st>>>((const u16*)dy, arg, (u16*)dx, g);
+    else if (bf)
+      maxpool_bwd_k3s2_kernel<u16, unsigned long><<<grid_for(tb), 256, 0, st>>>((const u16*)dy, arg, (u16*)dx, g);
+    else if (small)
+      maxpool_bwd_k3s2_kernel<float, unsigned><<<grid_for(tb), 256, 0, st>>>((const float*)dy, arg, (float*)dx, g);
+    else
+      maxpool_bwd_k3s2_kernel<float, unsigned long><<<grid_for(tb), 256, 0, st>>>((const float*)dy, arg, (float*)dx,
+                                                                                   g);
+    return (int)hipGetLastError();
+  }
   if (bf && small)
     maxpool_bwd_kernel<u16, unsigned><<<grid_for(total), 256, 0, st>>>((const u16*)dy, arg, (u16*)dx, g);
   else if (bf)

@@ -185,6 +185,26 @@ def test_maxpool_nhwc_matches_torch(shape, k, s, p, dtype):
     assert (dx.cpu().double() - dxr.permute(0, 2, 3, 1)).abs().max() <= tol * dxr.abs().max()
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 9, 7, 16), (1, 10, 10, 8), (2, 1, 2, 8)])
+def test_maxpool_k3s2_backward_bitwise(monkeypatch, shape, dtype):
+    """The 3x3/s2/p1 backward specialisation (2x2 input pixels per thread, each window loaded once)
+    == the general gather, bitwise (same per-pixel summation order), ties included."""
+    from distributed_pytorch_amd.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(shape, generator=g).round(decimals=1).to(dtype).cuda().requires_grad_(True)
+    y = Fn.max_pool_nhwc(x, 3, 2, 1)
+    dy = torch.randn(y.shape, generator=g).to(dtype).cuda()
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("DPA_POOL_K3S2", on)
+        (dx,) = torch.autograd.grad(y, x, dy, retain_graph=True)
+        torch.cuda.synchronize()
+        out.append(dx.view(torch.int16) if dtype == torch.bfloat16 else dx)
+    assert torch.equal(out[0], out[1])
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape,pool", [((4, 16, 16, 64), (3, 2, 1)), ((2, 15, 17, 16), (3, 2, 1)),
                                         ((2, 8, 8, 8), (2, 2, 0))])
