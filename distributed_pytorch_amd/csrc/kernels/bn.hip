@@ -350,20 +350,17 @@ __global__ __launch_bounds__(256) void bn_finalize_cm_kernel(const float2* __res
   const int c = blockIdx.x, t = threadIdx.x;
   const float2* pc = part + (long)c * nblk;
   Welford acc{0.f, 0.f, 0.f};
-  int k = t;
-  for (; k + 7 * 256 < nblk; k += 8 * 256) {
+  // 8 partials per thread in flight (guarded: the ResNet-50 epilogue partials, ~400-1600 per
+  // channel, are 2-7 per thread -- a rolled tail loop paid one memory latency each), same order
+  for (int k = t; k < nblk; k += 8 * 256) {
     float2 p[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) p[u] = pc[k + 256 * u];
+    for (int u = 0; u < 8; ++u) p[u] = k + 256 * u < nblk ? pc[k + 256 * u] : make_float2(0.f, 0.f);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int kk = k + 256 * u;
-      acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
+      if (kk < nblk) acc = merge(acc, Welford{(float)min(rpb, M - kk * rpb), p[u].x, p[u].y});
     }
-  }
-  for (; k < nblk; k += 256) {
-    const float2 p = pc[k];
-    acc = merge(acc, Welford{(float)min(rpb, M - k * rpb), p.x, p.y});
   }
   __shared__ Welford sh[256];
   sh[t] = acc;
