@@ -156,7 +156,20 @@ __global__ __launch_bounds__(256) void head_bwd_prep_kernel(const float* __restr
   if (j >= J) return;
   const float g = gout[0];
   float s = 0.f;
-  for (int n = 0; n < N; ++n) {
+  int n = 0;
+  // 16 rows' loads in flight (the rolled loop paid one memory latency per row: 33 us for N = 128 on
+  // the ResNet-50 step); rows still summed in order
+  for (; n + 16 <= N; n += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = dlogits[(long)(n + u) * J + j] * g;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      dl[(long)(n + u) * J + j] = v[u];
+      s += v[u];
+    }
+  }
+  for (; n < N; ++n) {
     const float v = dlogits[(long)n * J + j] * g;
     dl[(long)n * J + j] = v;
     s += v;
