@@ -53,7 +53,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (reference: 256 per node)")
     ap.add_argument("--mode", default="ddp", choices=["ddp", "allreduce", "gather", "zero1"])
     ap.add_argument("--model", default="VGG11")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"])
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "ipc", "torch", "gloo"],
+                    help="ipc: every collective on the peer-memory kernels (one node; ranks may share a GPU)")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--device", default="auto")
@@ -78,14 +79,12 @@ def parse(argv=None):
     ap.add_argument("--ipc", default="auto", choices=["auto", "on", "off"],
                     help="N>1 on one node: bucket all-reduces on the peer-memory kernel (parallel/ipc.py). "
                          "auto = one more comm-tuner plan; on = always (any --comm; several ranks may share a GPU)")
+    ap.add_argument("--ipc-blocks", default="32,16,64",
+                    help="workgroups per rank of the peer-memory collectives the comm tuner tries (comma list; the "
+                         "first is the --ipc on / --comm ipc default unless DPA_IPC_BLOCKS is set)")
     ap.add_argument("--rccl-channels", default="16,8",
                     help="N>1 with the native RCCL communicator: channel (workgroup) budgets the comm tuner also "
                          "tries, each on its own communicator (comma list; 'off' = RCCL's default only)")
-    ap.add_argument("--defer-update", default="auto", choices=["auto", "on", "off"],
-                    help="run each step's SGD at the start of the next step on the weight-gradient stream, idle "
-                         "during the forward (engine.defer_update; bitwise the same updates; the timed region ends "
-                         "with the last step's update).  auto = DPA_DEFER_UPDATE=1 (default 0: same-box A/B 172.0k immediate vs 163.5k "
-                         "deferred img/s, docs/PERF_NOTES.md); never with a HIP graph")
     ap.add_argument("--profile", action="store_true",
                     help="re-run this command under rocprofv3 --kernel-trace --stats (prints the command)")
     ap.add_argument("--profile-dir", default="gpurun_out/prof")
@@ -154,12 +153,13 @@ def make_step(engine, sync, it, graphed=None, probe=None):
 
 def comm_plans(a, rccl: bool = False, ipc: bool = False):
     """Candidate gradient-sync plans (bucket_mb, tail_mb, per-bucket update, rccl_channels,
-    ipc) for the warmup tuner.  Per-tensor modes keep their granularity (the reference's semantics)
+    ipc_blocks) for the warmup tuner.  Per-tensor modes keep their granularity (the reference's semantics)
     and only try the update placement; an explicit --bucket-mb pins the bucket size.  With a native
     RCCL communicator (``rccl``) the default plan is also tried on communicators limited to
     ``--rccl-channels`` workgroups: fewer RCCL workgroups leave more CUs to the backward the
     collectives overlap (channels 0 = the communicator RCCL sized itself).  ``ipc``: the default
-    plan is also tried with the bucket all-reduces on the peer-memory kernel (parallel/ipc.py)."""
+    plan is also tried with every collective on the peer-memory kernels (parallel/ipc.py), at each of
+    the ``--ipc-blocks`` workgroup budgets."""
     fixed = a.bucket_mb
     if a.mode == "ddp":
         sizes = [fixed] if fixed is not None else [10.0, 25.0, 5.0]
@@ -171,14 +171,19 @@ def comm_plans(a, rccl: bool = False, ipc: bool = False):
         plans = []
     if plans and rccl:
         plans += [plans[0][:3] + (c, False) for c in channel_budgets(a)]
-    if plans and ipc:
-        plans += [plans[0][:3] + (0, True)]
+    if plans and ipc:  # p[4]: the peer kernels' workgroups per rank (0: no peer kernels)
+        plans += [plans[0][:3] + (0, b) for b in ipc_block_budgets(a)]
     seen, out = set(), []
     for p in plans:
         if p not in seen:
             seen.add(p)
             out.append(p)
     return out
+
+
+def ipc_block_budgets(a):
+    """Workgroups per rank the tuner tries for the peer-memory collectives (``--ipc-blocks``)."""
+    return [int(b) for b in a.ipc_blocks.split(",") if int(b) > 0]
 
 
 def channel_budgets(a):
@@ -208,14 +213,15 @@ def ipc_possible(ctx, dev) -> bool:
             and int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world)) == ctx.world and ctx.world <= 8)
 
 
-def ipc_comm(ctx, dev, engine, cache: dict):
-    """The peer-memory communicator over ctx.comm with the gradient arena registered (collective)."""
+def ipc_comm(ctx, dev, engine, cache: dict, blocks: int = 0):
+    """The peer-memory communicator over ctx.comm with the engine's arenas registered (collective).
+    Plans with different workgroup budgets share it (``blocks`` is a per-collective launch size)."""
     if "ipc" not in cache:
         from distributed_pytorch_amd.parallel.ipc import IpcComm
 
         store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
-        c = IpcComm(ctx.comm, store, dev, timeout_s=float(os.environ.get("DPA_IPC_TUNE_TIMEOUT", "20")))
-        c.register(engine.grads.flat)
+        c = IpcComm(ctx.comm, store, dev, timeout_s=20.0)
+        c.prepare([engine.grads.flat, engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt])
         cache["ipc"] = c
     return cache["ipc"]
 
@@ -231,7 +237,7 @@ def ipc_agrees(ipc, flat: torch.Tensor, dev) -> bool:
     torch.cuda.synchronize(dev)
     err = (flat - ref).abs().max().item()
     scale = ref.abs().max().item()
-    return err <= 1e-5 * max(scale, 1e-30) and not ipc._c.take_timeout()
+    return err <= 1e-5 * max(scale, 1e-30) and not ipc.timed_out()
 
 
 def tune_comm(a, engine, sync, ctx, dev, batches):
@@ -252,17 +258,23 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     if ctx.world <= 1 or a.comm_tune == "off" or len(plans) < 2 or a.no_overlap:
         return sync, None
     it = batches()
-    engine.flush_update()
     snap = [t.clone() for t in (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt,
                                 engine.loss_accum)]
     steps_taken = engine.steps_taken
     syncs, comms = {}, {}
     for p in list(plans):
+        err = None
         try:
             comm = ipc_comm(ctx, dev, engine, comms) if p[4] else comm_for_channels(ctx, dev, p[3], comms)
-        except RuntimeError as e:  # deterministic on every rank (a config RCCL refuses): drop the plan
-            print(f"[rank {ctx.rank}] comm tuner: no communicator for plan {p} ({e})", flush=True)
+        except RuntimeError as e:
+            err = e
+        # a plan is dropped on EVERY rank if its communicator failed on ANY rank (a rank-local
+        # failure must not leave the ranks with different plan lists: mismatched collectives hang)
+        if ctx.all_max(1.0 if err is not None else 0.0) > 0:
+            print(f"[rank {ctx.rank}] comm tuner: no communicator for plan {p} ({err or 'failed on a peer'})",
+                  flush=True)
             plans.remove(p)
+            comms.pop("ipc" if p[4] else p[3], None)
             continue
         s = make_sync(a.mode, engine, comm, bucket_mb=p[0], overlap=True, broadcast_init=False, tail_mb=p[1])
         s.fuse_step = p[2] and s.fusable_step
@@ -271,6 +283,8 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     score = {}
     for _rep in range(2):
         for p in plans:
+            if p[4]:
+                comms["ipc"].blocks = p[4]
             step = make_step(engine, syncs[p], it)
             for _ in range(2):
                 step()
@@ -284,7 +298,7 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     # a plan whose peer-memory waits timed out (any rank), or whose all-reduce of the real gradient
     # arena disagrees with the communicator's (beyond summation-order rounding), is disqualified
     if "ipc" in comms:
-        bad = ctx.all_max(1.0 if comms["ipc"]._c.take_timeout() else 0.0) > 0
+        bad = ctx.all_max(1.0 if comms["ipc"].timed_out() else 0.0) > 0
         if not bad:
             bad = ctx.all_max(0.0 if ipc_agrees(comms["ipc"], engine.grads.flat, dev) else 1.0) > 0
         if bad:
@@ -306,11 +320,12 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
         if hasattr(sy, "_bufs_fresh"):
             sy._bufs_fresh = False  # the next forward broadcasts rank 0's (restored) buffers again
     report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2],
-                         "rccl_channels": best[3] or None, "ipc_allreduce": best[4]},
+                         "rccl_channels": best[3] or None, "ipc_blocks": best[4] or None},
               "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else "")
-                              + ("_ipc" if p[4] else ""): round(score[p], 4) for p in plans}}
+                              + (f"_ipc{p[4]}" if p[4] else ""): round(score[p], 4) for p in plans}}
     if best[4]:  # the peer-memory communicator carries the run from here on
         ctx.comm = comms.pop("ipc")
+        ctx.comm.blocks = best[4]
     elif best[3]:  # the bounded communicator carries the run from here on (and the replica check)
         ctx.comm = comms.pop(best[3])
     for c in comms.values():  # the other bounded communicators are drained and left idle
@@ -371,18 +386,11 @@ def main(argv=None):
         store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
         ctx.comm = IpcComm(ctx.comm, store, dev)
     engine, sync, batches = build_parts(a, dev, ctx.rank, ctx.world, ctx.comm)
-    if a.ipc == "on" and hasattr(ctx.comm, "register"):
-        ctx.comm.register(engine.grads.flat)
     sync, tune_report = tune_comm(a, engine, sync, ctx, dev, batches)
     it = batches()
     graphed = (GraphedStep(engine, sync, fallback=a.graph == "auto")
                if a.graph != "off" and ctx.world == 1 and not sync.active and dev.type == "cuda" else None)
-    engine.defer_update = (a.defer_update == "on" or (a.defer_update == "auto" and
-                                                      os.environ.get("DPA_DEFER_UPDATE", "0") == "1")) \
-        and graphed is None and dev.type == "cuda"
-    # the flush after the timed loop keeps the last step's (deferred) update inside the timed region
-    el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev,
-                              flush=engine.flush_update)
+    el = benchlib.timed_steps(make_step(engine, sync, it, graphed), a.steps, a.warmup, ctx, dev)
     engine.check_signals()
     loss = float(engine.loss.item())
     ms = el / a.steps * 1e3
@@ -403,7 +411,6 @@ def main(argv=None):
         sync.__dict__.pop("finish", None)  # drop make_step's probe wrapper
         diag = step_comm_report(samples, len(sync.buckets))
         diag["exposed_comm_ms"] = ctx.all_max(diag["exposed_comm_ms"] or 0.0)
-    engine.flush_update()
     benchlib.device_barrier(ctx, dev)
     pdiff = benchlib.replicas_max_diff(ctx.comm, engine.params.flat)
     if dev.type == "cuda":
@@ -437,13 +444,16 @@ def main(argv=None):
                        "bucket_mb": [round(4 * b.numel / 2 ** 20, 3) for b in sync.buckets] if sync.active else None,
                        "per_bucket_update": bool(sync.fuse_step), "comm_tune": tune_report,
                        "overlap": not a.no_overlap, "launcher": launcher,
-                       "deferred_update": bool(engine.defer_update),
                        "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)"},
             "per_gpu_img_s": round(per_gpu, 1),
             "solo_img_s": round(solo_img_s, 1) if solo_img_s else None,
             "scaling_efficiency": round(per_gpu / solo_img_s, 4) if solo_img_s else None,
             "rccl_world": cw,
             "ipc_allreduce_ops": getattr(ctx.comm, "ipc_ops", None),
+            # peer-memory collectives by kind, and collectives the IPC communicator handed to the
+            # communicator it wraps (0 with --comm ipc: no tensor byte through gloo / the host)
+            "ipc_ops_by_kind": dict(ctx.comm.ops) if hasattr(ctx.comm, "ops") else None,
+            "ipc_inner_tensor_ops": getattr(ctx.comm, "inner_tensor_ops", None),
             "replicas_identical": pdiff == 0.0,
             "replica_param_max_diff": pdiff,
             "comm_diag": diag,

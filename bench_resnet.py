@@ -37,7 +37,7 @@ def main(argv=None):
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--impl", default="bf16", choices=["bf16", "x3"])
     ap.add_argument("--bucket-mb", type=float, default=25.0)
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"])
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "ipc", "torch", "gloo"])
     ap.add_argument("--autotune", action="store_true",
                     help="time every conv kernel config during warmup and save tuning/generic_mi355x.json")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],

@@ -19,6 +19,7 @@ import argparse
 import concurrent.futures as cf
 import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -47,11 +48,25 @@ def _sources():
     return kern, host
 
 
-def _headers():
-    hs = []
-    for root, _, files in os.walk(CSRC):
-        hs += [os.path.join(root, f) for f in files if f.endswith((".h", ".hpp", ".cuh", ".inc"))]
-    return sorted(hs)
+_INC = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def _deps(src, seen=None):
+    """The in-tree headers ``src`` includes, transitively (quoted includes resolved against the
+    including file's directory, then csrc/): a source is rebuilt only when one of ITS headers
+    changes."""
+    seen = set() if seen is None else seen
+    with open(src, encoding="utf-8", errors="replace") as f:
+        text = f.read()
+    for inc in _INC.findall(text):
+        for base in (os.path.dirname(src), CSRC):
+            h = os.path.normpath(os.path.join(base, inc))
+            if os.path.isfile(h):
+                if h not in seen:
+                    seen.add(h)
+                    _deps(h, seen)
+                break
+    return sorted(seen)
 
 
 def _digest(path, extra):
@@ -80,14 +95,13 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     tdir, torch_inc, torch_lib = _torch_paths()
     os.makedirs(BUILD_DIR, exist_ok=True)
     kern, host = _sources()
-    hdrs = _headers()
     jobs = jobs or max(1, min(8, os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "8"))))
     todo, objs = [], []
     for src in kern + host:
         rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
         obj = os.path.join(BUILD_DIR, rel + ".o")
         stamp = obj + ".sha1"
-        dig = _digest(src, hdrs)
+        dig = _digest(src, _deps(src))
         objs.append(obj)
         if force or not os.path.exists(obj) or not os.path.exists(stamp) or open(stamp).read() != dig:
             todo.append((src, obj, stamp, dig))

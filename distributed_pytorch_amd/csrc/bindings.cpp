@@ -34,8 +34,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val,
-               const void* g2, const unsigned char* mask, unsigned* tick);
-long dpa_bn_tick_words(int M, int C);
+               const void* g2, const unsigned char* mask);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -45,16 +44,6 @@ int dpa_gap_bwd(const float* dfeat, void* dx, int N, int HW, int C, int xbf, hip
 long dpa_conv0_part_floats(int N);
 int dpa_gemm_f32(const float* A, int lda, int ak, const float* B, int ldb, int bk, float* C, int M, int N, int K,
                  const float* bias, float* slab, int splits, hipStream_t st);
-int dpa_conv0_stats(const float* x, const float* w, int CP, float* part, int N, const float* gamma, const float* beta,
-                    const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
-                    float* scale, float* shift, float momentum, float eps, hipStream_t st);
-int dpa_conv0_bn_pool(const float* x, const float* w, int CP, const float* scale, const float* shift, float* a,
-                      unsigned short* a3, int np, long ps, int N, hipStream_t st);
-long dpa_bn_bwd_l0_part_floats(int N);
-int dpa_bn_bwd_l0(const float* gsrc, int nsplit, long slab, const float* x, const float* w, int CP,
-                  const float* scale, const float* shift, const float* mean, const float* invstd, const float* gamma,
-                  float* wpart, float* dgamma, float* dbeta, float* dbias, float* dw, int N, hipStream_t st, int* sig,
-                  int sig_val);
 int dpa_conv0_fwd(const float* x, const float* w, int CP, float* z, float* part, int N, const float* gamma,
                   const float* beta, const float* bias, float* rmean, float* rvar, long long* nbt, float* mean,
                   float* invstd, float* scale, float* shift, float momentum, float eps, hipStream_t st);
@@ -73,20 +62,13 @@ int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
                       int reduce, int posmajor, int np, int obf, hipStream_t st, float* stats);
 int dpa_conv_stats_rows(int tile);
-int dpa_conv_x3_dgrad_bnin(const float* gin, const float* zin, int pool, const float* bsc, const float* bsh,
-                           const float* coef, unsigned short* dz3w, long dz3ps, const unsigned short* w, long wps,
-                           void* dx, float* slab, int N, int H, int W, int K, int C, int splits, int tile, int np,
-                           hipStream_t st, int* sig, int sig_val);
 long dpa_ipc_slice(long n, int world);
-int dpa_conv_x3_fprop_bnin(const float* zin, int pool, const float* bsc, const float* bsh, unsigned short* a3w,
-                           long a3ps, const unsigned short* w, long wps, void* out, float* slab, int N, int H, int W,
-                           int C, int Kout, int splits, int tile, int np, hipStream_t st, float* stats);
 int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const float* gamma, const float* beta,
                        const float* bias, float* rmean, float* rvar, long long* nbt, float* mean, float* invstd,
                        float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* dz, long dzps, float* dw, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
-                      int posmajor, int np, hipStream_t st, unsigned* fix, long nfix);
+                      int posmajor, int np, hipStream_t st);
 int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
 int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
@@ -95,15 +77,6 @@ int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short*
                       int sig_val);
 int dpa_wait_signal(const int* sig, int val, long long timeout_us, int* tmo, hipStream_t st);
 int dpa_bn_fused_geo(int Mo, int C, int pool, int bwd, int rmax, long* part_floats, long* cnt_words, int* blocks);
-int dpa_bn_cols_bwd(const float* gsrc, int nsplit, const float* z, int N, int H, int W, int C, int pool,
-                    const float* scale, const float* shift, const float* mean, const float* invstd,
-                    const float* gamma, float* dgamma, float* dbeta, float* dbias, float* dz, unsigned short* dz3,
-                    int np, long ps, int* sig, int sig_val, hipStream_t st);
-int dpa_bn_cols_ok(int units, int C, int pool);
-int dpa_bn_cols_fwd(const float* src, int nsplit, float* zw, int N, int H, int W, int C, int pool,
-                    const float* gamma, const float* beta, const float* bias, float* rmean, float* rvar,
-                    long long* nbt, float* mean, float* invstd, float* scale, float* shift, float* out,
-                    unsigned short* out3, int np, long ps, float momentum, float eps, hipStream_t st);
 int dpa_bn_fused_fwd(const float* src, int nsplit, float* zw, int N, int H, int W, int C, int pool, int rmax,
                      float* part, unsigned* cnt, const float* gamma, const float* beta, const float* bias,
                      float* rmean, float* rvar, long long* nbt, float* mean, float* invstd, float* scale,
@@ -383,130 +356,6 @@ void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, 
       "conv_x3_fprop");
 }
 
-// Forward conv with the previous layer's BatchNorm (+ReLU, +2x2 max-pool) applied on load: zin fp32
-// [N, H(*2), W(*2), C], scale/shift [C]; a3w (optional) receives the operand planes [NP,N,H,W,C];
-// w3 [NP,K,3,3,C]; out fp32 [N,H,W,K] (one split) or slabs (left unreduced).  Halo tiles 17 / 19.
-void conv_x3_fprop_bnin(Tensor zin, bool pool, Tensor scale, Tensor shift, OptT a3w, Tensor w3, Tensor out, OptT slab,
-                        int64_t splits, int64_t tile, OptT stats) {
-  need(zin, "zin");
-  need(scale, "scale");
-  need(shift, "shift");
-  need_planes(w3, "w3");
-  need(out, "out");
-  const int np = w3.size(0);
-  const int N = zin.size(0), C = zin.size(3);
-  const int H = pool ? zin.size(1) / 2 : zin.size(1), W = pool ? zin.size(2) / 2 : zin.size(2);
-  const int K = w3.size(1);
-  TORCH_CHECK(w3.size(2) == 3 && w3.size(3) == 3 && w3.size(4) == C, "conv_x3_fprop_bnin: weight shape");
-  TORCH_CHECK(scale.numel() == C && shift.numel() == C && C <= 512 && C % 32 == 0, "conv_x3_fprop_bnin: channels");
-  TORCH_CHECK(!pool || (zin.size(1) % 2 == 0 && zin.size(2) % 2 == 0), "conv_x3_fprop_bnin: odd pooled map");
-  TORCH_CHECK(out.size(0) == N && out.size(1) == H && out.size(2) == W && out.size(3) == K,
-              "conv_x3_fprop_bnin: out shape");
-  u16* a3p = nullptr;
-  long a3ps = 0;
-  if (a3w.has_value() && a3w->defined()) {
-    need_planes(*a3w, "a3w");
-    TORCH_CHECK(a3w->size(0) == np && a3w->size(1) == N && a3w->size(2) == H && a3w->size(3) == W &&
-                    a3w->size(4) == C,
-                "conv_x3_fprop_bnin: a3w shape");
-    a3p = up(*a3w);
-    a3ps = a3w->stride(0);
-  }
-  float* sl = nullptr;
-  const int eff = dpa_x3_splits(9 * C, (int)splits);
-  if (eff > 1) {
-    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_fprop_bnin: split-K needs a slab workspace");
-    need(*slab, "slab");
-    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * K, "conv_x3_fprop_bnin: slab too small");
-    sl = fp(*slab);
-  }
-  float* stp = nullptr;
-  if (stats.has_value() && stats->defined()) {
-    need(*stats, "stats");
-    const int rows = dpa_conv_stats_rows((int)tile);
-    TORCH_CHECK(rows > 0 && stats->numel() >= 2 * (int64_t)((N * H * W + rows - 1) / rows) * K,
-                "conv_x3_fprop_bnin: stats");
-    stp = fp(*stats);
-  }
-  chk(dpa_conv_x3_fprop_bnin(fp(zin), pool ? 1 : 0, fp(scale), fp(shift), a3p, a3ps, up(w3), w3.stride(0), fp(out), sl,
-                             N, H, W, C, K, (int)splits, (int)tile, np, cur_stream(), stp),
-      "conv_x3_fprop_bnin");
-}
-
-// Data gradient of a 3x3/s1/p1 conv with this layer's BatchNorm backward applied on load: g fp32
-// [N, H(/2), W(/2), K] (the summed dL/d(layer output)), z [N,H,W,K], scale/shift (forward) and coef
-// [3K] (bn_bwd statistics); dz3w (optional) receives dz's planes [3,N,H,W,K]; w3 [3,K,3,3,C];
-// dx fp32 [N,H,W,C] (one split) or slabs (left unreduced).  Halo tiles 17 / 19 / 20 / 21.
-void conv_x3_dgrad_bnin(Tensor g, Tensor z, bool pool, Tensor scale, Tensor shift, Tensor coef, OptT dz3w, Tensor w3,
-                        Tensor dx, OptT slab, int64_t splits, int64_t tile, OptT sig, int64_t sig_val) {
-  need(g, "g");
-  need(z, "z");
-  need(scale, "scale");
-  need(shift, "shift");
-  need(coef, "coef");
-  need_planes(w3, "w3");
-  need(dx, "dx");
-  const int np = w3.size(0);
-  const int N = z.size(0), H = z.size(1), W = z.size(2), K = z.size(3);
-  const int C = w3.size(4);
-  TORCH_CHECK(w3.size(1) == K && w3.size(2) == 3 && w3.size(3) == 3, "conv_x3_dgrad_bnin: weight shape");
-  TORCH_CHECK(g.numel() == (int64_t)N * H * W * K / (pool ? 4 : 1), "conv_x3_dgrad_bnin: g shape");
-  TORCH_CHECK(scale.numel() == K && shift.numel() == K && coef.numel() >= 3 * K && K <= 512 && K % 32 == 0,
-              "conv_x3_dgrad_bnin: channels");
-  TORCH_CHECK(dx.numel() == (int64_t)N * H * W * C, "conv_x3_dgrad_bnin: dx shape");
-  u16* dzp = nullptr;
-  long dzps = 0;
-  if (dz3w.has_value() && dz3w->defined()) {
-    need_planes(*dz3w, "dz3w");
-    TORCH_CHECK(dz3w->size(0) == np && dz3w->numel() == np * z.numel(), "conv_x3_dgrad_bnin: dz3w shape");
-    dzp = up(*dz3w);
-    dzps = dz3w->stride(0);
-  }
-  float* sl = nullptr;
-  const int eff = dpa_x3_splits(9 * K, (int)splits);
-  if (eff > 1) {
-    TORCH_CHECK(slab.has_value() && slab->defined(), "conv_x3_dgrad_bnin: split-K needs a slab workspace");
-    need(*slab, "slab");
-    TORCH_CHECK(slab->numel() >= (int64_t)eff * N * H * W * C, "conv_x3_dgrad_bnin: slab too small");
-    sl = fp(*slab);
-  }
-  chk(dpa_conv_x3_dgrad_bnin(fp(g), fp(z), pool ? 1 : 0, fp(scale), fp(shift), fp(coef), dzp, dzps, up(w3),
-                             w3.stride(0), fp(dx), sl, N, H, W, K, C, (int)splits, (int)tile, np, cur_stream(),
-                             opt_signal(sig, "conv_x3_dgrad_bnin"), (int)sig_val),
-      "conv_x3_dgrad_bnin");
-}
-
-// BN backward statistics only (reduce + finalize: dgamma, dbeta, dbias, coef); dz is formed on load
-// by the data-gradient conv (conv_x3_dgrad_bnin).  fp32, ReLU activation.
-// tick (optional): int32 counter words, zeroed once, for the backward reduce's ticketed finalize
-// (bn.hip TICK: no separate finalize launch); they re-arm themselves after every launch
-unsigned* tick_ptr(const OptT& tick, int Mo, int C, const char* what) {
-  if (!tick.has_value() || !tick->defined()) return nullptr;
-  TORCH_CHECK(tick->is_cuda() && tick->is_contiguous() && tick->scalar_type() == torch::kInt32 &&
-                  tick->numel() >= dpa_bn_tick_words(Mo, C),
-              what, ": tick must be a contiguous int32 CUDA tensor of bn_tick_words(M, C) zeroed words");
-  return reinterpret_cast<unsigned*>(tick->data_ptr<int32_t>());
-}
-
-void bn_bwd_stats(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean,
-                  Tensor invstd, Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias,
-                  bool pool, OptT sig, int64_t sig_val, OptT tick) {
-  need(gsrc, "gsrc");
-  need(g, "g");
-  need(z, "z");
-  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
-  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
-  TORCH_CHECK(g.numel() == (int64_t)Mo * C, "bn_bwd_stats: g shape");
-  TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_bwd_stats: gsrc too small");
-  TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd_stats: part too small");
-  TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd_stats: coef too small");
-  chk(dpa_bn_bwd(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part),
-                 fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), nullptr, nullptr, 0, N, H, W, C, pool ? 1 : 0, 0, nullptr,
-                 nullptr, 0, cur_stream(), opt_signal(sig, "bn_bwd_stats"), (int)sig_val, nullptr, nullptr,
-                 tick_ptr(tick, Mo, C, "bn_bwd_stats")),
-      "bn_bwd_stats");
-}
-
 // BN finalize from channel-major (mean, M2) partials [C][nblk] of row blocks of rpb rows (a conv
 // epilogue's statistics)
 void bn_finalize(Tensor part, int64_t nblk, int64_t rpb, int64_t M, Tensor gamma, Tensor beta, OptT bias, OptT rmean,
@@ -528,7 +377,7 @@ void bn_finalize(Tensor part, int64_t nblk, int64_t rpb, int64_t M, Tensor gamma
 
 // x3 [NP,N,H,W,C], dz3 [NP,N,P,Q,K], dw [K,R,S,C] fp32
 void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, int64_t posmajor, OptT fix) {
+                   int64_t tile, int64_t posmajor) {
   need_planes(x3, "x3");
   need_planes(dz3, "dz3");
   need(dw, "dw");
@@ -547,16 +396,8 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
     TORCH_CHECK(slab->numel() >= (int64_t)eff * K * R * S * C, "conv_x3_wgrad: slab too small");
     sl = fp(*slab);
   }
-  unsigned* fx = nullptr;  // optional per-tile split-K counters (int32, zeroed once): in-kernel fix-up
-  long nfx = 0;
-  if (fix.has_value() && fix->defined()) {
-    TORCH_CHECK(fix->is_cuda() && fix->scalar_type() == torch::kInt32 && fix->is_contiguous(),
-                "conv_x3_wgrad: fix must be a contiguous int32 device tensor");
-    fx = reinterpret_cast<unsigned*>(fix->data_ptr<int32_t>());
-    nfx = fix->numel();
-  }
   chk(dpa_conv_x3_wgrad(up(x3), x3.stride(0), up(dz3), dz3.stride(0), fp(dw), sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream(), fx, nfx),
+                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream()),
       "conv_x3_wgrad");
 }
 
@@ -780,73 +621,6 @@ void conv0_fwd(Tensor x, Tensor w, Tensor z, OptT part, OptT gamma, OptT beta, O
       "conv0_fwd");
 }
 
-// ---- layer 0 without a stored z (first_layer.hip): statistics pass, recomputing apply, one-pass
-// backward from (g, x) ----
-void conv0_check(const Tensor& x, const Tensor& w, const char* what) {
-  need(x, "x");
-  need(w, "w");
-  TORCH_CHECK(x.dim() == 4 && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4, what, ": x [N,32,32,4]");
-  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) >= 3,
-              what, ": w [64,3,3,CP]");
-}
-
-void conv0_stats(Tensor x, Tensor w, Tensor part, Tensor gamma, Tensor beta, OptT bias, OptT rmean, OptT rvar,
-                 OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, double momentum, double eps) {
-  conv0_check(x, w, "conv0_stats");
-  const int N = x.size(0);
-  need(part, "part");
-  TORCH_CHECK(part.numel() >= dpa_conv0_part_floats(N), "conv0_stats: part too small");
-  for (const Tensor* o : {&gamma, &beta, &mean, &invstd, &scale, &shift})
-    TORCH_CHECK(o->numel() == 64, "conv0_stats: channel vectors [64]");
-  long long* nb = nbt.has_value() && nbt->defined() ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr;
-  chk(dpa_conv0_stats(fp(x), fp(w), (int)w.size(3), fp(part), N, fp(gamma), fp(beta), ofp(bias), ofp(rmean),
-                      ofp(rvar), nb, fp(mean), fp(invstd), fp(scale), fp(shift), (float)momentum, (float)eps,
-                      cur_stream()),
-      "conv0_stats");
-}
-
-// out: fp32 [N,16,16,64] or bf16 planes [NP,N,16,16,64]
-void conv0_bn_pool(Tensor x, Tensor w, Tensor scale, Tensor shift, Tensor out) {
-  conv0_check(x, w, "conv0_bn_pool");
-  const int N = x.size(0);
-  const int64_t n = (int64_t)N * 16 * 16 * 64;
-  TORCH_CHECK(scale.numel() == 64 && shift.numel() == 64, "conv0_bn_pool: scale/shift [64]");
-  if (out.scalar_type() == at::kBFloat16) {
-    int np = 1;
-    if (out.numel() != n) {
-      need_planes(out, "out");
-      TORCH_CHECK(out.numel() == out.size(0) * n, "conv0_bn_pool: planes shape");
-      np = out.size(0);
-    }
-    chk(dpa_conv0_bn_pool(fp(x), fp(w), (int)w.size(3), fp(scale), fp(shift), nullptr, up(out), np, n, N,
-                          cur_stream()),
-        "conv0_bn_pool");
-  } else {
-    need(out, "out");
-    TORCH_CHECK(out.numel() == n, "conv0_bn_pool: out [N,16,16,64]");
-    chk(dpa_conv0_bn_pool(fp(x), fp(w), (int)w.size(3), fp(scale), fp(shift), fp(out), nullptr, 0, 0, N,
-                          cur_stream()),
-        "conv0_bn_pool");
-  }
-}
-
-void bn_bwd_l0(Tensor gsrc, int64_t nsplit, Tensor x, Tensor w, Tensor scale, Tensor shift, Tensor mean,
-               Tensor invstd, Tensor gamma, Tensor wpart, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dw, OptT sig,
-               int64_t sig_val) {
-  conv0_check(x, w, "bn_bwd_l0");
-  for (auto* t : {&gsrc, &scale, &shift, &mean, &invstd, &gamma, &wpart, &dgamma, &dbeta, &dw})
-    need(*t, "bn_bwd_l0 operand");
-  const int N = x.size(0);
-  const int64_t gn = (int64_t)N * 16 * 16 * 64;
-  TORCH_CHECK(gsrc.numel() >= nsplit * gn, "bn_bwd_l0: gsrc too small");
-  TORCH_CHECK(wpart.numel() >= dpa_bn_bwd_l0_part_floats(N), "bn_bwd_l0: wpart too small");
-  TORCH_CHECK(dw.numel() == 64 * 9 * w.size(3) && dw.size(-1) == w.size(3), "bn_bwd_l0: dw like w");
-  chk(dpa_bn_bwd_l0(fp(gsrc), (int)nsplit, gn, fp(x), fp(w), (int)w.size(3), fp(scale), fp(shift), fp(mean),
-                    fp(invstd), fp(gamma), fp(wpart), fp(dgamma), fp(dbeta), ofp(dbias), fp(dw), N, cur_stream(),
-                    opt_signal(sig, "bn_bwd_l0"), (int)sig_val),
-      "bn_bwd_l0");
-}
-
 // C = opA(A) @ opB(B) (+ bias), fp32 on the fp32 matrix cores (gemm_f32.hip).  opA(A) = A [M,K] or,
 // trans_a, A^T of A [K,M]; opB(B) = B [K,N] or, trans_b, B^T of B [N,K].  splits > 1: split-K
 // through slab (>= splits * M * N floats), fixed-order reduction.
@@ -924,7 +698,7 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask, OptT tick) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
@@ -974,8 +748,7 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   }
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp,
-                 tick_ptr(tick, Mo, C, "bn_bwd")),
+                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp),
       "bn_bwd");
 }
 
@@ -1047,47 +820,7 @@ void bn_fused_fwd(Tensor src, int64_t nsplit, Tensor z, bool pool, int64_t rmax,
       "bn_fused_fwd");
 }
 
-// Column-block forward BN (bn_cols.hip): one launch, no cross-block hand-off, for small layers.
-bool bn_cols_ok(int64_t units, int64_t C, bool pool) { return dpa_bn_cols_ok((int)units, (int)C, pool ? 1 : 0) != 0; }
 
-void bn_cols_fwd(Tensor src, int64_t nsplit, Tensor z, bool pool, Tensor gamma, Tensor beta, OptT bias, OptT rmean,
-                 OptT rvar, OptT nbt, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, OptT out,
-                 double momentum, double eps) {
-  need(src, "src");
-  need(z, "z");
-  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
-  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
-  TORCH_CHECK(dpa_bn_cols_ok(Mo, C, pool ? 1 : 0), "bn_cols_fwd: layer too large for the column-block BN");
-  TORCH_CHECK(src.numel() >= nsplit * z.numel(), "bn_cols_fwd: src too small");
-  TORCH_CHECK(nsplit == 1 || src.data_ptr() != z.data_ptr(), "bn_cols_fwd: slabs and z must differ");
-  long long* nb_p = nullptr;
-  if (nbt.has_value() && nbt->defined()) {
-    need(*nbt, "nbt", at::kLong);
-    nb_p = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
-  }
-  const OutPtrs o = out_ptrs(out, (int64_t)Mo * C, "bn_cols_fwd");
-  chk(dpa_bn_cols_fwd(fp(src), (int)nsplit, fp(z), N, H, W, C, pool ? 1 : 0, fp(gamma), fp(beta), ofp(bias),
-                      ofp(rmean), ofp(rvar), nb_p, fp(mean), fp(invstd), fp(scale), fp(shift), o.f, o.b, o.np, o.ps,
-                      (float)momentum, (float)eps, cur_stream()),
-      "bn_cols_fwd");
-}
-
-void bn_cols_bwd(Tensor gsrc, int64_t nsplit, Tensor z, bool pool, Tensor scale, Tensor shift, Tensor mean,
-                 Tensor invstd, Tensor gamma, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, OptT sig,
-                 int64_t sig_val) {
-  need(gsrc, "gsrc");
-  need(z, "z");
-  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
-  const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
-  TORCH_CHECK(dpa_bn_cols_ok(Mo, C, pool ? 1 : 0), "bn_cols_bwd: layer too large for the column-block BN");
-  TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_cols_bwd: gsrc too small");
-  const OutPtrs o = out_ptrs(dz, z.numel(), "bn_cols_bwd");
-  TORCH_CHECK(o.f || o.b, "bn_cols_bwd: dz required");
-  chk(dpa_bn_cols_bwd(fp(gsrc), (int)nsplit, fp(z), N, H, W, C, pool ? 1 : 0, fp(scale), fp(shift), fp(mean),
-                      fp(invstd), fp(gamma), fp(dgamma), fp(dbeta), ofp(dbias), o.f, o.b, o.np, o.ps,
-                      opt_signal(sig, "bn_cols_bwd"), (int)sig_val, cur_stream()),
-      "bn_cols_bwd");
-}
 
 void bn_fused_bwd(Tensor gsrc, int64_t nsplit, Tensor z, bool pool, int64_t rmax, Tensor part, Tensor cnt,
                   Tensor scale, Tensor shift, Tensor mean, Tensor invstd, Tensor gamma, Tensor dgamma, Tensor dbeta,
@@ -1319,26 +1052,63 @@ class PyRcclComm {
   dpa::RcclComm comm_;
 };
 
-// Peer-memory communicator (runtime/ipc_comm.cpp, kernels/ipc_allreduce.hip)
+// Peer-memory communicator (runtime/ipc_comm.cpp, kernels/ipc_coll.hip).  Tensors of any dtype
+// move as 4-byte words; reductions read them as fp32 (parallel/ipc.py checks the dtype).
+static int64_t ipc_words(const Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "ipc: contiguous GPU tensor expected");
+  TORCH_CHECK(t.nbytes() % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 4 == 0,
+              "ipc: tensor must be a whole number of 4-byte words");
+  return (int64_t)(t.nbytes() / 4);
+}
+
 class PyIpcComm {
  public:
-  PyIpcComm(int rank, int world, int device, int64_t stage_floats) : c_(rank, world, device, (long)stage_floats) {}
+  PyIpcComm(int rank, int world, int device, int64_t stage_words, int64_t inbox_words)
+      : c_(rank, world, device, (long)stage_words, (long)inbox_words) {}
   py::bytes sig_handle() { return py::bytes(c_.sig_handle()); }
   py::bytes stage_handle() { return py::bytes(c_.stage_handle()); }
+  py::bytes inbox_handle() { return py::bytes(c_.inbox_handle()); }
   static py::bytes tensor_handle(const Tensor& t) {
     TORCH_CHECK(t.is_cuda(), "ipc: GPU tensor expected");
     return py::bytes(dpa::IpcComm::export_handle(t.data_ptr()));
   }
-  void set_peers(const std::vector<std::string>& sig, const std::vector<std::string>& stage) { c_.set_peers(sig, stage); }
+  void set_peers(const std::vector<std::string>& sig, const std::vector<std::string>& stage,
+                 const std::vector<std::string>& inbox) {
+    c_.set_peers(sig, stage, inbox);
+  }
   int add_region(const std::vector<std::string>& handles, Tensor local) {
-    TORCH_CHECK(local.is_cuda() && local.is_contiguous() && local.scalar_type() == at::kFloat,
-                "ipc: region must be a contiguous fp32 GPU tensor");
-    return c_.add_region(handles, local.data_ptr<float>(), (long)local.numel());
+    return c_.add_region(handles, local.data_ptr(), (long)ipc_words(local));
   }
-  void all_reduce(int id, int64_t off, int64_t n, int blocks, int64_t timeout_us) {
-    c_.all_reduce(id, (long)off, (long)n, blocks, (long long)timeout_us, cur_stream());
+  // rid < 0: the input is bounced through the inbox; off: the input's word offset in region rid
+  void all_reduce(int rid, int64_t off, Tensor t, int red, int blocks, int64_t tmo_us) {
+    c_.all_reduce(rid, (long)off, t.data_ptr(), (long)ipc_words(t), red, blocks, (long long)tmo_us, cur_stream());
   }
+  void broadcast(int rid, int64_t off, Tensor t, int root, int blocks, int64_t tmo_us) {
+    c_.broadcast(rid, (long)off, t.data_ptr(), (long)ipc_words(t), root, blocks, (long long)tmo_us, cur_stream());
+  }
+  void gather(int rid, int64_t off, Tensor send, c10::optional<Tensor> recv, int root, int blocks, int64_t tmo_us) {
+    const int64_t n = ipc_words(send);
+    void* out = nullptr;
+    if (recv.has_value()) {
+      TORCH_CHECK(ipc_words(*recv) >= n * c_.world(), "ipc gather: recv too small");
+      out = recv->data_ptr();
+    }
+    c_.gather(rid, (long)off, send.data_ptr(), out, (long)n, root, blocks, (long long)tmo_us, cur_stream());
+  }
+  void reduce_scatter(int rid, int64_t off, Tensor send, Tensor recv, int red, int blocks, int64_t tmo_us) {
+    const int64_t n = ipc_words(recv);
+    TORCH_CHECK(ipc_words(send) == n * c_.world(), "ipc reduce_scatter: send must be world x recv");
+    c_.reduce_scatter(rid, (long)off, send.data_ptr(), recv.data_ptr(), (long)n, red, blocks, (long long)tmo_us,
+                      cur_stream());
+  }
+  void all_gather(int rid, int64_t off, Tensor send, Tensor recv, int blocks, int64_t tmo_us) {
+    const int64_t n = ipc_words(send);
+    TORCH_CHECK(ipc_words(recv) == n * c_.world(), "ipc all_gather: recv must be world x send");
+    c_.all_gather(rid, (long)off, send.data_ptr(), recv.data_ptr(), (long)n, blocks, (long long)tmo_us, cur_stream());
+  }
+  void barrier(int blocks, int64_t tmo_us) { c_.barrier(blocks, (long long)tmo_us, cur_stream()); }
   bool take_timeout() { return c_.take_timeout(); }
+  int64_t launches() const { return (int64_t)c_.launches(); }
   int rank() const { return c_.rank(); }
   int world() const { return c_.world(); }
 
@@ -1364,24 +1134,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = false);
   m.def("wflip", &wflip);
   m.def("x3_splits", &x3_splits);
-  m.def("conv_x3_dgrad_bnin", &conv_x3_dgrad_bnin, py::arg("g"), py::arg("z"), py::arg("pool"), py::arg("scale"),
-        py::arg("shift"), py::arg("coef"), py::arg("dz3w"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
-        py::arg("splits"), py::arg("tile"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
-  m.def("bn_bwd_stats", &bn_bwd_stats, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
-        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
-        py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("pool"),
-        py::arg("sig") = py::none(), py::arg("sig_val") = 0, py::arg("tick") = py::none());
-  m.def("conv_x3_fprop_bnin", &conv_x3_fprop_bnin, py::arg("zin"), py::arg("pool"), py::arg("scale"),
-        py::arg("shift"), py::arg("a3w"), py::arg("w3"), py::arg("out"), py::arg("slab"), py::arg("splits"),
-        py::arg("tile"), py::arg("stats") = py::none());
   m.def("conv_x3_fprop", &conv_x3_fprop, py::arg("x3"), py::arg("w3"), py::arg("out"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
         py::arg("posmajor") = 0, py::arg("stats") = py::none());
   m.def("conv_stats_rows", [](int64_t tile) { return (int64_t)dpa_conv_stats_rows((int)tile); });
   m.def("bn_finalize", &bn_finalize);
   m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
-        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0,
-        py::arg("fix") = py::none());
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0);
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
         py::arg("posmajor") = 0, py::arg("add") = py::none(), py::arg("sig") = py::none(),
@@ -1401,19 +1160,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
-        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none(),
-        py::arg("tick") = py::none());
-  m.def("bn_tick_words", [](int64_t M, int64_t C) { return (int64_t)dpa_bn_tick_words((int)M, (int)C); });
+        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none());
   m.def("bn_fused_geo", &bn_fused_geo, py::arg("Mo"), py::arg("C"), py::arg("pool"), py::arg("bwd"),
         py::arg("rmax"));
-  m.def("bn_cols_ok", &bn_cols_ok, py::arg("units"), py::arg("C"), py::arg("pool"));
-  m.def("bn_cols_fwd", &bn_cols_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
-        py::arg("gamma"), py::arg("beta"), py::arg("bias"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"),
-        py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("out"), py::arg("momentum"),
-        py::arg("eps"));
-  m.def("bn_cols_bwd", &bn_cols_bwd, py::arg("gsrc"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
-        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
   m.def("bn_fused_fwd", &bn_fused_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
         py::arg("rmax"), py::arg("part"), py::arg("cnt"), py::arg("gamma"), py::arg("beta"), py::arg("bias"),
         py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("mean"), py::arg("invstd"), py::arg("scale"),
@@ -1441,15 +1190,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("scale") = py::none(),
         py::arg("shift") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5);
   m.def("conv0_part_floats", [](int64_t N) { return dpa_conv0_part_floats((int)N); });
-  m.def("conv0_stats", &conv0_stats, py::arg("x"), py::arg("w"), py::arg("part"), py::arg("gamma"), py::arg("beta"),
-        py::arg("bias"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("mean"), py::arg("invstd"),
-        py::arg("scale"), py::arg("shift"), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5);
-  m.def("conv0_bn_pool", &conv0_bn_pool, py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
-        py::arg("out"));
-  m.def("bn_bwd_l0", &bn_bwd_l0, py::arg("gsrc"), py::arg("nsplit"), py::arg("x"), py::arg("w"), py::arg("scale"),
-        py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("wpart"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("dbias"), py::arg("dw"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
-  m.def("bn_bwd_l0_part_floats", [](int64_t N) { return dpa_bn_bwd_l0_part_floats((int)N); });
   m.def("wgrad0_part_floats", [](int64_t N) { return dpa_wgrad0_part_floats((int)N); });
   m.def("fc_ce_train", &fc_ce_train, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("loss_row"),
         py::arg("dlogits"), py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("loss_out"), py::arg("loss_accum"),
@@ -1512,19 +1252,32 @@ PYBIND11_MODULE(_C, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("barrier", &dpa::TcpStoreClient::barrier, py::call_guard<py::gil_scoped_release>());
   py::class_<PyIpcComm>(m, "IpcComm")
-      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("stage_floats"))
+      .def(py::init<int, int, int, int64_t, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("stage_words"), py::arg("inbox_words"))
       .def("sig_handle", &PyIpcComm::sig_handle)
       .def("stage_handle", &PyIpcComm::stage_handle)
+      .def("inbox_handle", &PyIpcComm::inbox_handle)
       .def_static("tensor_handle", &PyIpcComm::tensor_handle)
       .def("set_peers", &PyIpcComm::set_peers)
       .def("add_region", &PyIpcComm::add_region)
-      .def("all_reduce", &PyIpcComm::all_reduce, py::arg("region"), py::arg("off"), py::arg("n"), py::arg("blocks"),
-           py::arg("timeout_us"))
+      .def("all_reduce", &PyIpcComm::all_reduce)
+      .def("broadcast", &PyIpcComm::broadcast)
+      .def("gather", &PyIpcComm::gather)
+      .def("reduce_scatter", &PyIpcComm::reduce_scatter)
+      .def("all_gather", &PyIpcComm::all_gather)
+      .def("barrier", &PyIpcComm::barrier)
       .def("take_timeout", &PyIpcComm::take_timeout, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("launches", &PyIpcComm::launches)
       .def_property_readonly("rank", &PyIpcComm::rank)
       .def_property_readonly("world", &PyIpcComm::world);
   m.def("ipc_slice", [](int64_t n, int world) { return (int64_t)dpa_ipc_slice((long)n, world); });
+  m.def("ipc_pieces", [](int op, int64_t n, int world, int64_t stage_words, int64_t inbox_words, bool registered) {
+    std::vector<std::pair<int64_t, int64_t>> out;
+    for (const auto& p : dpa::IpcComm::pieces(op, (long)n, world, (long)stage_words, (long)inbox_words, registered))
+      out.emplace_back(p.first, p.second);
+    return out;
+  }, py::arg("op"), py::arg("n"), py::arg("world"), py::arg("stage_words"), py::arg("inbox_words"),
+     py::arg("registered"));
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<int, int, py::bytes, int, bool, double, double, bool, bool, bool, int>(), py::arg("rank"),
            py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("high_priority") = false,

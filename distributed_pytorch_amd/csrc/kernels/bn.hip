@@ -27,6 +27,7 @@
 // backward reduce uses RTB (256) -thread blocks, ~512 of them (see RTB).
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -55,58 +56,18 @@ constexpr int RT = 1024;  // forward-statistics block size
 // * larger tensors (ResNet-50 at batch 128: 3.2M-25.7M lanes per BN; autograd runs them on one
 //   stream): 1024-thread blocks, ~256 of them — 512 x 256 left ResNet-50 at 7,035 img/s against
 //   7,485 (measured A/B, 2048 x 256: 7,454).
-// DPA_BN_BWD_BLOCK=256|1024 forces one geometry for every layer, DPA_BN_BWD_BLOCKS the small-block
-// grid size (A/B switches).
 constexpr int RTB = 256;
 constexpr int BWD_BLOCKS = 512;
-// Four bf16 rows' loads in flight per thread in the apply passes and the wide reduce (DPA_BN_UNROLL=0:
-// one / two rows, as before; A/B: ResNet-50 +0.6 %).  Set once from the host before the first launch.
-__constant__ int g_bn_unr = 1;
-inline void bn_unroll_init() {
-  static const bool done = [] {
-    const char* e = std::getenv("DPA_BN_UNROLL");
-    const int v = (e && e[0] == '0') ? 0 : 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_bn_unr), &v, sizeof(int)) == hipSuccess;
-  }();
-  (void)done;
-}
+// Four bf16 rows' loads in flight per thread in the apply passes and the wide reduce (A/B:
+// ResNet-50 +0.6 % over one / two rows).
+constexpr bool g_bn_unr = true;
 constexpr long WIDE_MIN_F4 = 3L << 20;
-inline int bwd_force() {
-  static const int f = [] {
-    const char* e = std::getenv("DPA_BN_BWD_BLOCK");
-    return e ? std::atoi(e) : 0;
-  }();
-  return f;
-}
+constexpr int BWD_WIDE_BLOCKS = 256;
 // bf: bf16 tensors (the generic path, its 16-byte-lane reduce): the 1024-thread geometry at every
 // size (ResNet-50 A/B: 9,240 -> 9,330 img/s); fp32 (the VGG engine) by size as above.
-inline bool bwd_wide(long M, int C, bool bf = false) {
-  const int f = bwd_force();
-  if (f == 1024) return true;
-  if (f == 256) return false;
-  return bf || M * (long)(C >> 2) > WIDE_MIN_F4;
-}
-// channels per backward-finalize block: 8 (32 partial rows of each in flight) or 4 (64 rows;
-// DPA_BN_FIN_CPB=4).  Equal within noise in the step (158.5k vs 158.2k img/s), 8 is kept.
-inline int fin_cpb() {
-  static const int v = [] {
-    const char* e = std::getenv("DPA_BN_FIN_CPB");
-    return e ? std::atoi(e) : 8;
-  }();
-  return v;
-}
+inline bool bwd_wide(long M, int C, bool bf = false) { return bf || M * (long)(C >> 2) > WIDE_MIN_F4; }
 inline int bwd_rt(long M, int C, bool bf = false) { return bwd_wide(M, C, bf) ? RT : RTB; }
-inline int bwd_blocks(long M, int C, bool bf = false) {
-  static const int nb = [] {
-    const char* e = std::getenv("DPA_BN_BWD_BLOCKS");
-    return e ? std::atoi(e) : BWD_BLOCKS;
-  }();
-  static const int nw = [] {  // 1024-thread geometry (A/B: DPA_BN_BWD_WIDE_BLOCKS)
-    const char* e = std::getenv("DPA_BN_BWD_WIDE_BLOCKS");
-    return e ? std::atoi(e) : 256;
-  }();
-  return bwd_wide(M, C, bf) ? nw : nb;
-}
+inline int bwd_blocks(long M, int C, bool bf = false) { return bwd_wide(M, C, bf) ? BWD_WIDE_BLOCKS : BWD_BLOCKS; }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -145,7 +106,6 @@ __host__ inline int red_rows_per_block(int M, int C, int rt = RT, int blocks = 2
   return rpb < g.RPI ? g.RPI : rpb;
 }
 
-// (the fp32 rule sizes dpa_bn_part_floats: the bf16 geometry never needs more partial rows)
 inline int bwd_rows_per_block(int M, int C, bool bf = false) {
   return red_rows_per_block(M, C, bwd_rt(M, C, bf), bwd_blocks(M, C, bf));
 }
@@ -508,98 +468,8 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 // dyout (ACT 2, optional): the gradient through the add+ReLU, dy = relu'(u + r) * (g + g2), is
 // stored here (it is the residual's gradient dres); the apply pass then reads dy alone (ACT 1)
 // instead of g, g2 and the mask again.
-// Ticketed finalize (TICK): the reduce kernel finishes the statistics itself instead of a separate
-// bn_bwd_finalize launch, in bn_bwd_finalize_kernel<8>'s exact summation order (bitwise the same
-// coefficients).  Each block stores its partial row device-coherently (agent-scope stores, written
-// through the XCD's L2) and takes a ticket on the counter of its residue group (block % TG); the
-// group's last block sums the group's rows in ascending block order (the finalize's per-thread
-// strided sum) into a level-2 row and takes a ticket on the kernel's counter; the last of those
-// combines the TG group sums with the finalize's LDS tree order and writes dgamma, dbeta, dbias and the
-// apply coefficients.  No block waits for another (no residency assumption); counters re-arm
-// themselves (the next launch is stream-ordered behind this one).
-constexpr int TG = 32;  // = 256 / 8: bn_bwd_finalize_kernel<8>'s row groups
-struct FinArgs {
-  unsigned* tick;  // [1 + TG] zeroed words
-  float* part2;    // [TG][3][C]
-  const float* gamma;
-  float *dgamma, *dbeta, *dbias, *coef;
-  float Mfull;
-};
-__device__ __forceinline__ void st_agent(float* p, float v) {
-  __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st4_agent(float* p, float4 v) {
-  st_agent(p, v.x);
-  st_agent(p + 1, v.y);
-  st_agent(p + 2, v.z);
-  st_agent(p + 3, v.w);
-}
-// thread 0 takes a ticket on *ctr (n takers); true in every thread of the block that drew the last
-__device__ __forceinline__ bool last_ticket(unsigned* ctr, unsigned n, unsigned* flag) {
-  typedef __attribute__((address_space(1))) unsigned gu32;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's device-coherent stores are acked
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned v = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = v == n - 1;
-    if (last) {
-      __hip_atomic_store((gu32*)ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0u;
-}
-template <int NT>
-__device__ void ticket_finalize(const FinArgs& f, const float* part, int nblk, int C, const float* mean,
-                                const float* invstd, unsigned* flag) {
-  const int grp = blockIdx.x % TG, ng = nblk < TG ? nblk : TG;
-  if (!last_ticket(f.tick + 1 + grp, (unsigned)((nblk - 1 - grp) / TG + 1), flag)) return;
-  for (int q = threadIdx.x; q < 3 * C; q += NT) {  // level 1: rows grp, grp + TG, ... in order
-    float a = 0.f;
-    int k = grp;
-    for (; k + 7 * TG < nblk; k += 8 * TG) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(long)(k + u * TG) * 3 * C + q];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a += v[u];
-    }
-    for (; k < nblk; k += TG) a += part[(long)k * 3 * C + q];
-    st_agent(f.part2 + (long)grp * 3 * C + q, a);
-  }
-  if (!last_ticket(f.tick, (unsigned)ng, flag)) return;
-  for (int c = threadIdx.x; c < C; c += NT) {  // level 2: bn_bwd_finalize_kernel<8>'s LDS tree order
-    float r[3];
-#pragma unroll 1
-    for (int j = 0; j < 3; ++j) {  // one quantity at a time: 32 live values, not 96
-      float v[TG];
-#pragma unroll
-      for (int g = 0; g < TG; ++g) v[g] = g < ng ? f.part2[((long)g * 3 + j) * C + c] : 0.f;
-#pragma unroll
-      for (int h = TG / 2; h >= 1; h >>= 1)
-#pragma unroll
-        for (int g = 0; g < h; ++g) v[g] += v[g + h];
-      r[j] = v[0];
-    }
-    const float sdy = r[0], sdx = r[1], sx = r[2];
-    const float iv = invstd[c], gm = f.gamma[c];
-    const float k1 = gm * iv;
-    const float k2x = -k1 * sdx / f.Mfull;
-    const float k3 = -k1 * sdy / f.Mfull;
-    f.dgamma[c] = sdx;
-    f.dbeta[c] = sdy;
-    if (f.dbias) f.dbias[c] = k2x * sx;
-    f.coef[c] = k1;
-    f.coef[C + c] = k2x * iv;
-    f.coef[2 * C + c] = k3 - k2x * iv * mean[c];
-  }
-}
-
 // part layout: [block][3][C]
-template <bool POOL, int ACT, typename TZ, int RTB, bool TICK = false>
+template <bool POOL, int ACT, typename TZ, int RTB>
 __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict__ gsrc, TZ* __restrict__ gout,
                                                             int nsplit, const TZ* __restrict__ z,
                                                             const TZ* __restrict__ res,
@@ -611,7 +481,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             int rpb, int* sig, int sig_val,
                                                             const TZ* __restrict__ g2,
                                                             const unsigned char* __restrict__ mask,
-                                                            TZ* __restrict__ dyout, FinArgs fin = FinArgs{}) {
+                                                            TZ* __restrict__ dyout) {
   start_signal(sig, sig_val);
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
@@ -730,18 +600,9 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
       sh[0][t] = vals[q];
       __syncthreads();
       tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-      if (cval && lane_r == 0) {
-        if constexpr (TICK)
-          st4_agent(o + q * C, sh[0][t]);
-        else
-          *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
-      }
+      if (cval && lane_r == 0) *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
       __syncthreads();
     }
-  }
-  if constexpr (TICK) {
-    __shared__ unsigned flag;
-    ticket_finalize<RTB>(fin, part, gridDim.x, C, mean, invstd, &flag);
   }
 }
 
@@ -989,38 +850,31 @@ void bn_bwd_apply_launch(int act, int grid, hipStream_t st, const TZ* g, const T
 }
 
 // Backward statistics: reduce pass (summing split-K dgrad slabs of g into g when nsplit > 1) and
-// finalize (dgamma, dbeta, dbias, apply coefficients).
+// finalize (dgamma, dbeta, dbias, apply coefficients).  Returns a HIP error code.
 template <typename TZ>
-void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
-                  const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
-                  float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
-                  hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
-                  const unsigned char* mask = nullptr, TZ* dyout = nullptr, unsigned* tick = nullptr) {
+int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* scale, const float* shift,
+                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
+                 float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
+                 hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
+                 const unsigned char* mask = nullptr, TZ* dyout = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   constexpr bool bf = sizeof(TZ) == 2;
   const int rpb = bwd_rows_per_block(Mo, C, bf);
   int nblk = (Mo + rpb - 1) / rpb;
   const bool wide = bwd_wide(Mo, C, bf);
-  // ticketed finalize inside the reduce (256-thread geometry; part holds the level-2 rows after the
-  // block rows, dpa_bn_part_floats; its order is the 8-channel finalize's)
-  const bool ticked = tick != nullptr && !wide && fin_cpb() == 8;
-  FinArgs fin{};
-  if (ticked) fin = FinArgs{tick, part + (long)nblk * 3 * C, gamma, dgamma, dbeta, dbias, coef, (float)N * H * W};
-  int nw = 0;  // bf16 in the 1024-thread geometry: 16-byte lanes (bn_wide.hip)
+  int nw = 0;  // bf16 in the 1024-thread geometry: 16-byte lanes (bn_wide.hip); 0 = not applicable
   if constexpr (sizeof(TZ) == 2) {
-    if (wide && !pool && nsplit == 1)
+    if (wide && !pool && nsplit == 1) {
       nw = dpa_bn_bwd_reduce_wide(gsrc, g2, z, res, mask, dyout, scale, shift, mean, invstd, part, Mo, C, act, rpb,
                                   sig, sig_val, st);
+      if (nw < 0) return -nw;  // a failed launch (not "not applicable")
+    }
   }
 #define RED(P, A)                                                                                               \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
                                                             N, H, W, C, rpb, sig, sig_val, g2, mask, dyout);            \
-  else if (ticked)                                                                                                \
-    bn_bwd_reduce_kernel<P, A, TZ, RTB, true><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean,    \
-                                                                    invstd, part, N, H, W, C, rpb, sig, sig_val, g2, \
-                                                                    mask, dyout, fin);                               \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
                                                               part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout)
@@ -1036,15 +890,10 @@ void bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* s
     RED(false, 2);
   }
 #undef RED
-  if (ticked && nw <= 0) return;  // the reduce finalized
-  if (fin_cpb() == 8)
-    bn_bwd_finalize_kernel<8><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
-                                                          dgamma, dbeta, dbias, coef);
-  else
-    bn_bwd_finalize_kernel<4><<<cdiv(C, 4), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
-                                                          dgamma, dbeta, dbias, coef);
+  bn_bwd_finalize_kernel<8><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
+                                                        dbeta, dbias, coef);
+  return (int)hipGetLastError();
 }
-
 
 // ---- first layer: BN backward apply fused with the 3x3/s1/p1 weight gradient on the network input.
 // Layer 0 of VGG (model.py:18-25 with in_channels 3) has no data gradient, so its dz is read only by
@@ -1192,15 +1041,14 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                 const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2,
-                const unsigned char* mask, unsigned* tick) {
+                const unsigned char* mask) {
   if (nsplit < 1) nsplit = 1;
   // add+ReLU: the reduce pass stores dy (= dres) and the apply pass reads it alone as an identity
-  // activation (DPA_BN_DY_PASS=0: the apply re-reads g, g2 and the mask / residual)
-  const char* dy_env = std::getenv("DPA_BN_DY_PASS");  // read per call: tests switch it in-process
-  const bool dy_pass = !(dy_env && dy_env[0] == '0');
-  const bool dyp = dy_pass && act == 2 && nsplit == 1 && !pool && dres != nullptr;
-  bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, H, W,
-                   C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr, tick);
+  // activation (measured faster than re-reading g, g2 and the mask / residual)
+  const bool dyp = act == 2 && nsplit == 1 && !pool && dres != nullptr;
+  const int rc0 = bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta,
+                                   dbias, N, H, W, C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr);
+  if (rc0) return rc0;
   if (dyp) {
     act = 1;
     gsrc = dres;
@@ -1209,8 +1057,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
     res = nullptr;
     dres = nullptr;
   }
-  if (dz == nullptr && dz3 == nullptr) return (int)hipGetLastError();  // statistics only: dz is formed on load
-                                                                        // by its consumer (conv_x3.hip BNIN 3/4)
+  if (dz == nullptr && dz3 == nullptr) return -2;
   const int Mo = N * (pool ? (H / 2) * (W / 2) : H * W);
   const TZ* gg = nsplit > 1 ? g : gsrc;
   if constexpr (sizeof(TZ) == 2) {  // bf16 in, one bf16 plane out: 16-byte lanes (bn_wide.hip)
@@ -1241,18 +1088,16 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
 
 extern "C" {
 // floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (3 per ...)
+// (backward: rows of the fp32 or the bf16 geometry, whichever has more; the bf16 wide reduce of
+// bn_wide.hip uses the bf16 geometry's rows per block)
 long dpa_bn_part_floats(int M, int C, int bwd) {
-  const int rpb = bwd ? bwd_rows_per_block(M, C) : red_rows_per_block(M, C);
-  const long nblk = (M + rpb - 1) / rpb;
-  // backward: the block rows, then the ticketed finalize's level-2 rows (bn_bwd_reduce_kernel TICK)
-  return bwd ? (nblk + TG) * C * 3 : nblk * C * 2;
-}
-
-// counter words the ticketed backward finalize needs (zeroed once; they re-arm themselves)
-long dpa_bn_tick_words(int M, int C) {
-  (void)M;
-  (void)C;
-  return 1 + TG;
+  if (!bwd) {
+    const int rpb = red_rows_per_block(M, C);
+    return (long)((M + rpb - 1) / rpb) * C * 2;
+  }
+  const int r32 = bwd_rows_per_block(M, C, false), r16 = bwd_rows_per_block(M, C, true);
+  const long nblk = std::max((M + r32 - 1) / r32, (M + r16 - 1) / r16);
+  return nblk * C * 3;
 }
 
 // z [M][C] (or nsplit fp32 slabs of it in src; then z is written) -> partials -> finalize.
@@ -1297,7 +1142,6 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
 // 1 none, 2 relu(. + res).  zbf: z and res are bf16.
 int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
                  int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st, unsigned char* mask) {
-  bn_unroll_init();
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && !res)) return -2;
   if (mask && act != 2) return -2;
   if (zbf)
@@ -1315,8 +1159,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2,
-               const unsigned char* mask, unsigned* tick) {
-  bn_unroll_init();
+               const unsigned char* mask) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && ((!res && !mask) || !dres))) return -2;
   if (mask && act != 2) return -2;
   if (zbf && nsplit > 1) return -2;
@@ -1324,10 +1167,10 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask, tick);
+                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st, sig, sig_val, (const float*)g2, mask, tick);
+                            (float*)dres, st, sig, sig_val, (const float*)g2, mask);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.
@@ -1338,11 +1181,11 @@ int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, c
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
                       float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val) {
-  bn_unroll_init();
   if (nsplit < 1) nsplit = 1;
   if (CP < 3) return -2;
-  bn_bwd_stats<float>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, N, 32,
-                      32, 64, 1, 0, nullptr, st, sig, sig_val);
+  const int rc = bn_bwd_stats<float>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta,
+                                     dbias, N, 32, 32, 64, 1, 0, nullptr, st, sig, sig_val);
+  if (rc) return rc;
   const float* gg = nsplit > 1 ? g : gsrc;
   const int nblk = N * (16 / WB0_RPB);
   bn_bwd_wgrad0_kernel<<<nblk, 256, 0, st>>>(gg, z, scale, shift, coef, x, wpart);

@@ -134,21 +134,12 @@ __global__ __launch_bounds__(64 * G) void splitk_reduce_kernel(const float4* __r
   }
 }
 
-// DPA_SPLITK_BLOCKS (A/B): cap on the reduce grid (0 = one block per 64 float4 columns)
-inline long splitk_block_cap() {
-  static const long cap = [] {
-    const char* e = getenv("DPA_SPLITK_BLOCKS");
-    return e ? atol(e) : 0L;
-  }();
-  return cap;
-}
-
 // out: float4 (fp32) or ushort4 (bf16, round-to-nearest-even); add: optional addend of out's type
 template <typename TO>
 inline int launch_splitk_reduce_t(const float* slabs, TO* o4, long n4, int splits, hipStream_t st,
                                   const TO* add = nullptr) {
-  const long full = (n4 + 63) / 64, cap = splitk_block_cap();
-  const long blocks = cap > 0 && full > cap ? cap : full;
+  const long blocks = (n4 + 63) / 64;
+  const long full = blocks;
   const float4* in4 = reinterpret_cast<const float4*>(slabs);
   if (splits >= 16 && full < 4096)
     splitk_reduce_kernel<16, TO><<<blocks, 1024, 0, st>>>(in4, o4, n4, splits, add);

@@ -97,12 +97,6 @@ struct Args {
     int Ktot, S, r0, s0, padh, padw;
     FastDiv fd_S;
   } phase[4];
-  // WGRAD split-K fix-up in the kernel (optional): per-tile arrival counters (zeroed once,
-  // self-resetting) and the final dW.  The last split block of a tile to arrive sums the tile's
-  // slabs in split order into fout: no separate reduce launch (splitk_fixup below).
-  unsigned* fix;
-  float* fout;
-  int fix_wt;  // 1: slab stores are agent-scope (write-through) stores and the release fence is skipped
 };
 
 __device__ __forceinline__ void decode_row(const Args& a, unsigned m, unsigned& img, unsigned& oh, unsigned& ow) {
@@ -136,64 +130,6 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, long elem_off, 
 }
 
 enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
-
-// ---- split-K fix-up inside the weight-gradient kernel (ticketed, deterministic) ----
-// Every split block of a tile stores its fp32 slab as before, drains its stores, and one lane
-// releases them at agent scope and takes a ticket on the tile's counter (bn_fused.hip's hand-off).
-// The block that draws the last ticket re-arms the counter (the next launch is stream-ordered behind
-// this one), acquires, and sums the tile's slabs in split order 0..S-1 into fout: the same value
-// whichever block arrives last, so results are deterministic.  No block waits for another (no
-// residency assumption, no spin); the separate reduce launch and its re-read of every slab from a
-// cold kernel are gone.  flag: 4 bytes of the kernel's LDS (every wave is past its epilogue reads).
-// Slab stores of a fix-up launch: agent-scope (device-coherent) stores, written through the XCD's L2,
-// so the hand-off needs no agent-scope release fence (that fence writes back the whole L2 of the
-// XCD, dirty lines of every other kernel included, once per block).
-__device__ __forceinline__ void store4_agent(float* p, uint4 v) {
-  typedef __attribute__((address_space(1))) unsigned long long gu64;
-  const unsigned long long lo = v.x | ((unsigned long long)v.y << 32), hi = v.z | ((unsigned long long)v.w << 32);
-  __hip_atomic_store((gu64*)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gu64*)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int BM, int BN, int THREADS>
-__device__ __forceinline__ void splitk_fixup(const Args& a, int tile, int m0, int n0, unsigned* flag) {
-  typedef __attribute__((address_space(1))) unsigned gu32;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's device-coherent slab stores are acked
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (!a.fix_wt) {  // slabs stored through the L2 (plain stores): release them
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const unsigned t = __hip_atomic_fetch_add((gu32*)(a.fix + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = t == (unsigned)a.splits - 1;
-    if (last) {
-      __hip_atomic_store((gu32*)(a.fix + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (*flag == 0u) return;
-  constexpr int C4 = BN / 4;
-  for (int q = threadIdx.x; q < BM * C4; q += THREADS) {
-    const int r = q / C4, row = m0 + r, col = n0 + (q - r * C4) * 4;
-    if (row < a.Nout && col < a.Ktot) {
-      const long off = (long)row * a.Ktot + col;
-      float4 s = *reinterpret_cast<const float4*>(a.out + off);
-#pragma unroll 4
-      for (int k = 1; k < a.splits; ++k) {
-        const float4 v = *reinterpret_cast<const float4*>(a.out + k * a.slab + off);
-        s.x += v.x;
-        s.y += v.y;
-        s.z += v.z;
-        s.w += v.w;
-      }
-      *reinterpret_cast<float4*>(a.fout + off) = s;
-    }
-  }
-}
 
 // The plane products of one k-slice over a TM x TN register tile, product-major: the TM*TN
 // accumulators are independent, so back-to-back MFMAs never wait on each other's result (an
@@ -788,8 +724,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
           if (row < nrows && col < ncols) {
             if constexpr (OB)
               *reinterpret_cast<uint4*>(a.outb + mrow_of(row) * ldc + col) = v;
-            else if (WG && a.fix_wt)
-              store4_agent(out + mrow_of(row) * ldc + col, v);
             else
               *reinterpret_cast<uint4*>(out + mrow_of(row) * ldc + col) = v;
           }
@@ -811,18 +745,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
               const long mrow = mrow_of(row);
               if constexpr (OB)
                 a.outb[mrow * ldc + col] = bf16_rne(acc[i][j][r]);
-              else if (WG && a.fix_wt)
-                __hip_atomic_store((__attribute__((address_space(1))) float*)(out + mrow * ldc + col), acc[i][j][r],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               else
                 out[mrow * ldc + col] = acc[i][j][r];
             }
           }
         }
       }
-  }
-  if constexpr (WG && !OB) {
-    if (a.fix != nullptr) splitk_fixup<BM, BN, THREADS>(a, tile, m0, n0, reinterpret_cast<unsigned*>(lds));
   }
   if constexpr (MODE == XM_FPROP) {
     if (a.stats != nullptr)
@@ -1065,44 +993,13 @@ struct HArgs {
   int sig_val;
   float2* stats;            // FPROP, one split: per (row tile, output channel) BN (mean, M2)
   int sepi;                 // OB: stores staged through LDS (DPA_OB_EPI)
-  // FPROP with the previous layer's BatchNorm applied on load (BNIN > 0, consumer-side BN): the
-  // A operand is relu(zin * bsc + bsh) (BNIN 2: 2x2/s2 max-pooled; zin is [N, 2H, 2W, C]) split into
-  // planes in registers, instead of planes a bn_apply pass wrote.  a3w (optional): the block's own
-  // pixels' planes are also stored there [NP][M][C] (plane stride a3ps) -- the weight-gradient
-  // conv's operand -- by the blocks of column tile 0.
-  const float* zin;
-  unsigned zbytes;
-  const float* bsc;
-  const float* bsh;
-  u16* a3w;
-  long a3ps;
-  int bnin;  // host side: 1 = affine + ReLU, 2 = affine + ReLU + 2x2 max-pool; 3 / 4: DGRAD (below)
-  // DGRAD with this layer's BatchNorm backward applied on load (BNIN 3, or 4 with the 2x2 max-pool
-  // routing): the A operand dz = k1*dy + k2*z + k3 is formed from gin (dL/d(layer output) [N, H, W, C],
-  // or [N, H/2, W/2, C] pooled), zin and the coefficients, with dy routed through the ReLU mask (and
-  // the window's first max) recomputed from z with the forward bsc / bsh -- bn_bwd_apply's exact
-  // arithmetic; a3w receives dz's planes (the weight-gradient conv's operand).
-  const float* gin;
-  unsigned gbytes;
-  const float* bcoef;  // k1 [C], k2 [C], k3 [C]
-  int dbg;  // EXPERIMENT: bit 0 skip B stores, 1 skip B loads, 2 skip A stores, 3 skip A loads
 };
 
 // staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
 __host__ __device__ constexpr int halo_slots(int BM) { return BM + BM / 2 + 1; }
 
-constexpr int BNIN_CMAX = 512;  // largest input channel count of the BatchNorm-on-load convs
-
-__device__ __forceinline__ float4 bload_f4(__amdgpu_buffer_rsrc_t r, long elem_off, bool valid) {
-  const unsigned vo = valid ? (unsigned)(elem_off * 4) : OOB;
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vo, 0, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, bool OB, int BNIN = 0>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, bool OB>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs a) {
-  static_assert(BNIN == 0 || (DG == (BNIN >= 3) && !OB), "BatchNorm on load: fp32 outputs; 1-2 forward, 3-4 dgrad");
-  constexpr bool BWD = BNIN >= 3, BPOOL = BNIN == 2 || BNIN == 4;
   start_signal(a.sig, a.sig_val);
   constexpr int THREADS = WAVES_M * WAVES_N * 64;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
@@ -1121,8 +1018,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   constexpr int NCA = (ACH + THREADS - 1) / THREADS;
   constexpr int NCB = (BCH + THREADS - 1) / THREADS;
   __shared__ __attribute__((aligned(16))) u16 lds[NP * A_PLANE + 2 * NP * B_PLANE];
-  // BNIN: per-channel scale, shift (and for the backward k1, k2, k3)
-  __shared__ __attribute__((aligned(16))) float bnc[BNIN >= 3 ? 5 : 2][BNIN ? BNIN_CMAX : 4];
   u16* const As = lds;
   u16* const Bs = lds + NP * A_PLANE;
   auto swz = [](int row) { return (row / RPB) & (CPR - 1); };
@@ -1136,17 +1031,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
     for (int p = 0; p < NP; ++p)
       *reinterpret_cast<uint4*>(lds + p * A_PLANE + ZS * BC + ((tid ^ ((ZS / RPB) & (CPR - 1))) << 3)) =
           make_uint4(0u, 0u, 0u, 0u);
-  }
-  if constexpr (BNIN != 0) {
-    for (int i = tid; i < a.C; i += THREADS) {
-      bnc[0][i] = a.bsc[i];
-      bnc[1][i] = a.bsh[i];
-      if constexpr (BWD) {
-        bnc[2][i] = a.bcoef[i];
-        bnc[3][i] = a.bcoef[a.C + i];
-        bnc[4][i] = a.bcoef[2 * a.C + i];
-      }
-    }
   }
   const int tile = xcd_remap(blockIdx.x, a.gm * a.gn);
   const int bm = tile / a.gn, bn = tile % a.gn;
@@ -1196,139 +1080,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
     for (int j = 0; j < NCA; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p) ra[j][p] = bload(rx[p], a_off[j] + c0, a_ok[j]);
-  };
-  // ---- BatchNorm on load (BNIN): the raw fp32 z of one staging slot group j (the 2x2 window of each
-  // slot pixel when pooled) is loaded at tap j of the previous chunk and converted to planes at tap
-  // j + 1 (one tap of latency; only one group's raw values live in registers), with the coefficients
-  // from LDS ----
-  constexpr int ZQ = BPOOL ? 4 : 1;
-  // raw register sets: one per slot group when a group's raw values are small (no pooling window),
-  // so a chunk's loads are all in flight from its first tap on; one set (group by group) otherwise
-  constexpr int NZB = 1;  // (one set per group measured: spills to scratch in the 256x128 tile)
-  float4 rz[NZB][ZQ][2], rg[NZB][BWD ? 2 : 1];
-  int z_off[BNIN ? NCA : 1];  // (fp32 z maps are < 2^31 elements: zbytes is a 32-bit range)
-  int g_off[BWD ? NCA : 1];
-  int z_u[BNIN == 4 ? NCA : 1];  // BNIN 4: the slot pixel's position in its pool window (scan order)
-  int zc0 = 0;
-  const int a_cc = tid % CPR;  // every staging chunk of this thread has the same 16-B piece (THREADS % CPR == 0)
-  const __amdgpu_buffer_rsrc_t rzr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.zin), (short)0, BNIN ? (int)a.zbytes : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rgr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.gin), (short)0, BWD ? (int)a.gbytes : 0, 0x00020000);
-  // z row of a window for the pooled modes: BNIN 2 reads the 2W-wide map under the conv input, BNIN 4
-  // the conv input itself (W wide)
-  const int zrow = (BNIN == 2 ? 2 * a.W : a.W) * a.C;
-  if constexpr (BNIN != 0) {
-    static_assert(THREADS % CPR == 0, "BNIN staging");
-#pragma unroll
-    for (int j = 0; j < NCA; ++j) {
-      const int q = tid + j * THREADS;
-      const int slot = q / CPR;
-      const int gp = m0 - a.W - 1 + slot;
-      const int g = gp < 0 ? 0 : gp;
-      const int img = g / HW, pix = g - img * HW, y = pix / a.W, x = pix - y * a.W;
-      int zp = gp;
-      if constexpr (BNIN == 2)  // pooled pixel (img, y, x) -> z pixel (img, 2y, 2x) of the 2H x 2W map
-        zp = (img * 2 * a.H + 2 * y) * 2 * a.W + 2 * x;
-      if constexpr (BNIN == 4) {  // the window of pixel (y, x): origin (y & ~1, x & ~1), g at (y/2, x/2)
-        zp = (img * a.H + (y & ~1)) * a.W + (x & ~1);
-        z_u[j] = (y & 1) * 2 + (x & 1);
-        g_off[j] = ((img * (a.H / 2) + (y >> 1)) * (a.W / 2) + (x >> 1)) * a.C + a_cc * 8;
-      }
-      if constexpr (BNIN == 3) g_off[j] = gp * a.C + a_cc * 8;
-      z_off[j] = zp * a.C + a_cc * 8;
-    }
-  }
-  auto load_zj = [&](int j, int c0) {
-    if constexpr (BNIN != 0) {
-      zc0 = c0;
-      const int b = j % NZB;
-#pragma unroll
-      for (int qq = 0; qq < ZQ; ++qq)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          rz[b][qq][h] = bload_f4(rzr, z_off[j] + (qq & 1) * a.C + (qq >> 1) * zrow + c0 + 4 * h, a_ok[j]);
-      if constexpr (BWD) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) rg[b][h] = bload_f4(rgr, g_off[j] + c0 + 4 * h, a_ok[j]);
-      }
-    }
-  };
-  // slot group j from rz -> ra[j] (bn_apply_kernel's exact arithmetic: relu(fma), the pool max in its
-  // order, then the plane split), and the planes of the block's own pixels to a3w (fresh: a new chunk)
-  auto convert = [&](int j, bool fresh) {
-    if constexpr (BNIN != 0) {
-      auto ar = [](float z, float sc, float sh) { return fmaxf(fmaf(z, sc, sh), 0.f); };
-      const float4 sc4[2] = {*reinterpret_cast<const float4*>(&bnc[0][zc0 + a_cc * 8]),
-                             *reinterpret_cast<const float4*>(&bnc[0][zc0 + a_cc * 8 + 4])};
-      const float4 sh4[2] = {*reinterpret_cast<const float4*>(&bnc[1][zc0 + a_cc * 8]),
-                             *reinterpret_cast<const float4*>(&bnc[1][zc0 + a_cc * 8 + 4])};
-      auto f4k = [](const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
-      float4 k14[2], k24[2], k34[2];
-      if constexpr (BWD) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          k14[h] = *reinterpret_cast<const float4*>(&bnc[BWD ? 2 : 0][zc0 + a_cc * 8 + 4 * h]);
-          k24[h] = *reinterpret_cast<const float4*>(&bnc[BWD ? 3 : 0][zc0 + a_cc * 8 + 4 * h]);
-          k34[h] = *reinterpret_cast<const float4*>(&bnc[BWD ? 4 : 0][zc0 + a_cc * 8 + 4 * h]);
-        }
-      }
-      u16 o[8][3];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int h = e >> 2, k = e & 3;
-        const float sc = k == 0 ? sc4[h].x : k == 1 ? sc4[h].y : k == 2 ? sc4[h].z : sc4[h].w;
-        const float sh = k == 0 ? sh4[h].x : k == 1 ? sh4[h].y : k == 2 ? sh4[h].z : sh4[h].w;
-        auto zq = [&](int qq) {
-          const float4& v = rz[j % NZB][qq][h];
-          return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-        };
-        float y;
-        if constexpr (BWD) {  // bn_bwd_apply_kernel: dy (route1 / the ReLU mask), then fma(k1, dy, fma(k2, z, k3))
-          const float gg = f4k(rg[j % NZB][h], k), k1 = f4k(k14[h], k), k2 = f4k(k24[h], k), k3 = f4k(k34[h], k);
-          float dy, zz;
-          if constexpr (BNIN == 4) {
-            const float y00 = fmaxf(fmaf(zq(0), sc, sh), 0.f), y01 = fmaxf(fmaf(zq(1), sc, sh), 0.f);
-            const float y10 = fmaxf(fmaf(zq(2), sc, sh), 0.f), y11 = fmaxf(fmaf(zq(3), sc, sh), 0.f);
-            int arg = 0;
-            float mx = y00;
-            if (y01 > mx) { mx = y01; arg = 1; }
-            if (y10 > mx) { mx = y10; arg = 2; }
-            if (y11 > mx) { mx = y11; arg = 3; }
-            const int u = z_u[j];
-            const float yu = u == 0 ? y00 : u == 1 ? y01 : u == 2 ? y10 : y11;
-            zz = u == 0 ? zq(0) : u == 1 ? zq(1) : u == 2 ? zq(2) : zq(3);
-            dy = (arg == u && yu > 0.f) ? gg : 0.f;
-          } else {
-            zz = zq(0);
-            dy = fmaf(zz, sc, sh) > 0.f ? gg : 0.f;
-          }
-          y = fmaf(k1, dy, fmaf(k2, zz, k3));
-        } else if constexpr (BNIN == 2) {
-          // max over the window of relu(fma(z, sc, sh)) == relu(fma(max z, sc, sh)) for sc >= 0 and
-          // relu(fma(min z, sc, sh)) for sc < 0, bit for bit: a correctly rounded fma is monotonic in z
-          const float zmx = fmaxf(fmaxf(zq(0), zq(1)), fmaxf(zq(2), zq(3)));
-          const float zmn = fminf(fminf(zq(0), zq(1)), fminf(zq(2), zq(3)));
-          y = ar(sc >= 0.f ? zmx : zmn, sc, sh);
-        } else {
-          y = ar(zq(0), sc, sh);
-        }
-        split_val<NP>(a_ok[j] ? y : 0.f, o[e]);
-      }
-#pragma unroll
-      for (int p = 0; p < NP; ++p)
-        ra[j][p] = make_uint4(o[0][p] | ((unsigned)o[1][p] << 16), o[2][p] | ((unsigned)o[3][p] << 16),
-                              o[4][p] | ((unsigned)o[5][p] << 16), o[6][p] | ((unsigned)o[7][p] << 16));
-      if (fresh && a.a3w != nullptr && bn == 0) {
-        const int slot = (tid + j * THREADS) / CPR;
-        const int gp = m0 - a.W - 1 + slot;
-        if (slot >= a.W + 1 && slot < a.W + 1 + BM && gp < a.M) {
-#pragma unroll
-          for (int p = 0; p < NP; ++p)
-            *reinterpret_cast<uint4*>(a.a3w + p * a.a3ps + (long)gp * a.C + zc0 + a_cc * 8) = ra[j][p];
-        }
-      }
-    }
   };
   auto store_a = [&]() {
 #pragma unroll
@@ -1440,61 +1191,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   const int nch = a.C / BC;
   const int cb = blockIdx.y * a.cps, ce = min(nch, cb + a.cps);
   const int nsteps = max(0, ce - cb) * 9;
-  if (BNIN != 0 && nsteps > 0) {
-    // Same steps and barriers as below with the 9 taps unrolled.  The next chunk's raw z (and g) is
-    // loaded after tap 0's MFMAs were issued (all slot groups at once when the raw values are small;
-    // otherwise group j after tap j's), and slot group j is converted after tap j + 1's MFMAs: the
-    // waits for those loads and the conversion's VALU work sit behind queued matrix work, in the same
-    // straight-line code as that tap.
-    static_assert(NCA < 9, "BNIN pipeline");
-    load_b(0, cb * BC);
-    __syncthreads();  // bnc
-    if constexpr (NZB == NCA) {
-#pragma unroll
-      for (int j = 0; j < NCA; ++j) load_zj(j, cb * BC);
-#pragma unroll
-      for (int j = 0; j < NCA; ++j) convert(j, true);
-    } else {
-#pragma unroll
-      for (int j = 0; j < NCA; ++j) {
-        load_zj(j, cb * BC);
-        convert(j, true);
-      }
-    }
-    store_a();
-    store_b(0);
-    if (nsteps > 1) load_b(1, cb * BC);
-    __syncthreads();
-    for (int ch = cb; ch < ce; ++ch) {
-      const int st0 = (ch - cb) * 9;
-      const bool nxt = ch + 1 < ce;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int st = st0 + tap;
-        compute(tap, st & 1);
-        if (tap >= 1 && tap <= NCA) convert(tap - 1, nxt);  // (no next chunk: unused, not stored)
-        if (nxt) {
-          if constexpr (NZB == NCA) {
-            if (tap == 0) {
-#pragma unroll
-              for (int j = 0; j < NCA; ++j) load_zj(j, (ch + 1) * BC);
-            }
-          } else if (tap < NCA) {
-            load_zj(tap, (ch + 1) * BC);
-          }
-        }
-        if (st + 1 < nsteps) {
-          store_b((st + 1) & 1);
-          if (st + 2 < nsteps) load_b(tap == 8 ? 1 : (tap == 7 ? 0 : tap + 2), (tap >= 7 ? ch + 1 : ch) * BC);
-          if (tap == 8) {
-            __syncthreads();
-            store_a();
-          }
-        }
-        __syncthreads();
-      }
-    }
-  } else if (nsteps > 0) {
+  if (nsteps > 0) {
     load_a(cb * BC);
     load_b(0, cb * BC);
     store_a();
@@ -1503,18 +1200,17 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
     if (cb + 1 < ce) load_a((cb + 1) * BC);
     __syncthreads();
     int tap = 0, ch = cb;
-    const int dbg = a.dbg;
     for (int st = 0; st < nsteps; ++st) {
       compute(tap, st & 1);
       const bool last_tap = tap == 8;
       const int tap1 = last_tap ? 0 : tap + 1, ch1 = last_tap ? ch + 1 : ch;  // step st + 1
       if (st + 1 < nsteps) {
-        if (!(dbg & 1)) store_b((st + 1) & 1);
-        if (st + 2 < nsteps && !(dbg & 2)) load_b(tap1 == 8 ? 0 : tap1 + 1, (tap1 == 8 ? ch1 + 1 : ch1) * BC);
+        store_b((st + 1) & 1);
+        if (st + 2 < nsteps) load_b(tap1 == 8 ? 0 : tap1 + 1, (tap1 == 8 ? ch1 + 1 : ch1) * BC);
         if (last_tap) {  // every wave is done with this chunk's image before it is replaced
           __syncthreads();
-          if (!(dbg & 4)) store_a();
-          if (ch + 2 < ce && !(dbg & 8)) load_a((ch + 2) * BC);
+          store_a();
+          if (ch + 2 < ce) load_a((ch + 2) * BC);
         }
       }
       __syncthreads();
@@ -2104,37 +1800,10 @@ __global__ __launch_bounds__(256) void pad_split_kernel(const float* __restrict_
   }
 }
 
-// DPA_WGRAD_BPC=b (b >= 1; read per call): a weight-gradient launch reserves unused dynamic LDS so
-// that at most b of its blocks share a CU.  The VGG engine runs these convs on its second stream
-// beside the critical path's BatchNorm passes; packed 3 blocks per CU (e.g. 148 VGPRs x 3 waves per
-// SIMD) they leave no registers for those passes' waves until conv blocks retire.
-int wgrad_bpc() {
-  const char* e = getenv("DPA_WGRAD_BPC");
-  return e ? atoi(e) : 0;
-}
-constexpr int LDS_PER_CU = 160 * 1024;
-
 template <int BM, int BN, int WM, int WN, int MODE, int NP, int BK, int NS, bool OB>
 int launch_x3(const Args& a, hipStream_t st) {
   dim3 grid(a.gm * a.gn, a.splits, a.nph > 1 ? a.nph : 1);
-  auto kern = conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS, OB>;
-  size_t dyn = 0;
-  if (MODE == XM_WGRAD) {
-    const int b = wgrad_bpc();
-    if (b > 0) {
-      static int stat = -1;  // this instantiation's static LDS bytes
-      if (stat < 0) {
-        hipFuncAttributes fa;
-        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) != hipSuccess) return 1;
-        stat = (int)fa.sharedSizeBytes;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_PER_CU - stat);
-      }
-      const int want = LDS_PER_CU / (b + 1) + 256 - stat;  // b + 1 blocks no longer fit
-      if (want > 0) dyn = (size_t)std::min(want, LDS_PER_CU - stat);
-    }
-  }
-  kern<<<grid, WM * WN * 64, dyn, st>>>(a);
+  conv_x3_kernel<BM, BN, WM, WN, MODE, NP, BK, NS, OB><<<grid, WM * WN * 64, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -2173,11 +1842,9 @@ int launch_any(const Args& a, int tile, int np, int obf, hipStream_t st) {
   if (obf) return launch_tile<MODE, 1, true>(a, tile, st);
   return np == 3 ? launch_tile<MODE, 3>(a, tile, st) : launch_tile<MODE, 1>(a, tile, st);
 }
-// bf16-output epilogue through LDS (conv_x3_kernel OB); DPA_OB_EPI=0: direct 2-byte stores (A/B)
-int ob_epi() {
-  const char* e = getenv("DPA_OB_EPI");
-  return (e && e[0] == '0') ? 0 : 1;
-}
+// epilogue stores staged through LDS as 16-byte row pieces (conv_x3_kernel / conv_halo_kernel): measured
+// faster than direct 2-/4-byte stores on every conv of the VGG and ResNet steps (docs/PERF_NOTES.md)
+constexpr int ob_epi() { return 1; }
 bool small_tile(int tile) { return tile == 1 || tile == 3 || tile == 6 || tile == 11 || tile == 15; }
 int tile_rows(int tile) { return small_tile(tile) ? 64 : ((tile == 7 || tile == 10 || tile == 14) ? 256 : 128); }
 int tile_cols(int tile) { return small_tile(tile) ? 64 : 128; }
@@ -2228,40 +1895,16 @@ int xsplits(int Kred, int splits) {
 //                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32,
 //                  20 = 256x64 / 32 (8 waves of 64x32), 21 = 128x64 / 32 (4 waves of 64x32) for
 //                  64-channel outputs (e.g. the data gradient into a 64-channel layer),
-//                  22 = 256x128 / 32 with 16 waves of 64x32, 23 = 128x128 / 32 with 8 waves of
-//                  64x32 (four / two waves per SIMD beside the one-block-per-CU LDS footprint)
 //   WGRAD:         16 = 64-pixel chunks, 17 = 32-pixel chunks
-bool is_halo(int tile) { return tile >= 16 && tile <= 23; }
-int halo_bm(int tile) { return (tile <= 17 || tile == 20 || tile == 22) ? 256 : 128; }
+bool is_halo(int tile) { return tile >= 16 && tile <= 21; }
+int halo_bm(int tile) { return (tile <= 17 || tile == 20) ? 256 : 128; }
 int halo_bn(int tile) { return tile == 20 || tile == 21 ? 64 : 128; }
-int halo_bc(int tile) { return (tile & 1) || tile == 20 || tile == 22 ? 32 : 16; }
+int halo_bc(int tile) { return (tile & 1) || tile == 20 ? 32 : 16; }
 
 template <int BM, int BN, int WM, int WN, bool DG, int NP, int BC, bool OB>
 int launch_halo(const HArgs& a, int splits, hipStream_t st) {
   dim3 grid(a.gm * a.gn, splits);
   conv_halo_kernel<BM, BN, WM, WN, DG, NP, BC, OB><<<grid, WM * WN * 64, 0, st>>>(a);
-  return (int)hipGetLastError();
-}
-
-// BatchNorm on load (fp32 output): the 32-channel-chunk tiles 17 / 19, and for the data gradient
-// also the 64-column tiles 20 / 21
-template <bool DG, int NP, int BNIN>
-int launch_halo_bnin(const HArgs& a, int tile, int splits, hipStream_t st) {
-  dim3 grid(a.gm * a.gn, splits);
-  if (tile == 17) {
-    conv_halo_kernel<256, 128, 4, 2, DG, NP, 32, false, BNIN><<<grid, 512, 0, st>>>(a);
-  } else if (tile == 19) {
-    conv_halo_kernel<128, 128, 2, 2, DG, NP, 32, false, BNIN><<<grid, 256, 0, st>>>(a);
-  } else if constexpr (DG) {
-    if (tile == 20)
-      conv_halo_kernel<256, 64, 4, 2, DG, NP, 32, false, BNIN><<<grid, 512, 0, st>>>(a);
-    else if (tile == 21)
-      conv_halo_kernel<128, 64, 2, 2, DG, NP, 32, false, BNIN><<<grid, 256, 0, st>>>(a);
-    else
-      return -6;
-  } else {
-    return -6;
-  }
   return (int)hipGetLastError();
 }
 
@@ -2273,17 +1916,11 @@ int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
     case 18: return launch_halo<128, 128, 2, 2, DG, NP, 16, OB>(a, splits, st);
     case 20: return launch_halo<256, 64, 4, 2, DG, NP, 32, OB>(a, splits, st);
     case 21: return launch_halo<128, 64, 2, 2, DG, NP, 32, OB>(a, splits, st);
-    case 22: return launch_halo<256, 128, 4, 4, DG, NP, 32, OB>(a, splits, st);
-    case 23: return launch_halo<128, 128, 2, 4, DG, NP, 32, OB>(a, splits, st);
     default: return launch_halo<128, 128, 2, 2, DG, NP, 32, OB>(a, splits, st);
   }
 }
 
 // -6: the conv does not fit the halo tile (channels, or rows wider than BM/4 - 1 pixels)
-inline int halo_dbg() {  // EXPERIMENT (staging cost bounds): DPA_HALO_DBG bit mask, read per call
-  const char* e = getenv("DPA_HALO_DBG");
-  return e ? atoi(e) : 0;
-}
 template <bool DG>
 int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st,
              const void* add = nullptr) {
@@ -2294,24 +1931,13 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
   a.gm = cdiv(a.M, BM);
   a.gn = cdiv(a.Nout, halo_bn(tile));
   a.sepi = ob_epi();
-  a.dbg = halo_dbg();
   a.cps = cdiv(a.C / BC, splits);
   a.out = splits > 1 ? slab : (float*)out;
   a.outb = (u16*)out;
   if (add && splits > 1 && !reduce) return -4;
   a.slab = splits > 1 ? (long)a.M * a.Nout : 0;
   int rc;
-  if (a.zin != nullptr) {  // BatchNorm on load (dpa_conv_x3_fprop_bnin / dpa_conv_x3_dgrad_bnin)
-    if (obf || DG != (a.bnin >= 3)) return -4;
-    if constexpr (DG) {
-      if (np != 3) return -4;  // (the x3 backward only)
-      rc = a.bnin == 4 ? launch_halo_bnin<true, 3, 4>(a, tile, splits, st) : launch_halo_bnin<true, 3, 3>(a, tile, splits, st);
-    } else if (a.bnin == 2) {
-      rc = np == 3 ? launch_halo_bnin<false, 3, 2>(a, tile, splits, st) : launch_halo_bnin<false, 1, 2>(a, tile, splits, st);
-    } else {
-      rc = np == 3 ? launch_halo_bnin<false, 3, 1>(a, tile, splits, st) : launch_halo_bnin<false, 1, 1>(a, tile, splits, st);
-    }
-  } else if (obf && splits == 1)
+  if (obf && splits == 1)
     rc = launch_halo_tile<DG, 1, true>(a, tile, splits, st);
   else if (np == 3)
     rc = launch_halo_tile<DG, 3, false>(a, tile, splits, st);
@@ -2386,14 +2012,10 @@ int run_stream(const u16* x, const u16* w, void* out, int M, int N, int K, int n
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::min(s.gm * s.gn, 2 * cus);
-  const char* ee = getenv("DPA_STREAM_EPI");  // A/B: 0 = direct 2-byte epilogue stores
-  const bool sepi = !(ee && ee[0] == '0');
   if (dgrad) {
-    if (sepi) gemm_stream_kernel<256, 128, 4, 2, 32, true><<<grid, 512, 0, st>>>(s);
-    else gemm_stream_kernel<256, 128, 4, 2, 32, true, false><<<grid, 512, 0, st>>>(s);
+    gemm_stream_kernel<256, 128, 4, 2, 32, true><<<grid, 512, 0, st>>>(s);
   } else {
-    if (sepi) gemm_stream_kernel<256, 128, 4, 2, 32, false><<<grid, 512, 0, st>>>(s);
-    else gemm_stream_kernel<256, 128, 4, 2, 32, false, false><<<grid, 512, 0, st>>>(s);
+    gemm_stream_kernel<256, 128, 4, 2, 32, false><<<grid, 512, 0, st>>>(s);
   }
   return (int)hipGetLastError();
 }
@@ -2579,80 +2201,6 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   return 0;
 }
 
-// Forward 3x3/s1/p1 conv whose input is the previous layer's BatchNorm output, applied on load
-// (consumer-side BN): x = relu(zin * bsc + bsh) per channel, 2x2/s2 max-pooled
-// when pool (zin [N, 2H, 2W, C] fp32, else [N, H, W, C]), split into np planes in the conv's operand
-// staging -- no bn_apply pass and no read of its planes.  a3w (optional, [np][N,H,W,C], plane stride
-// a3ps): the planes are also stored there (the weight-gradient conv reads them), bitwise those
-// bn_apply would write.  Halo tiles 17 / 19 only (-6 otherwise); out / slab / stats as
-// dpa_conv_x3_fprop (slabs left unreduced).
-int dpa_conv_x3_fprop_bnin(const float* zin, int pool, const float* bsc, const float* bsh, u16* a3w, long a3ps,
-                           const u16* w, long wps, void* out, float* slab, int N, int H, int W, int C, int Kout,
-                           int splits, int tile, int np, hipStream_t st, float* stats) {
-  if (tile != 17 && tile != 19) return -6;
-  const int sk = xsplits(9 * C, splits);
-  if (stats && sk > 1) return -7;
-  HArgs h{};
-  h.w = w;
-  h.wps = wps;
-  h.N = N;
-  h.H = H;
-  h.W = W;
-  h.C = C;
-  h.Nout = Kout;
-  h.stats = reinterpret_cast<float2*>(stats);
-  h.zin = zin;
-  h.bnin = pool ? 2 : 1;
-  h.bsc = bsc;
-  h.bsh = bsh;
-  h.a3w = a3w;
-  h.a3ps = a3ps;
-  const long zel = (long)N * H * W * C * (pool ? 4 : 1);
-  if (zel * 4 >= (1L << 31) || (long)Kout * 9 * C * 2 >= (1L << 31)) return -5;
-  h.zbytes = (unsigned)(zel * 4);
-  h.wbytes = (unsigned)((long)Kout * 9 * C * 2);
-  return run_halo<false>(h, tile, sk, np, 0, slab, out, 0, st);
-}
-
-// Data gradient of a 3x3/s1/p1 conv whose output's BatchNorm backward is applied on load (consumer-
-// side BN): dz = k1*dy + k2*z + k3 per channel (coef = [k1 | k2 | k3], C = K
-// channels each), dy = gin routed through the ReLU mask recomputed from z with the forward scale /
-// shift, and for pool through the 2x2 window's first max (gin [N, H/2, W/2, K], else [N, H, W, K]);
-// z [N, H, W, K] fp32.  dz3w (optional, [3][N,H,W,K], plane stride dz3ps) receives dz's planes,
-// bitwise those bn_bwd_apply would write.  x3 planes (np 3), halo tiles 17 / 19 / 20 / 21 (-6
-// otherwise); dx / slab as dpa_conv_x3_dgrad (slabs left unreduced).
-int dpa_conv_x3_dgrad_bnin(const float* gin, const float* zin, int pool, const float* bsc, const float* bsh,
-                           const float* coef, u16* dz3w, long dz3ps, const u16* w, long wps, void* dx, float* slab,
-                           int N, int H, int W, int K, int C, int splits, int tile, int np, hipStream_t st, int* sig,
-                           int sig_val) {
-  if (tile != 17 && tile != 19 && tile != 20 && tile != 21) return -6;
-  if (pool && (H % 2 || W % 2)) return -6;
-  HArgs h{};
-  h.sig = sig;
-  h.sig_val = sig_val;
-  h.w = w;
-  h.wps = wps;
-  h.N = N;
-  h.H = H;
-  h.W = W;
-  h.C = K;
-  h.Nout = C;
-  h.zin = zin;
-  h.gin = gin;
-  h.bnin = pool ? 4 : 3;
-  h.bsc = bsc;
-  h.bsh = bsh;
-  h.bcoef = coef;
-  h.a3w = dz3w;
-  h.a3ps = dz3ps;
-  const long zel = (long)N * H * W * K;
-  if (zel * 4 >= (1L << 31) || (long)K * 9 * C * 2 >= (1L << 31)) return -5;
-  h.zbytes = (unsigned)(zel * 4);
-  h.gbytes = (unsigned)(zel * 4 / (pool ? 4 : 1));
-  h.wbytes = (unsigned)((long)K * 9 * C * 2);
-  return run_halo<true>(h, tile, xsplits(9 * K, splits), np, 0, slab, dx, 0, st);
-}
-
 // Data gradient of conv(x [N,H,W,C], w [K,R,S,C], stride, pad) -> dZ [N,Hd,Wd,K]:
 // dx [N,H,W,C] fp32 (or slabs) from dz planes [NP][N,Hd,Wd,K] and the forward weight planes.
 // stride must be a power of two.
@@ -2779,7 +2327,7 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] Xcol[m][rsc]; x planes [NP][N,H,W,C], dz planes [NP][N,P,Q,Kout]
 int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* dw, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int posmajor, int np,
-                      hipStream_t st, unsigned* fix, long nfix) {
+                      hipStream_t st) {
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     WHArgs h{};
@@ -2811,16 +2359,9 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   a.out = a.splits > 1 ? slab : dw;
   a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
   a.sepi = ob_epi();
-  if (fix != nullptr && a.splits > 1) {  // slabs summed by each tile's last split block
-    if (nfix < (long)a.gm * a.gn) return -8;
-    a.fix = fix;
-    a.fout = dw;
-    const char* e = getenv("DPA_FIXUP_WT");  // A/B: 0 = plain slab stores + release fence
-    a.fix_wt = !(e && e[0] == '0');
-  }
   const int rc = np == 3 ? launch_tile<XM_WGRAD, 3>(a, tile, st) : launch_tile<XM_WGRAD, 1>(a, tile, st);
   if (rc) return rc;
-  if (a.splits > 1 && a.fix == nullptr) {
+  if (a.splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;
     return launch_splitk_reduce(slab, dw, n4, a.splits, st);
   }

@@ -34,14 +34,8 @@ int RcclComm::version() {
 namespace {
 // Fence / completion events only order streams of this device (and let the watchdog observe
 // completion), so they record with a device-scope release: a system-scope one writes back and
-// invalidates L2 under the compute kernels running beside the collective.  DPA_EVENT_SCOPE=torch
-// restores the default system scope for A/B runs.
-unsigned event_flags() {
-  const char* e = std::getenv("DPA_EVENT_SCOPE");
-  if (e && std::string(e) == "torch") return hipEventDisableTiming;
-  if (e && std::string(e) == "nofence") return hipEventDisableTiming | hipEventDisableSystemFence;
-  return hipEventDisableTiming | hipEventReleaseToDevice;
-}
+// invalidates L2 under the compute kernels running beside the collective.
+unsigned event_flags() { return hipEventDisableTiming | hipEventReleaseToDevice; }
 }  // namespace
 
 RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,

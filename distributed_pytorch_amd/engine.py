@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import json
 import os
-import weakref
 from collections import OrderedDict
 from typing import Callable, Dict, List, Optional
 
@@ -99,9 +98,8 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
 
 # Halo-staged 3x3/s1/p1 tiles of conv_x3.hip (ids after the 16 implicit-GEMM tiles): the block's
 # input pixels are staged once per channel chunk and the 9 taps read shifted views of them.
-HALO_TILES = (16, 17, 18, 19, 20, 21, 22, 23)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19, 22, 23)
-                                               # or 64 (20, 21) output channels, 16 or 32-channel
-                                               # chunks; 22 / 23: 17 / 19 with twice the waves
+HALO_TILES = (16, 17, 18, 19, 20, 21)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19) or 64 (20, 21)
+                                       # output channels, 16 or 32-channel chunks
 HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
 POS_TILES = (24, 25, 26, 27, 28, 29)  # fprop / dgrad of small images: position-major rows, padding taps
                                       # skipped (conv_x3.hip conv_pos_kernel)
@@ -116,7 +114,7 @@ def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
         return p is not None and cred % 8 == 0 and cout % 8 == 0 and p + 2 * w + 2 <= 2 * p + 3
     if tile not in HALO_TILES:
         return False
-    bm, bc = (256 if tile in (16, 17, 20, 22) else 128), (32 if tile & 1 or tile in (20, 22) else 16)
+    bm, bc = (256 if tile in (16, 17, 20) else 128), (32 if tile & 1 or tile == 20 else 16)
     return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= bm + bm // 2
 
 
@@ -203,7 +201,6 @@ class VGGEngine:
         self.stats = []  # per layer dict(mean, invstd, scale, shift)
         self.eval_ss = []
         part_need = 1
-        tick_need = 0
         for i, l in enumerate(L):
             hw, ho = l.hw, (l.hw // 2 if l.pool else l.hw)
             nxt_planes = i + 1 < len(L) and self.planes[i + 1]
@@ -223,7 +220,6 @@ class VGGEngine:
             M, Mo = N * hw * hw, N * ho * ho
             part_need = max(part_need, self.K.bn_part_floats(M, l.cout, False),
                             self.K.bn_part_floats(Mo, l.cout, True))
-            tick_need = max(tick_need, self.K.bn_tick_words(Mo, l.cout) if hasattr(self.K, "bn_tick_words") else 0)
         # Weight gradients run on a second HIP stream (DPA_WGRAD_STREAM=0: one stream): wgrad(i) needs
         # only dz(i) and the stored forward activation, so it runs beside dgrad(i) and the BN
         # backward of layer i-1, whose reduce/finalize kernels leave most CUs idle.  It has its own
@@ -253,18 +249,11 @@ class VGGEngine:
         # communicator), so it has its own short bound: a residency shortfall surfaces in seconds,
         # not after the communicator's timeout.
         self.bn_fused_timeout_us = int(os.environ.get("DPA_BN_FUSED_TIMEOUT_US", "2000000"))
-        # params_free hands the sync a later kernel's signal instead of recording an event (A/B: 0)
-        self.free_signal = os.environ.get("DPA_FREE_SIGNAL", "1") == "1"
-        self.head_side = self.ksignal and os.environ.get("DPA_HEAD_SIDE", "1") == "1"
+        # params_free hands the sync a later kernel's signal instead of recording an event
+        self.free_signal = True
+        self.head_side = self.ksignal
         self.slab = torch.empty(1, **f32)
         self.wslab = torch.empty(1, **f32) if self.wstream is not None else None
-        # split-K weight gradients with at most this many splits sum their slabs inside the conv
-        # kernel (conv_x3.hip splitk_fixup: per-tile tickets, one self-resetting counter array per
-        # stream) instead of a separate reduce launch; 0 = always the reduce kernel
-        self.wgrad_fixup_max = int(os.environ.get("DPA_WGRAD_FIXUP_MAX", "0")) if dev.type == "cuda" else 0
-        self.wfix_main = torch.zeros(4096, dtype=torch.int32, device=dev) if self.wgrad_fixup_max > 0 else None
-        self.wfix_side = (torch.zeros(4096, dtype=torch.int32, device=dev)
-                          if self.wgrad_fixup_max > 0 and self.wstream is not None else None)
         for i in range(len(L)):  # size the split-K workspaces for the full-batch plan
             for kind in ("fprop", "dgrad", "wgrad"):
                 if kind == "dgrad" and i == 0:
@@ -284,17 +273,6 @@ class VGGEngine:
                             and os.environ.get("DPA_FUSED_CONV0", "1") == "1"
                             and l0.hw == 32 and l0.cout == 64 and l0.cin <= 3)
         self.part0 = torch.empty(self.K.conv0_part_floats(N), **f32) if self.fused_conv0 else None
-        # Layer 0 without a stored z (DPA_L0_RECOMPUTE=1, needs both fused layer-0 paths): the
-        # 27-MAC conv is recomputed by each consumer instead of writing and re-reading 67 MB of z —
-        # a statistics pass, an apply pass writing the pooled planes (first_layer.hip
-        # conv0_bn_pool_kernel), and ONE backward pass over (g, x) that accumulates the BN sums and
-        # the coefficient-free parts of the weight gradient (bn_bwd_l0_kernel).
-        # Off by default: the recompute trades 67 MB of z traffic for VALU work, and measured slower
-        # (forward 43 vs 45 us, backward 112 vs 82 us beside the weight-gradient stream; 173.5k-174.3k
-        # vs 176.5k-177.0k img/s, docs/PERF_NOTES.md).  Kept as an option and tested.
-        self.l0_recompute = (self.fused_conv0 and self.fused_wgrad0 and hasattr(self.K, "bn_bwd_l0")
-                             and os.environ.get("DPA_L0_RECOMPUTE", "0") == "1")
-        self.l0part = torch.empty(self.K.bn_bwd_l0_part_floats(N), **f32) if self.l0_recompute else None
         # Head: the last layer's BN + ReLU + 2x2 max-pool folded into the classifier kernel's row load
         # (fc_ce.hip BnIn: one launch less on the critical path); DPA_FUSED_HEAD=0 runs bn_apply
         lL = L[-1]
@@ -309,15 +287,6 @@ class VGGEngine:
         # (layers 4-7 at batch 256), backward only for the 2x2 layers (<= 0.6M; beside the weight-
         # gradient convs the 4x4 layers' rendezvous waits for CUs and loses to the three kernels).
         self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", "2200000")) if dev.type == "cuda" else 0
-        # BN of those small layers as ONE column-block launch instead (bn_cols.hip: a block owns 4
-        # channels over all rows, no rendezvous between blocks; DPA_BN_COLS=1 forward,
-        # DPA_BN_COLS_BWD=1 backward).  Off: same box, 175.1k (bn_fused / three kernels) vs 160.1k
-        # (forward) vs 143.9k img/s (both) -- the 16-byte-per-row loads of a 4-channel column touch
-        # one cache line per lane, and C/4 blocks leave half the CUs idle (docs/PERF_NOTES.md).
-        self.bn_cols = (dev.type == "cuda" and hasattr(self.K, "bn_cols_fwd")
-                        and os.environ.get("DPA_BN_COLS", "0") == "1")
-        self.bn_cols_bwd = (dev.type == "cuda" and hasattr(self.K, "bn_cols_bwd")
-                            and os.environ.get("DPA_BN_COLS_BWD", "0") == "1")
         self.bn_fused_bwd_max = (int(os.environ.get("DPA_BN_FUSED_BWD_MAX", "600000"))
                                  if dev.type == "cuda" else 0)
         self.bn_fused_rmax = int(os.environ.get("DPA_BN_FUSED_RMAX", "64"))
@@ -343,46 +312,8 @@ class VGGEngine:
             if rows:
                 epart = max(epart, 2 * ((N * l.hw * l.hw + rows - 1) // rows) * l.cout)
         self.epart = torch.empty(max(epart, 1), **f32)
-        # Consumer-side BatchNorm, forward: a forward conv on a halo tile applies
-        # the previous layer's BN + ReLU (+ 2x2 max-pool) while it stages its operand from that layer's
-        # fp32 z (conv_x3.hip BNIN), so the bn_apply pass (or the one-launch BN's apply phase) and the
-        # read of its planes go; the conv also stores the planes for the weight-gradient conv.
-        # DPA_BN_ON_LOAD=0 keeps the apply passes (A/B).
-        self.bn_on_load = (dev.type == "cuda" and os.environ.get("DPA_BN_ON_LOAD", "0") == "1"
-                           and hasattr(self.K, "conv_x3_fprop_bnin"))
-        # ... and backward (item 1b): the data-gradient conv of layer i forms dz = k1*dy + k2*z + k3 on
-        # load from the summed g, z and the BN backward coefficients (conv_x3.hip BNIN 3/4) and stores
-        # dz's planes for the weight-gradient conv, which then waits for that conv to END (the next BN
-        # backward's start signal) instead of its start.  DPA_BN_BWD_ON_LOAD=0 keeps bn_bwd_apply.
-        self.bn_bwd_on_load = (dev.type == "cuda" and os.environ.get("DPA_BN_BWD_ON_LOAD", "0") == "1"
-                               and hasattr(self.K, "conv_x3_dgrad_bnin"))
-        # BN reduction workspace; zero-initialised once (its head holds self-resetting tickets)
+        # BN reduction workspace
         self.part = torch.zeros(part_need, **f32)
-        # Ticketed BN-backward finalize (bn.hip TICK, DPA_BN_TICK=1): the reduce kernel's last blocks
-        # finalize the statistics (bitwise the finalize kernel's result), so the main stream runs no
-        # separate finalize launch per layer.  Off by default: same-box A/B 176.0k (finalize launch)
-        # vs 170.5k img/s (ticketed) -- the serial two-level tail inside the reduce, behind
-        # device-coherent stores and an agent-scope acquire, outlasts the launch it saves
-        # (docs/PERF_NOTES.md, round 4).  Counter words zeroed once; they re-arm themselves.
-        self.bn_tick = (torch.zeros(max(tick_need, 1), device=dev, dtype=torch.int32)
-                        if dev.type == "cuda" and tick_need and os.environ.get("DPA_BN_TICK", "0") == "1" else None)
-        # Deferred optimizer step (``defer_update``, set by the caller, e.g. bench.py): the update of
-        # step k runs at the start of step k+1 on the weight-gradient stream -- idle during the forward
-        # -- instead of at the end of step k on the main stream.  Layer 0's slice still runs at once
-        # (its conv is the next kernel to read parameters); the main stream waits for layers 1-3 before
-        # conv 1 and for the rest (layers 4.., the classifier) before conv 4, long after they finished.
-        # Same kernels, same slices of the same element-wise update: results are bitwise those of the
-        # immediate step.  Measured slower (VGG-11 x3: 172.0k immediate vs 163.5k img/s deferred, same
-        # box): the update's 184 MB stream competes with the forward's BatchNorm passes and the two
-        # cross-stream waits sit on the main stream -- off unless the caller sets it.  Anything that reads the parameters or momenta from outside the step calls
-        # ``flush_update()`` first (state_dict, evaluation, loading, broadcast, the bench's timed region).
-        self.defer_update = False
-        self._pending_upd = None  # (grad_scale, first) of a deferred update not yet issued
-        self._upd_ev = [DevEvent(), DevEvent(), DevEvent()] if dev.type == "cuda" else None
-        self._upd_wait: Dict[int, DevEvent] = {}
-        los = [self.params.offsets[f"{l.conv_key}.weight"] for l in L]
-        nl = len(L)
-        self._upd_cut = (los[min(1, nl - 1)], los[min(4, nl - 1)], self.params.flat.numel())
         self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
         self.loss_row = torch.zeros(N, **f32)
         self.dlogits = torch.zeros(N, num_classes, **f32)
@@ -394,17 +325,10 @@ class VGGEngine:
         self.init_parameters(seed=None)
 
     def _make_wgrad_stream(self, dev: torch.device):
-        """The weight-gradient stream: a default-priority torch stream.  ``DPA_WGRAD_PRIO=low``
-        creates it at HIP's lowest priority instead (A/B only: no gain without a communicator,
-        and with the RCCL comm stream present the mixed queue priorities cost 28 % of the step,
-        docs/PERF_NOTES.md)."""
-        if os.environ.get("DPA_WGRAD_PRIO", "normal") != "low":
-            return torch.cuda.Stream(dev)
-        least, _greatest = self.K.stream_priority_range()
-        with torch.cuda.device(dev):
-            ptr = self.K.stream_create(least)
-        weakref.finalize(self, self.K.stream_destroy, ptr)
-        return torch.cuda.ExternalStream(ptr, device=dev)
+        """The weight-gradient stream: a default-priority torch stream (a lowest-priority one was
+        measured: no gain alone, and beside the RCCL comm stream the mixed queue priorities cost
+        28 % of the step, docs/PERF_NOTES.md)."""
+        return torch.cuda.Stream(dev)
 
     # ------------------------------------------------------------------ parameters / state
     @torch.no_grad()
@@ -421,7 +345,6 @@ class VGGEngine:
 
     @torch.no_grad()
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
-        self.flush_update()
         sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
         seen = set()
         for l in self.spec.convs:
@@ -450,14 +373,12 @@ class VGGEngine:
         """Re-split the parameter arena into the bf16 operand planes (one launch).  Needed after
         parameters change outside ``sgd_step`` (load, broadcast); the SGD kernel refreshes them
         itself."""
-        self.flush_update()
         if self.wplanes is not None:
             self.K.split_planes(self.params.flat, self.wplanes)
 
     @torch.no_grad()
     def state_dict(self, prefix: str = "") -> "OrderedDict[str, torch.Tensor]":
         """Reference-layout state_dict (58 keys for VGG-11, OIHW fp32, CPU tensors)."""
-        self.flush_update()
         out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         for i, l in enumerate(self.spec.convs):
             out[prefix + f"{l.conv_key}.weight"] = (
@@ -489,7 +410,6 @@ class VGGEngine:
     @torch.no_grad()
     def optimizer_state_dict(self) -> dict:
         """torch.optim.SGD-format state_dict (momentum buffers in OIHW)."""
-        self.flush_update()
         names = self.spec.param_names()
         state = {}
         if self.steps_taken > 0:
@@ -503,7 +423,6 @@ class VGGEngine:
 
     @torch.no_grad()
     def load_optimizer_state_dict(self, osd: dict):
-        self.flush_update()
         names = self.spec.param_names()
         pg = osd["param_groups"][0]
         self.lr, self.momentum, self.weight_decay = pg["lr"], pg["momentum"], pg["weight_decay"]
@@ -530,21 +449,6 @@ class VGGEngine:
             return None  # layer 0: conv0_fwd / bn_bwd_wgrad0 fuse its BN with the convolution instead
         ho = l.hw // 2 if l.pool else l.hw
         return self.K.bn_fused_geo(n * ho * ho, l.cout, l.pool, bwd, self.bn_fused_rmax)
-
-    def _cols(self, i: int, n: int, bwd: bool = False) -> bool:
-        """Layer i's BN as the column-block kernel (bn_cols.hip): layers up to the one-launch BN's
-        size bound whose register tile fits (DPA_BN_COLS=0 / DPA_BN_COLS_BWD=0: never)."""
-        key = ("cols", i, n, bwd)
-        v = self._fgeo.get(key)
-        if v is None:
-            l = self.spec.convs[i]
-            ho = l.hw // 2 if l.pool else l.hw
-            on = self.bn_cols_bwd if bwd else self.bn_cols
-            v = bool(on and i > 0 and 0 < n * l.hw * l.hw * l.cout <= self.bn_fused_max
-                     and self.K.bn_cols_ok(n * ho * ho, l.cout, l.pool)
-                     and not (bwd and self._bnin_bwd(i, n)))  # (BN on load forms dz in the dgrad instead)
-            self._fgeo[key] = v
-        return v
 
     def _fused(self, i: int, n: int, bwd: bool) -> bool:
         key = (i, n, bwd)
@@ -658,9 +562,6 @@ class VGGEngine:
                     ev1.record()
                     torch.cuda.synchronize(self.device)
                     ms = ev0.elapsed_time(ev1) / iters
-                    if verbose and os.environ.get("DPA_TUNE_VERBOSE_ALL") == "1":
-                        print("  cand", conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout), [tile, s, pm, round(ms, 5)],
-                              flush=True)
                     if best is None or ms < best[3]:
                         best = [tile, s, pm, ms]
                 self._cfg_cache[key] = tuple(best[:3])
@@ -688,51 +589,14 @@ class VGGEngine:
         tile, s, _ = self.conv_config(i, "fprop", n)
         return self.K.conv_stats_rows(tile) if s == 1 else 0
 
-    def _bnin(self, i: int, n: int) -> bool:
-        """Whether layer i's training forward conv applies layer i-1's BatchNorm on load (its input
-        planes are then written by that conv, not by a bn_apply pass)."""
-        key = ("bnin", i, n)
-        v = self._cfg_cache.get(key)
-        if v is None:
-            v = False
-            if self.bn_on_load and i > 0 and self.planes[i] and self.a3[i - 1] is not None:
-                lp = self.spec.convs[i - 1]
-                tile, _, _ = self.conv_config(i, "fprop", n)
-                v = (tile in (17, 19) and lp.cout % 32 == 0 and lp.cout <= 512
-                     and not (i == 1 and self.l0_recompute))  # (that path stores no z for layer 0)
-            self._cfg_cache[key] = v
-        return v
-
-    def _bnin_bwd(self, i: int, n: int) -> bool:
-        """Whether layer i's data-gradient conv applies layer i's BatchNorm backward on load (x3
-        planes, a halo tile, the three-kernel BN backward, kernel-start signals available)."""
-        key = ("bnin_bwd", i, n)
-        v = self._cfg_cache.get(key)
-        if v is None:
-            v = False
-            if (self.bn_bwd_on_load and i > 0 and self.planes[i] and self.np == 3
-                    and self.ksignal and self.free_signal and not self._fused(i, n, True)):
-                l = self.spec.convs[i]
-                tile, _, _ = self.conv_config(i, "dgrad", n)
-                v = tile in (17, 19, 20, 21) and l.cout % 32 == 0 and l.cout <= 512 and (not l.pool or l.hw % 2 == 0)
-            self._cfg_cache[key] = v
-        return v
-
-    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool, stats: Optional[torch.Tensor] = None,
-                  bnin: bool = False) -> int:
+    def _conv_fwd(self, i: int, x: torch.Tensor, n: int, reduce: bool, stats: Optional[torch.Tensor] = None) -> int:
         """Forward conv of layer i into z[i] (or split-K slabs); returns the split count left
-        UNREDUCED in self.slab (1 = result is in z[i]).  stats: BN partials from the epilogue.
-        bnin: apply layer i-1's BN on load (``_bnin``; training forward, slabs never reduced)."""
+        UNREDUCED in self.slab (1 = result is in z[i]).  stats: BN partials from the epilogue."""
         l = self.spec.convs[i]
         tile, s, pm = self.conv_config(i, "fprop", n)
         self._ensure_slab(self._slab_need(i, "fprop", n))
         z = self.z[i][:n]
         slab = self.slab if s > 1 else None
-        if bnin:
-            lp, sp = self.spec.convs[i - 1], self.stats[i - 1]
-            self.K.conv_x3_fprop_bnin(self.z[i - 1][:n], lp.pool, sp["scale"], sp["shift"], self.a3[i - 1][:, :n],
-                                      self.w3[i], z, slab, s, tile, stats)
-            return s
         if self.planes[i]:
             self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm, stats)
         else:
@@ -748,12 +612,6 @@ class VGGEngine:
         self._ensure_slab(self._slab_need(i, "dgrad", n))
         slab = self.slab if s > 1 else None
         out = self.g[i - 1][:n]
-        if sig_val > 0 and self._bnin_bwd(i, n):
-            l, st = self.spec.convs[i], self.stats[i]
-            self.K.conv_x3_dgrad_bnin(self.g[i][:n], self.z[i][:n], l.pool, st["scale"], st["shift"], self.coef,
-                                      self.dz3[i][:, :n], self.w3[i], out, slab, s, tile, sig=self.ksig[i:i + 1],
-                                      sig_val=sig_val)
-            return s
         if self.planes[i]:
             if sig_val > 0:
                 self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm,
@@ -777,13 +635,7 @@ class VGGEngine:
         slab = (self.wslab if side else self.slab) if s > 1 else None
         dw = self.grads[f"{l.conv_key}.weight"]
         if self.planes[i]:
-            fix = None
-            if s > 1 and s <= self.wgrad_fixup_max:  # slabs summed in-kernel by each tile's last split
-                fix = self.wfix_side if side else self.wfix_main
-            if fix is not None:
-                self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm, fix)
-            else:
-                self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
+            self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
         else:
             xin = x if i == 0 else self.a[i - 1][:n]
             self.K.conv_wgrad(xin, self.dz[i][:n], dw, slab, 1, 1, s, tile, pm)
@@ -821,23 +673,8 @@ class VGGEngine:
             epoch = self._sig_epoch
         if self.x0p is not None and not (self.fused_conv0 and self.fused_wgrad0):  # plane kernels read x0p
             K.pad_split8(x, self.x0p[:, :n])
-        self._issue_deferred_update()
-        main = torch.cuda.current_stream(self.device) if self._upd_wait else None
         for i, l in enumerate(L):
             z, st = self.z[i][:n], self.stats[i]
-            if self._upd_wait and i in self._upd_wait:  # this layer's (and later) parameters updated
-                self._upd_wait.pop(i).wait(main)
-            if i == 0 and self.l0_recompute:
-                if buffers_wait is not None:
-                    buffers_wait()
-                    buffers_wait = None
-                w0 = P[f"{l.conv_key}.weight"]
-                K.conv0_stats(x, w0, self.part0, P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"],
-                              P[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
-                              self.buffers[f"{l.bn_key}.running_var"], self.nbt[i:i + 1], st["mean"], st["invstd"],
-                              st["scale"], st["shift"], self.bn_momentum, self.bn_eps)
-                K.conv0_bn_pool(x, w0, st["scale"], st["shift"], self._act_out(i, n))
-                continue
             if i == 0 and self.fused_conv0:
                 if buffers_wait is not None:
                     buffers_wait()
@@ -846,12 +683,10 @@ class VGGEngine:
                             P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
                             self.buffers[f"{l.bn_key}.running_var"], self.nbt[i:i + 1], st["mean"], st["invstd"],
                             st["scale"], st["shift"], self.bn_momentum, self.bn_eps)
-                if not self._bnin(i + 1, n):
-                    K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
+                K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
             erows = self._epi_rows(i, n)
-            nxt_bnin = i + 1 < len(L) and self._bnin(i + 1, n)  # the next conv applies this BN on load
-            ns = self._conv_fwd(i, x, n, reduce=False, stats=self.epart if erows else None, bnin=self._bnin(i, n))
+            ns = self._conv_fwd(i, x, n, reduce=False, stats=self.epart if erows else None)
             if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
                 buffers_wait()
                 buffers_wait = None
@@ -862,20 +697,12 @@ class VGGEngine:
                               self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                               self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
                               self.bn_momentum, self.bn_eps)
-                if not (i == len(L) - 1 and self.fused_head) and not nxt_bnin:
+                if not (i == len(L) - 1 and self.fused_head):
                     K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
-            if self._cols(i, n):  # one launch, no cross-block hand-off (bn_cols.hip)
-                head = (i == len(L) - 1 and self.fused_head) or nxt_bnin
-                K.bn_cols_fwd(self.slab if ns > 1 else z, ns, z, l.pool, P[f"{l.bn_key}.weight"],
-                              P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
-                              self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
-                              self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"],
-                              None if head else self._act_out(i, n), self.bn_momentum, self.bn_eps)
-                continue
             if self._fused(i, n, False):
-                # the head kernel, or the next conv, applies it: statistics and coefficients only
-                head = (i == len(L) - 1 and self.fused_head) or nxt_bnin
+                # the head kernel applies it: statistics and coefficients only
+                head = i == len(L) - 1 and self.fused_head
                 K.bn_fused_fwd(self.slab if ns > 1 else z, ns, z, l.pool, self.bn_fused_rmax, self.fpart, self.fcnt,
                                P[f"{l.bn_key}.weight"], P[f"{l.bn_key}.bias"], P[f"{l.conv_key}.bias"],
                                self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
@@ -888,18 +715,15 @@ class VGGEngine:
                            self.buffers[f"{l.bn_key}.running_mean"], self.buffers[f"{l.bn_key}.running_var"],
                            self.nbt[i:i + 1], st["mean"], st["invstd"], st["scale"], st["shift"], self.bn_momentum,
                            self.bn_eps)
-            if (i == len(L) - 1 and self.fused_head) or nxt_bnin:
-                continue  # applied inside the head kernel below / by the next conv on load
+            if i == len(L) - 1 and self.fused_head:
+                continue  # applied inside the head kernel below
             K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
-        for ev in self._upd_wait.values():  # (networks too short for the layer-indexed waits)
-            ev.wait(main)
-        self._upd_wait = {}
         feat = self.a[-1][:n].view(n, -1)
         bn_in = (dict(bn_z=self.z[-1][:n], bn_scale=self.stats[-1]["scale"], bn_shift=self.stats[-1]["shift"])
                  if self.fused_head else {})
         # the head's weight gradient / batch loss kernel goes to the wgrad stream (nothing on the critical
         # path reads them); it waits for the first BN backward's start signal, which implies the row
-        # kernel (features, dlogits) has completed.  DPA_HEAD_SIDE=0 keeps both on the main stream.
+        # kernel (features, dlogits) has completed.
         head_side = bool(epoch) and self.wstream is not None and self.head_side
         head_args = (feat, P["fc1.weight"], P["fc1.bias"], target, self.loss_row[:n], self.dlogits[:n],
                      self.g[-1][:n].view(n, -1), G["fc1.weight"], G["fc1.bias"], self.loss, self.loss_accum)
@@ -928,10 +752,7 @@ class VGGEngine:
 
         def side_work(j: int, nm: List[str]):
             with torch.cuda.stream(ws):
-                # dz planes written by the data-gradient conv itself (BN backward on load): wait until
-                # it has ENDED, i.e. the next BN backward (layer j-1) has started
-                sig = self.bsig[j - 1:j] if self._bnin_bwd(j, n) else self.ksig[j:j + 1]
-                K.wait_signal(sig, epoch, self.ksig_timeout_us, self.ksig_tmo)
+                K.wait_signal(self.ksig[j:j + 1], epoch, self.ksig_timeout_us, self.ksig_tmo)
                 self._conv_wgrad(j, x, n)
                 if grad_ready is not None:
                     grad_ready(nm)
@@ -977,18 +798,6 @@ class VGGEngine:
             dzbuf = self.dz3[i][:, :n] if self.planes[i] else self.dz[i][:n]
             names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
             bsig = dict(sig=self.bsig[i:i + 1], sig_val=epoch) if epoch else {}
-            if i == 0 and self.l0_recompute:
-                K.bn_bwd_l0(self.slab if gsplit > 1 else g, gsplit, x, P[f"{l.conv_key}.weight"], st["scale"],
-                            st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"], self.l0part,
-                            G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"],
-                            G[f"{l.conv_key}.weight"], **bsig)
-                after_bn(i)
-                drain_side()
-                if grad_ready is not None:
-                    grad_ready(names)
-                if params_free is not None:
-                    params_free(names)
-                continue
             if i == 0 and self.fused_wgrad0:
                 K.bn_bwd_wgrad0(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                                 st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
@@ -1001,23 +810,15 @@ class VGGEngine:
                 if params_free is not None:
                     params_free(names)
                 continue
-            if self._cols(i, n, True):  # one launch, no cross-block hand-off (bn_cols.hip)
-                K.bn_cols_bwd(self.slab if gsplit > 1 else g, gsplit, z, l.pool, st["scale"], st["shift"], st["mean"],
-                              st["invstd"], P[f"{l.bn_key}.weight"], G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"],
-                              G[f"{l.conv_key}.bias"], dzbuf, **bsig)
-            elif self._fused(i, n, True):
+            if self._fused(i, n, True):
                 K.bn_fused_bwd(self.slab if gsplit > 1 else g, gsplit, z, l.pool, self.bn_fused_rmax, self.fpart,
                                self.fcnt, st["scale"], st["shift"], st["mean"], st["invstd"], P[f"{l.bn_key}.weight"],
                                G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf,
                                self.bn_tmo, self.bn_fused_timeout_us, **bsig)
-            elif epoch and self._bnin_bwd(i, n):  # dz is formed on load by dgrad(i)
-                K.bn_bwd_stats(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
-                               st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                               G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], l.pool, tick=self.bn_tick, **bsig)
             else:
                 K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                          st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, tick=self.bn_tick, **bsig)
+                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig)
             after_bn(i)
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
@@ -1078,60 +879,11 @@ class VGGEngine:
 
     def sgd_step(self, grad_scale: float = 1.0, offset: int = 0, count: int = -1, first: Optional[bool] = None):
         """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
-        self.flush_update()
         self._sgd(grad_scale, offset, count, self.steps_taken == 0 if first is None else first)
 
     def _sgd(self, grad_scale: float, offset: int, count: int, first: bool):
         self.K.sgd_flat(self.params.flat, self.grads.flat, self.mom.flat, self.lr, self.momentum, self.weight_decay,
                         grad_scale, first, offset, count, self.wplanes)
-
-    def sgd_step_deferred(self, grad_scale: float = 1.0):
-        """The whole-arena SGD of this step, deferred (see ``defer_update``): layer 0's slice now, the
-        rest at the start of the next ``forward_backward`` (or at ``flush_update``)."""
-        if not (self.defer_update and self._upd_ev is not None and self.wstream is not None
-                and not torch.cuda.is_current_stream_capturing()):
-            self.sgd_step(grad_scale)
-            return
-        self.flush_update()
-        first = self.steps_taken == 0
-        c1 = self._upd_cut[0]
-        self._sgd(grad_scale, 0, c1, first)
-        self._upd_ev[0].record(torch.cuda.current_stream(self.device))
-        self._pending_upd = (grad_scale, first)
-
-    def _issue_deferred_update(self):
-        """Start of a step: the pending update on the weight-gradient stream, behind the end of the
-        previous step; the forward waits for its two halves before conv 1 and conv 4."""
-        if self._pending_upd is None:
-            return
-        scale, first = self._pending_upd
-        self._pending_upd = None
-        c1, c4, end = self._upd_cut
-        s = self.wstream
-        self._upd_ev[0].wait(s)
-        with torch.cuda.stream(s):
-            self._sgd(scale, c1, c4 - c1, first)
-            self._upd_ev[1].record(s)
-            self._sgd(scale, c4, end - c4, first)
-            self._upd_ev[2].record(s)
-        nl = len(self.spec.convs)
-        self._upd_wait = {min(1, nl - 1): self._upd_ev[1], min(4, nl - 1): self._upd_ev[2]}
-        if min(1, nl - 1) == min(4, nl - 1):
-            self._upd_wait = {min(1, nl - 1): self._upd_ev[2]}
-
-    def flush_update(self):
-        """Run a deferred update now, on the current stream (callers that read parameters or momenta
-        outside the step).  Also makes the current stream wait for an issued one."""
-        if self._pending_upd is not None:
-            scale, first = self._pending_upd
-            self._pending_upd = None
-            c1, _, end = self._upd_cut
-            self._sgd(scale, c1, end - c1, first)
-        if self._upd_wait:
-            cur = torch.cuda.current_stream(self.device)
-            for ev in self._upd_wait.values():
-                ev.wait(cur)
-            self._upd_wait = {}
 
     def wait_signal(self, signal):
         """The current stream waits (one polling wave, bounded) for a ``(flag, value)`` signal."""
@@ -1154,7 +906,6 @@ class VGGEngine:
 
     # ------------------------------------------------------------------ evaluation
     def begin_eval(self):
-        self.flush_update()
         for i, l in enumerate(self.spec.convs):
             self.K.bn_eval_params(self.params[f"{l.bn_key}.weight"], self.params[f"{l.bn_key}.bias"],
                                   self.params[f"{l.conv_key}.bias"], self.buffers[f"{l.bn_key}.running_mean"],
@@ -1173,10 +924,6 @@ class VGGEngine:
         if self.x0p is not None and not self.fused_conv0:
             self.K.pad_split8(x, self.x0p[:, :n])
         for i, l in enumerate(self.spec.convs):
-            if i == 0 and self.l0_recompute:
-                self.K.conv0_bn_pool(x, P[f"{l.conv_key}.weight"], self.eval_ss[0]["scale"], self.eval_ss[0]["shift"],
-                                     self._act_out(0, n))
-                continue
             if i == 0 and self.fused_conv0:
                 self.K.conv0_fwd(x, P[f"{l.conv_key}.weight"], self.z[0][:n])
             else:

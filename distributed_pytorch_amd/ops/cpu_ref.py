@@ -133,7 +133,7 @@ def bn_apply(z, a, scale, shift, pool, act=0, res=None, mask=None):  # mask: nat
 
 
 def bn_bwd(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta, dbias, dz, pool,
-           act=0, res=None, dres=None, sig=None, sig_val=0, g2=None, mask=None, tick=None):
+           act=0, res=None, dres=None, sig=None, sig_val=0, g2=None, mask=None):
     N, H, W, C = z.shape
     if nsplit > 1:
         g.copy_(gsrc[:nsplit * g.numel()].view(nsplit, -1).sum(0).view(g.shape))

@@ -245,13 +245,13 @@ def conv_config(kind: str, M: int, Ngemm: int, Kred: int, hw_small: bool) -> Tup
 # (that gradient, the addend).  The gradient's consumer -- the BN backward that produced the block
 # input -- sums the addend on load (bn.hip ``g2``) instead of an elementwise add pass over it.
 _DEFERRED: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
-DEFER_JOIN = os.environ.get("DPA_DEFER_JOIN", "1") == "1"  # A/B switch (0: add pass as before)
+DEFER_JOIN = True  # (tests switch it off: the add pass instead)
 DEFER_STATS = {"summed_on_load": 0}  # BN backwards that consumed a deferred contribution (tests)
-BN_RELU_MASK = os.environ.get("DPA_BN_RELU_MASK", "1") == "1"  # A/B switch (0: backward re-reads the residual)
+BN_RELU_MASK = True  # the add+ReLU forward stores a 1-bit ReLU mask the backward reads (tests: False)
 # BN statistics from the producing conv's epilogue (conv_x3.hip epi_col_stats): a training conv with
 # one split registers its (mean, M2) partials under its output's address; the BN that normalises
 # that output finalizes from them instead of re-reading z (bn_stats_kernel).
-EPI_STATS = os.environ.get("DPA_EPI_STATS", "1") == "1"
+EPI_STATS = True
 # (entries hold the output tensor itself, so its address cannot be reused while the entry lives)
 _STATS: Dict[int, Tuple[torch.Tensor, int, int, Tuple[int, int], torch.Tensor]] = {}
 STATS_USED = {"epilogue": 0}  # BN forwards that finalized from conv epilogue partials (tests)
@@ -261,93 +261,6 @@ def clear_deferred():
     """Drop deferred contributions of an abandoned backward (called at every training forward)."""
     _DEFERRED.clear()
     _STATS.clear()
-    _SIDE_STATE["armed"] = False  # an abandoned backward's end-of-pass join never ran
-    _SIDE_STATE["queue"] = []
-
-
-# Weight gradients on a second stream (the VGG engine's two-stream backward, for autograd): a conv's
-# wgrad reads only its saved input and dz, and nothing in the backward reads dW, so it runs on a
-# per-device side stream behind an event of the compute stream while the compute stream continues
-# with the data gradient, the BatchNorm backwards and the next layers (bandwidth-bound BN passes
-# beside MFMA-bound weight gradients).  Joins: the compute stream waits for the side stream at the
-# end of every backward pass (an autograd engine callback, so plain ``loss.backward()`` users see
-# final .grad), and a collective that reads gradients mid-backward (parallel/ddp.py) joins it into
-# the communicator's stream first (``wgrad_join``).  Tensors the side stream reads are
-# ``record_stream``-ed, so the caching allocator cannot hand their memory to the compute stream early.
-# Only a weight whose gradient autograd adopts without a kernel takes this path (no .grad yet, one
-# use in the forward): an accumulation or a multi-use sum would read dW on the compute stream.
-# DPA_GENERIC_WGRAD_STREAM=1 turns it on (default off); DPA_WGRAD_BATCH=k: the side stream forks from the
-# compute stream once per k weight gradients (they queue until then; fewer cross-stream edges in a
-# captured graph), default 1.  Measured on ResNet-50 (bench_resnet.py, HIP-graph replay, same box,
-# interleaved): one stream 9,175-9,201 img/s; side stream 8,950-8,988; batched forks k = 3 / 8:
-# 8,896-8,942 / 8,917-8,929 (an earlier box: 8,982-8,990 vs 8,966-9,061).  The replayed graph
-# leaves ~0.9 ms per step idle around the cross-stream edges and the overlapped kernels slow each
-# other (kernel time 14.2 -> 16.5 ms); the eager step overlaps better but is host-bound and erratic
-# (9,467 and 7,402 img/s).  docs/PERF_NOTES.md, round 4.
-WGRAD_STREAM = os.environ.get("DPA_GENERIC_WGRAD_STREAM", "0") == "1"
-WGRAD_BATCH = max(1, int(os.environ.get("DPA_WGRAD_BATCH", "1")))
-_SIDE: Dict[torch.device, torch.cuda.Stream] = {}
-_SIDE_STATE = {"armed": False, "pending": set(), "queue": []}
-
-
-def _wgrad_side(dev: torch.device, w: torch.Tensor) -> Optional["torch.cuda.Stream"]:
-    if not (WGRAD_STREAM and dev.type == "cuda") or _AUTOTUNE["on"]:
-        return None
-    if w.grad is not None or getattr(w, "_dpa_uses", 1) != 1:
-        return None
-    s = _SIDE.get(dev)
-    if s is None:
-        s = _SIDE[dev] = torch.cuda.Stream(dev)
-    return s
-
-
-def _flush_side():
-    """Launch the queued weight gradients on their side streams, behind their compute streams."""
-    q = _SIDE_STATE["queue"]
-    if not q:
-        return
-    _SIDE_STATE["queue"] = []
-    forked = set()
-    for main, dev, run, keep in q:
-        side = _SIDE[dev]
-        if (main, dev) not in forked:
-            side.wait_stream(main)
-            forked.add((main, dev))
-        with torch.cuda.stream(side):
-            run()
-        for t in keep:
-            t.record_stream(side)
-
-
-def wgrad_join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
-    """Order ``stream`` (default: the current stream) after every weight gradient queued so far on
-    the side stream of ``device`` (default: every device with pending side work)."""
-    _flush_side()
-    devs = [torch.device(device)] if device is not None else list(_SIDE_STATE["pending"])
-    for d in devs:
-        s = _SIDE.get(d)
-        if s is not None and d in _SIDE_STATE["pending"]:
-            (stream or torch.cuda.current_stream(d)).wait_stream(s)
-
-
-def _side_submit(main: "torch.cuda.Stream", dev: torch.device, run: Callable[[], None], keep) -> None:
-    """Queue one weight gradient for the side stream (launched at once when WGRAD_BATCH is 1) and
-    arm the end-of-backward join."""
-    _SIDE_STATE["pending"].add(dev)
-    _SIDE_STATE["queue"].append((main, dev, run, keep))
-    if len(_SIDE_STATE["queue"]) >= WGRAD_BATCH:
-        _flush_side()
-    if _SIDE_STATE["armed"]:
-        return
-
-    def join():
-        _SIDE_STATE["armed"] = False
-        _flush_side()
-        main.wait_stream(_SIDE[dev])
-        _SIDE_STATE["pending"].discard(dev)
-
-    _SIDE_STATE["armed"] = True
-    torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 class GradJoin:
@@ -539,21 +452,14 @@ class Conv2dNHWC(torch.autograd.Function):
             dw = grad_slot(ctx.w_param)
             if dw is None:
                 dw = torch.empty(K, R, S, C, device=dz.device, dtype=torch.float32)
-            side = _wgrad_side(dz.device, ctx.w_param)
-            skey = "slab" if side is None else "wslab"  # the side stream's own split-K slab
 
             def run_w(tile, s, pm):
-                slab = WS.get(skey, s * K * R * S * C, dz.device) if s > 1 else None
+                slab = WS.get("slab", s * K * R * S * C, dz.device) if s > 1 else None
                 Kx.conv_x3_wgrad(xp, dzp, dw, slab, stride, pad, s, tile, pm)
 
             cfg = choose_config(ctx.impl, "wgrad", geom, N * P * Q, K, R * S * C, P * Q <= 16, run_w,
                                 lambda s: 4 * s * K * R * S * C)
-            if side is None:
-                run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
-            else:
-                sk = Kx.x3_splits(N * P * Q, cfg[1])
-                _side_submit(torch.cuda.current_stream(dz.device), dz.device,
-                             lambda: run_w(cfg[0], sk, cfg[2]), (xp, dzp, dw))
+            run_w(cfg[0], Kx.x3_splits(N * P * Q, cfg[1]), cfg[2])
         if dx is not None and ctx.cx != C:
             dx = dx[..., :ctx.cx].contiguous()
         if join is not None and dx is not None and addend is None:
@@ -695,10 +601,10 @@ class BnActNHWC(torch.autograd.Function):
         return dz, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None, None
 
 
-# BN + ReLU + max-pool as one forward pass (bn_act_nhwc ``pool``); A/B switch (0: apply pass + pool)
-FUSE_BN_POOL = os.environ.get("DPA_FUSE_BN_POOL", "1") == "1"
-# the downsample branch's BN applied inside the block's add + ReLU (bn_act_nhwc ``res_bn``); A/B switch
-FUSE_RES_BN = os.environ.get("DPA_FUSE_RES_BN", "1") == "1"
+# BN + ReLU + max-pool as one forward pass (bn_act_nhwc ``pool``; tests: False = apply pass + pool)
+FUSE_BN_POOL = True
+# the downsample branch's BN applied inside the block's add + ReLU (bn_act_nhwc ``res_bn``; tests: False)
+FUSE_RES_BN = True
 
 
 def bn_act_nhwc(z, gamma, beta, running_mean, running_var, num_batches_tracked, training: bool = True,

@@ -66,6 +66,10 @@ class Comm:
     def wait(self):
         pass
 
+    def prepare(self, tensors):
+        """Collective hint (every rank, same tensors, same order): these tensors will carry
+        collectives for the communicator's lifetime (the peer-memory communicator maps them)."""
+
     def synchronize(self):
         pass
 
@@ -253,7 +257,7 @@ class RcclComm(Comm):
             uid = exchange_unique_id(store, rank, C.rccl_unique_id, tag)
         with torch.cuda.device(self.device):
             self._c = C.RcclComm(rank, world, bytes(uid), self.device.index or 0,
-                                 high_priority=os.environ.get("DPA_COMM_HIPRIO", "0") == "1",
+                                 high_priority=False,
                                  timeout_s=float(os.environ.get("DPA_COMM_TIMEOUT", "600")),
                                  watchdog=os.environ.get("DPA_WATCHDOG", "1") == "1",
                                  exit_on_error=os.environ.get("DPA_WATCHDOG_EXIT", "1") == "1",

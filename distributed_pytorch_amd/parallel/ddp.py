@@ -23,7 +23,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn as nn
 
-from ..ops.functional import NPLANES, wgrad_join
+from ..ops.functional import NPLANES
 from .comm import Comm, NullComm
 
 ALIGN = 64
@@ -112,6 +112,7 @@ class DistributedDataParallel(nn.Module):
         self._bufs_sent = False   # buffers broadcast during the current step (first gradient hook)
         self._bufs_fresh = False  # replicas already hold rank 0's buffers for the next forward
         if self.active:
+            self.comm.prepare([self._gflat.flat, self._pflat.flat] + [fl.flat for fl in self._bufs])
             self._broadcast_state()
         self._init_planes(order, dev)
 
@@ -181,7 +182,6 @@ class DistributedDataParallel(nn.Module):
                 # fused optimizer read
                 v = self._gflat.view(i, p)
                 if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
-                    wgrad_join()  # the gradient may still be in flight on the weight-gradient stream
                     with torch.no_grad():
                         v.copy_(p.grad)
                     p.grad = v
@@ -213,7 +213,6 @@ class DistributedDataParallel(nn.Module):
         self._issued[b] = True
         lo, hi = self._span(b)
         with self.comm.region():
-            wgrad_join()  # the communicator's stream also waits for the weight-gradient stream
             self.comm.all_reduce(self._gflat.flat[lo:hi], "sum")
 
     def finish(self) -> float:

@@ -12,8 +12,10 @@ One process per GPU: LOCAL_RANK (or rank mod #GPUs) selects the device.  Rendezv
   (ncclUniqueId exchange) and provides the CPU-side barriers;
 * ``torch`` (default on CPU, and for ``--comm torch``): a torch.distributed gloo group carries the
   rendezvous store and barriers — on CPU it is also the communicator (the multi-process test oracle).
-On GPU the gradient collectives go through the native RCCL communicator (``comm="rccl"``), or
-through torch's own nccl group (``comm="torch"``, torch rendezvous only) for A/B comparison.
+On GPU the gradient collectives go through the native RCCL communicator (``comm="rccl"``), the
+peer-memory kernels alone (``comm="ipc"``, one node: HIP IPC mappings, several ranks may share a
+GPU; parallel/ipc.py), or torch's own nccl group (``comm="torch"``, torch rendezvous only) for A/B
+comparison.
 There is no silent fallback: if the native communicator cannot be created the job fails
 (``DPA_COMM_FALLBACK=1`` opts into torch's nccl group instead, which the bench reports).
 """
@@ -97,7 +99,7 @@ def _rendezvous(device: torch.device, comm: str = "rccl") -> str:
     if r not in ("auto", "torch", "native"):
         raise ValueError("DPA_RENDEZVOUS must be 'auto', 'torch' or 'native'")
     if r == "auto":
-        return "native" if device.type == "cuda" and comm == "rccl" else "torch"
+        return "native" if device.type == "cuda" and comm in ("rccl", "ipc") else "torch"
     return r
 
 
@@ -140,6 +142,12 @@ def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=Non
         if store is not None:
             raise RuntimeError("native rendezvous drives RCCL only: use DPA_RENDEZVOUS=torch (gloo) on CPU")
         return TorchComm(device=device)
+    if kind == "ipc":  # peer-memory collectives only (parallel/ipc.py): no host staging, no RCCL
+        from .ipc import IpcComm
+
+        if store is None:
+            store = dist.distributed_c10d._get_default_store()
+        return IpcComm(None, store, device, rank=rank, world=world)
     if kind == "gloo":  # GPU tensors staged through gloo: several ranks may share one GPU (rehearsal)
         if store is not None:
             raise RuntimeError("--comm gloo needs the torch rendezvous")

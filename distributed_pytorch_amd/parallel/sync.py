@@ -39,9 +39,6 @@ from ..utils.streams import DevEvent, StreamJoin
 from .comm import Comm
 
 
-# DPA_BUF_BCAST=pre restores the per-forward buffer broadcast of torch DDP (A/B); default post
-_POST_FORWARD_BUFFERS = os.environ.get("DPA_BUF_BCAST", "post") != "pre"
-_SIGNAL_BUFFERS = os.environ.get("DPA_BUF_SIGNAL", "1") == "1"  # A/B switch (DDPSync)
 
 
 class Bucket:
@@ -146,8 +143,8 @@ class GradSync:
         # The last bucket's collective goes on the stream that reports it (the main stream, right
         # after backward) once that stream has waited for the comm stream: the all-reduce then needs
         # no hop there and no hop back before the update (1-rank RCCL trace: ~34 us of step tail in
-        # two cross-stream hops).  DPA_TAIL_HERE=0: every bucket on the comm stream (A/B).
-        self.tail_here = (self._cuda and os.environ.get("DPA_TAIL_HERE", "1") == "1"
+        # two cross-stream hops).
+        self.tail_here = (self._cuda
                           and type(self).reduce_bucket_here is not GradSync.reduce_bucket_here)
         self._joined = False
         self._main = None
@@ -155,13 +152,15 @@ class GradSync:
         # collective on the comm stream (bench diagnostic phase only)
         self.probe = None
         self._index = {id(b): i for i, b in enumerate(self.buckets)}
+        if self.active and self._cuda:  # the arenas every collective of this strategy moves
+            e = engine
+            comm.prepare([e.grads.flat, e.params.flat, e.mom.flat, e.buffers.flat, e.nbt])
         if broadcast_init and self.active:
             self.broadcast_state()
 
     # -- state broadcast (DDP ctor semantics; torch distributed.py:862-871) --
     def broadcast_state(self):
         e = self.engine
-        e.flush_update()
         with self.comm.region():
             self.comm.broadcast(e.params.flat, 0)
             if self.shared_buffers:
@@ -174,8 +173,7 @@ class GradSync:
 
     def prepare_checkpoint(self):
         """Collective hook before every rank writes its checkpoint: make the local optimizer state
-        complete (a no-op except for sharded optimizer state and a deferred update)."""
-        self.engine.flush_update()
+        complete (a no-op except for sharded optimizer state)."""
 
     def pre_forward(self):
         """Called before the training forward.  May return a callable that the engine invokes
@@ -308,7 +306,7 @@ class GradSync:
         """Apply the optimizer step to the synchronised gradients (the whole arena by default;
         with the fused step only slices whose update was not already queued during backward)."""
         if not self.fuse_step:
-            self.engine.sgd_step_deferred(grad_scale)  # (immediate unless engine.defer_update)
+            self.engine.sgd_step(grad_scale)
             return
         for b in self.buckets:
             if not b.stepped:
@@ -360,8 +358,7 @@ class DDPSync(GradSync):
     after each training forward (under the backward) instead of before the next forward, so after
     the last training step every replica already holds rank 0's statistics — which torch DDP only
     establishes at the first eval forward.  Eval results are identical; a per-rank checkpoint taken
-    at that point holds rank 0's statistics on every rank (``DPA_BUF_BCAST=pre`` restores torch's
-    placement)."""
+    at that point holds rank 0's statistics on every rank."""
 
     mode = "ddp"
 
@@ -393,14 +390,14 @@ class DDPSync(GradSync):
         self._bufs_sent = self._bufs_fresh = True
 
     def _post_forward_send(self) -> bool:
-        return self.active and self.broadcast_buffers and not self._bufs_sent and _POST_FORWARD_BUFFERS
+        return self.active and self.broadcast_buffers and not self._bufs_sent
 
     def begin_step(self):
         super().begin_step()
         self._bufs_sent = False
         # a signal will come with the head's params_free (engine forward_backward, eager steps)
         e = self.engine
-        self._sig_bufs = (_SIGNAL_BUFFERS and getattr(e, "ksignal", False) and getattr(e, "free_signal", False)
+        self._sig_bufs = (getattr(e, "ksignal", False) and getattr(e, "free_signal", False)
                           and not torch.cuda.is_current_stream_capturing())
 
     def grad_ready(self, names: List[str]):
@@ -462,7 +459,6 @@ class ZeroSync(DDPSync):
         rank holds the complete momentum arena already (``prepare_checkpoint`` all-gathers the
         shards before each save)."""
         e = self.engine
-        e.flush_update()
         with self.comm.region():
             self.comm.broadcast(e.params.flat, 0)
             if self.shared_buffers:
@@ -474,7 +470,6 @@ class ZeroSync(DDPSync):
     def prepare_checkpoint(self):
         """All-gather every bucket's owned momentum shards so each rank's arena (and checkpoint)
         holds the full, current SGD state."""
-        self.engine.flush_update()
         if not self.active:
             return
         e = self.engine

@@ -169,7 +169,7 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--train-size", type=int, default=50000)
     g.add_argument("--test-size", type=int, default=10000)
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
-    g.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"])
+    g.add_argument("--comm", default="rccl", choices=["rccl", "ipc", "torch", "gloo"])
     g.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
                    help="GPU conv kernels: x3 (fp32-grade via bf16 planes, default) | fp32 MFMA | bf16")
     g.add_argument("--bucket-mb", type=float, default=None)

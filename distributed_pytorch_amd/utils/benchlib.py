@@ -62,21 +62,14 @@ def device_barrier(ctx, dev: torch.device):
         torch.cuda.synchronize(dev)
 
 
-def timed_steps(step: Callable[[], None], steps: int, warmup: int, ctx, dev: torch.device,
-                flush: Optional[Callable[[], None]] = None) -> float:
-    """Seconds for ``steps`` steps after ``warmup`` untimed ones; max over ranks.  ``flush``: issues
-    work a step leaves for the next one (a deferred optimizer update), after the warmup (untimed) and
-    after the last timed step (timed), so the timed region holds exactly ``steps`` steps of work."""
+def timed_steps(step: Callable[[], None], steps: int, warmup: int, ctx, dev: torch.device) -> float:
+    """Seconds for ``steps`` steps after ``warmup`` untimed ones; max over ranks."""
     for _ in range(warmup):
         step()
-    if flush is not None:
-        flush()
     device_barrier(ctx, dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    if flush is not None:
-        flush()
     device_barrier(ctx, dev)
     el = time.perf_counter() - t0
     return ctx.all_max(el)

@@ -5,27 +5,20 @@ invalidates L2, and the next kernel on the recording stream starts only after th
 ``tools/event_overhead.py``).  The step's dependencies are all between streams of one device, so
 the framework records native events (``_C.DevEvent``) with a device-scope release instead.
 
-``DPA_EVENT_SCOPE``: ``device`` (default, hipEventReleaseToDevice), ``nofence``
-(hipEventDisableSystemFence) or ``torch`` (plain torch.cuda.Event, for A/B comparison).
+(hipEventReleaseToDevice; torch events and hipEventDisableSystemFence were measured slower,
+docs/PERF_NOTES.md.)
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
-_SCOPE = os.environ.get("DPA_EVENT_SCOPE", "device")
-
-
 def _native_flags() -> Optional[int]:
-    if _SCOPE == "torch":
-        return None
     from .. import _ext
 
     C = _ext.require()
-    extra = C.EVENT_DISABLE_SYSTEM_FENCE if _SCOPE == "nofence" else C.EVENT_RELEASE_TO_DEVICE
-    return C.EVENT_DISABLE_TIMING | extra
+    return C.EVENT_DISABLE_TIMING | C.EVENT_RELEASE_TO_DEVICE
 
 
 class DevEvent:

@@ -11,5 +11,5 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 gpurun_out/rn3_tests.log
 timeout -k 10 600 python bench_resnet.py --autotune --steps 5 --warmup 2 > gpurun_out/rn_autotune.log 2>&1 || { tail -20 gpurun_out/rn_autotune.log; exit 1; }
 cp distributed_pytorch_amd/tuning/generic_mi355x.json gpurun_out/generic_mi355x.json
-AB_ENVS="${AB:-DPA_BN_DY_PASS=0|DPA_BN_DY_PASS=1}" REPS=3 BENCH=bench_resnet.py STEPS=100 WARMUP=10 bash scripts/gpu_ab.sh
+AB_ENVS="${AB:-X=0|X=1}" REPS=3 BENCH=bench_resnet.py STEPS=100 WARMUP=10 bash scripts/gpu_ab.sh
 REPS=2 BENCH=bench_resnet.py STEPS=100 WARMUP=10 ARGS="--graph on" bash scripts/gpu_ab.sh

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/val_gpu_tests.log 2>&1 || { tail -40 gpurun_out/val_gpu_tests.log; exit 1; }
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/val_gpu_tests.log 2>&1 || { tail -40 gpurun_out/val_gpu_tests.log; exit 1; }
 tail -1 gpurun_out/val_gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/val_smoke.log 2>&1 || { tail -20 gpurun_out/val_smoke.log; exit 1; }
 tail -1 gpurun_out/val_smoke.log

@@ -282,43 +282,6 @@ def test_conv_x3_wgrad(shape, splits, tile, posmajor, np_):
     assert rel_err(dw.permute(0, 3, 1, 2), gw) < (1e-5 if np_ == 3 else 2e-2)
 
 
-@pytest.mark.parametrize("shape", [(64, 4, 4, 256, 512, 3, 1, 1), (16, 8, 8, 64, 128, 3, 1, 1),
-                                   (8, 2, 2, 512, 512, 3, 1, 1)])
-@pytest.mark.parametrize("splits", [2, 8])
-@pytest.mark.parametrize("tile", [0, 2, 7, 11])
-def test_conv_x3_wgrad_fixup(shape, splits, tile):
-    """In-kernel split-K fix-up (conv_x3.hip splitk_fixup): dW is bitwise the split-order sum of the
-    slabs the same launch left behind, within fp64 tolerance of autograd, and the per-tile counters
-    are re-armed (all zero) after every launch, so back-to-back calls stay correct."""
-    C = _C()
-    N, H, W, Cin, K, R, st, pd = shape
-    g = torch.Generator().manual_seed(21)
-    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
-    w = (torch.randn(K, Cin, R, R, generator=g, dtype=torch.float64) * 0.1).requires_grad_(True)
-    y = F.conv2d(x, w, stride=st, padding=pd)
-    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
-    (gw,) = torch.autograd.grad(y, w, dy)
-    x3 = _planes(x.float().permute(0, 2, 3, 1), 3)
-    dz3 = _planes(dy.float().permute(0, 2, 3, 1), 3)
-    fix = torch.zeros(4096, dtype=torch.int32, device="cuda")
-    slab = torch.full((splits * K * R * R * Cin,), float("nan"), device="cuda")
-    ref = torch.empty(K, R, R, Cin, device="cuda")
-    C.conv_x3_wgrad(x3, dz3, ref, slab.clone(), st, pd, splits, tile, 0)  # separate reduce kernel
-    for rep in range(3):
-        dw = torch.full((K, R, R, Cin), float("nan"), device="cuda")
-        C.conv_x3_wgrad(x3, dz3, dw, slab, st, pd, splits, tile, 0, fix)
-        torch.cuda.synchronize()
-        assert int(fix.abs().sum()) == 0, rep
-        sl = [r for r in slab.view(-1, K * R * R * Cin) if not torch.isnan(r).all()]  # effective splits
-        assert len(sl) > 1
-        seq = sl[0].clone()
-        for r in sl[1:]:
-            seq = seq + r
-        assert torch.equal(dw.flatten(), seq), rep
-        assert rel_err(dw.permute(0, 3, 1, 2), gw) < 1e-5
-        assert (dw - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-
-
 def test_x3_accuracy_matches_fp32_mfma():
     """The bf16x6 plane path must be as accurate as the exact-fp32 MFMA path (both vs fp64):
     this is what licenses reporting it as fp32 compute."""
@@ -381,11 +344,11 @@ def _halo_ok(kind, tile, w, cred, cout):
 
 @pytest.mark.parametrize("shape", HALO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21])
 @pytest.mark.parametrize("np_", [3, 1])
 @pytest.mark.parametrize("dgrad", [False, True])
 def test_conv_halo(shape, splits, tile, np_, dgrad):
-    """Halo-staged 3x3 fprop / data gradient (tiles 16-23) against fp64: partial blocks, blocks
+    """Halo-staged 3x3 fprop / data gradient (tiles 16-21) against fp64: partial blocks, blocks
     across image boundaries, bands of rows, partial column tiles (128- and 64-column tiles) and
     split-K."""
     C = _C()

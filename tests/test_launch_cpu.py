@@ -277,8 +277,11 @@ def test_comm_plans_per_mode():
                                                                       (None, 2.0, True, 0, False)]
     assert bench.comm_plans(bench.parse(["--mode", "gather"])) == []
     assert bench.comm_plans(bench.parse(["--mode", "zero1"])) == []
-    p = bench.comm_plans(bench.parse(["--mode", "ddp"]), ipc=True)
-    assert p[-1] == (10.0, 2.0, False, 0, True) and len(p) == 6
+    p = bench.comm_plans(bench.parse(["--mode", "ddp"]), ipc=True)  # ipc block budgets
+    assert p[-3:] == [(10.0, 2.0, False, 0, 32), (10.0, 2.0, False, 0, 16), (10.0, 2.0, False, 0, 64)]
+    assert len(p) == 8
+    p = bench.comm_plans(bench.parse(["--mode", "ddp", "--ipc-blocks", "8"]), ipc=True)
+    assert p[-1] == (10.0, 2.0, False, 0, 8) and len(p) == 6
 
 
 def test_comm_plans_rccl_channel_budgets(monkeypatch):
@@ -300,31 +303,32 @@ def test_comm_plans_rccl_channel_budgets(monkeypatch):
 
 
 def test_ipc_collective_pieces_cover_the_tensor():
-    """parallel/ipc.py: a collective larger than the staging buffer runs as consecutive pieces of at
-    most stage * world elements (multiples of 4 * world: 16-byte aligned offsets) that cover it
-    exactly; a small one is one piece."""
-    import torch
+    """csrc/runtime/ipc_comm.cpp IpcComm::pieces: a collective larger than what the staging buffer
+    (all-reduce) or the inbox (bounced inputs) holds runs as consecutive pieces that cover it
+    exactly, each a multiple of 4 words except the last (16-byte aligned offsets), each fitting its
+    buffer; registered inputs of the copy collectives are one piece."""
+    from distributed_pytorch_amd import _ext
 
-    from distributed_pytorch_amd.parallel.ipc import IpcComm
-
-    calls = []
-
-    class FakeNative:
-        def all_reduce(self, rid, off, n, blocks, tmo):
-            calls.append((rid, off, n))
-
-    for world, stage, n in ((2, 1000, 4099), (8, 65536, 9_225_000), (4, 1 << 22, 12345)):
-        c = object.__new__(IpcComm)
-        c.world, c.blocks, c.timeout_s, c.ipc_ops = world, 16, 1.0, 0
-        c.max_elems = (stage // 4 * 4) * world
-        c._c = FakeNative()
-        t = torch.zeros(n + 64)
-        c._regions = {(t.data_ptr(), t.numel()): 3}
-        calls.clear()
-        c._peer_all_reduce(t[16:16 + n])
-        assert sum(k for _, _, k in calls) == n and c.ipc_ops == len(calls)
-        pos = 16
-        for rid, off, k in calls:
-            assert rid == 3 and off == pos and k <= c.max_elems and off % 4 == 0
+    C = _ext.require()
+    AR, BC, GA, RS, AG = 0, 1, 2, 3, 4
+    for op, world, stage, inbox, n, reg in ((AR, 2, 1000, 1 << 20, 4099, True), (AR, 8, 65536, 1 << 22, 9_225_000, True),
+                                            (AR, 4, 1 << 22, 1 << 22, 12345, True), (AR, 8, 1 << 22, 40_000, 9_231_114, False),
+                                            (BC, 2, 4, 40_000, 100_003, False), (BC, 8, 4, 40_000, 100_003, True),
+                                            (GA, 4, 4, 4096, 65_537, False), (RS, 2, 4, 40_000, 40_028, False),
+                                            (RS, 8, 4, 40_000, 40_028, True), (AG, 3, 4, 40_000, 40_031, False)):
+        ps = C.ipc_pieces(op, n, world, stage, inbox, reg)
+        pos = 0
+        for off, k in ps:
+            assert off == pos and k > 0 and off % 4 == 0, (op, ps)
             pos += k
-        assert len(calls) == -(-n // c.max_elems)
+            if op == AR:
+                sl = C.ipc_slice(k, world)
+                assert sl <= stage and (reg or sl * world <= inbox), (op, k, sl)
+            elif op == RS and not reg:
+                assert k * world <= inbox
+            elif not reg:
+                assert k <= inbox
+        assert pos == n, (op, n, ps)
+        if reg and op != AR:
+            assert len(ps) == 1
+    assert C.ipc_pieces(AR, 0, 4, 1 << 20, 1 << 20, True) == []

@@ -1,7 +1,7 @@
-"""Layer 0 of VGG-11 without a stored z (first_layer.hip): the statistics pass, the recomputing
-apply pass and the one-pass backward from (g, x) against torch autograd in fp64 — conv2d(3->64,
-3x3, pad 1) -> BatchNorm2d(train) -> ReLU -> MaxPool2d(2, 2), /root/reference/model.py:16-25 — and
-against the framework's earlier z-storing kernels (conv0_fwd + bn_apply, bn_bwd_wgrad0).
+"""Layer 0 of VGG-11 on its fused kernels (first_layer.hip conv0_fwd with the BN statistics in its
+epilogue, bn_apply with the 2x2 max-pool, bn.hip bn_bwd_wgrad0: the BN backward apply fused with
+the weight gradient) against torch autograd in fp64 — conv2d(3->64, 3x3, pad 1) ->
+BatchNorm2d(train) -> ReLU -> MaxPool2d(2, 2), /root/reference/model.py:16-25.
 
 Operands sit on coarse binary grids (x in quarters, w in eighths), so every conv output is exact
 in fp32 and fp64 alike; beta puts each channel's ReLU threshold half-way between two output levels.
@@ -71,25 +71,29 @@ def _case(N, CP, seed):
 
 
 @pytest.mark.parametrize("N,CP", [(256, 8), (16, 4), (2, 8)])
-def test_layer0_recompute_forward_and_backward(N, CP):
+def test_layer0_fused_forward_and_backward(N, CP):
     C = _C()
     ops, ref = _case(N, CP, 10 + N)
     dev = "cuda"
     part = torch.zeros(C.conv0_part_floats(N), device=dev)
     mean, invstd, scale, shift = (torch.zeros(64, device=dev) for _ in range(4))
     rm, rv, nbt = ops["rm"].clone(), ops["rv"].clone(), torch.zeros(1, dtype=torch.int64, device=dev)
-    C.conv0_stats(ops["x"], ops["w"], part, ops["gamma"], ops["beta"], ops["bias"], rm, rv, nbt, mean, invstd, scale,
-                  shift, MOM, EPS)
+    z = torch.empty(N, 32, 32, 64, device=dev)
+    C.conv0_fwd(ops["x"], ops["w"], z, part, ops["gamma"], ops["beta"], ops["bias"], rm, rv, nbt, mean, invstd, scale,
+                shift, MOM, EPS)
     planes = torch.empty(3, N, 16, 16, 64, device=dev, dtype=torch.bfloat16)
-    C.conv0_bn_pool(ops["x"], ops["w"], scale, shift, planes)
+    C.bn_apply(z, planes, scale, shift, True)
     a32 = torch.empty(N, 16, 16, 64, device=dev)
-    C.conv0_bn_pool(ops["x"], ops["w"], scale, shift, a32)
-    wpart = torch.empty(C.bn_bwd_l0_part_floats(N), device=dev)
+    C.bn_apply(z, a32, scale, shift, True)
+    g = ops["gout"].clone()
+    bpart = torch.zeros(C.bn_part_floats(N * 256, 64, True), device=dev)
+    coef = torch.empty(3 * 64, device=dev)
+    wpart = torch.empty(C.wgrad0_part_floats(N), device=dev)
     dg, db, dbias = (torch.zeros(64, device=dev) for _ in range(3))
     dw = torch.empty_like(ops["w"])
     sig = torch.zeros(1, dtype=torch.int32, device=dev)
-    C.bn_bwd_l0(ops["gout"], 1, ops["x"], ops["w"], scale, shift, mean, invstd, ops["gamma"], wpart, dg, db, dbias, dw,
-                sig=sig, sig_val=5)
+    C.bn_bwd_wgrad0(g, 1, g, z, scale, shift, mean, invstd, ops["gamma"], bpart, coef, dg, db, dbias, ops["x"], wpart,
+                    dw, sig=sig, sig_val=5)
     torch.cuda.synchronize()
     assert int(sig.item()) == 5
     assert _rel(mean, ref["mean"]) < 1e-5 and _rel(invstd, ref["invstd"]) < 1e-5
@@ -101,45 +105,3 @@ def test_layer0_recompute_forward_and_backward(N, CP):
     assert dbias.abs().max().item() < 1e-3 * ref["dbeta"].abs().max().item() + 1e-4  # analytically 0
     assert _rel(dw[..., :3].permute(0, 3, 1, 2), ref["dw"]) < 2e-5, _rel(dw[..., :3].permute(0, 3, 1, 2), ref["dw"])
     assert dw[..., 3:].abs().max().item() == 0.0 if CP > 3 else True
-
-
-def test_layer0_recompute_matches_stored_z_kernels():
-    """The recompute path and the earlier z-storing kernels agree: statistics bitwise, the pooled
-    planes bitwise, gradients to fp32 rounding."""
-    C = _C()
-    N, CP = 64, 8
-    ops, _ = _case(N, CP, 3)
-    dev = "cuda"
-    outs = {}
-    for path in ("stored", "recompute"):
-        part = torch.zeros(C.conv0_part_floats(N), device=dev)
-        mean, invstd, scale, shift = (torch.zeros(64, device=dev) for _ in range(4))
-        rm, rv, nbt = ops["rm"].clone(), ops["rv"].clone(), torch.zeros(1, dtype=torch.int64, device=dev)
-        planes = torch.empty(3, N, 16, 16, 64, device=dev, dtype=torch.bfloat16)
-        dg, db, dbias = (torch.zeros(64, device=dev) for _ in range(3))
-        dw = torch.empty_like(ops["w"])
-        if path == "stored":
-            z = torch.empty(N, 32, 32, 64, device=dev)
-            C.conv0_fwd(ops["x"], ops["w"], z, part, ops["gamma"], ops["beta"], ops["bias"], rm, rv, nbt, mean,
-                        invstd, scale, shift, MOM, EPS)
-            C.bn_apply(z, planes, scale, shift, True)
-            g = ops["gout"].clone()
-            bpart = torch.zeros(C.bn_part_floats(N * 256, 64, True), device=dev)
-            coef = torch.empty(3 * 64, device=dev)
-            wpart = torch.empty(C.wgrad0_part_floats(N), device=dev)
-            C.bn_bwd_wgrad0(g, 1, g, z, scale, shift, mean, invstd, ops["gamma"], bpart, coef, dg, db, dbias, ops["x"],
-                            wpart, dw)
-        else:
-            C.conv0_stats(ops["x"], ops["w"], part, ops["gamma"], ops["beta"], ops["bias"], rm, rv, nbt, mean, invstd,
-                          scale, shift, MOM, EPS)
-            C.conv0_bn_pool(ops["x"], ops["w"], scale, shift, planes)
-            wpart = torch.empty(C.bn_bwd_l0_part_floats(N), device=dev)
-            C.bn_bwd_l0(ops["gout"], 1, ops["x"], ops["w"], scale, shift, mean, invstd, ops["gamma"], wpart, dg, db,
-                        dbias, dw)
-        torch.cuda.synchronize()
-        outs[path] = dict(stats=torch.cat([mean, invstd, scale, shift, rm, rv]), planes=planes, dg=dg, db=db, dw=dw)
-    s, r = outs["stored"], outs["recompute"]
-    assert torch.equal(s["stats"], r["stats"])
-    assert torch.equal(s["planes"], r["planes"])
-    for k in ("dg", "db", "dw"):
-        assert _rel(r[k], s[k]) < 1e-5, (k, _rel(r[k], s[k]))

@@ -428,7 +428,7 @@ def test_resnet_relu_mask_matches_residual_recompute(monkeypatch, impl):
 
 @pytest.mark.parametrize("impl", ["x3", "bf16"])
 def test_resnet_epilogue_bn_stats(monkeypatch, impl):
-    """BN statistics from the producing conv's epilogue (DPA_EPI_STATS) vs the statistics pass:
+    """BN statistics from the producing conv's epilogue (functional.EPI_STATS) vs the statistics pass:
     the forward BNs really take the epilogue path, the running statistics agree to fp32 rounding
     and the loss and gradients within the conditioning of a batch-8 step."""
     from distributed_pytorch_amd.models import resnet as R
@@ -485,43 +485,6 @@ def test_eval_no_grad_registers_no_epilogue_stats():
     assert len(R.Fn._STATS) == 0
 
 
-@pytest.mark.parametrize("impl", ["x3", "bf16"])
-def test_resnet_bn_dy_pass(monkeypatch, impl):
-    """Add+ReLU BN backward with the dy pass (DPA_BN_DY_PASS=1: the reduce kernel stores
-    dy = relu'(u + r) * (g + g2), which is the residual gradient, and the apply pass reads dy alone)
-    against the apply pass re-reading g, g2 and the mask (=0).  x3: dy is stored in fp32, so the
-    gradients are bitwise equal.  bf16: the apply pass reads the bf16-rounded dy; both paths are
-    compared with the x3 (fp32-grade) gradients, and the dy pass must be no less accurate."""
-    from distributed_pytorch_amd.models import resnet as R
-
-    torch.manual_seed(0)
-    sd = R.ResNet([1, 3, 1, 1], 10, impl=impl).state_dict()
-    g = torch.Generator().manual_seed(9)
-    x = torch.randn(8, 64, 64, 3, generator=g).cuda()
-    t = torch.randint(0, 10, (8,), generator=g).cuda()
-
-    def run(impl_, dy_pass):
-        monkeypatch.setenv("DPA_BN_DY_PASS", "1" if dy_pass else "0")
-        m = R.ResNet([1, 3, 1, 1], 10, impl=impl_)
-        m.load_state_dict(sd)
-        m = m.cuda()
-        m(x, t).backward()
-        torch.cuda.synchronize()
-        return {n: p.grad.detach().float().clone() for n, p in m.named_parameters()}
-
-    off, on = run(impl, False), run(impl, True)
-    if impl == "x3":
-        for n in off:
-            assert torch.equal(off[n], on[n]), n
-        return
-    ref = run("x3", False)
-    e_off = sorted(rel(off[n], ref[n]) for n in ref)
-    e_on = sorted(rel(on[n], ref[n]) for n in ref)
-    med = len(ref) // 2
-    assert e_on[med] <= 1.25 * e_off[med] + 1e-3, (e_on[med], e_off[med])
-    assert e_on[-1] <= 1.5 * e_off[-1] + 1e-2, (e_on[-1], e_off[-1])
-
-
 def test_resnet_graph_replay_matches_eager():
     """bench_resnet.py --graph: a whole ResNet training step (forward, autograd backward through the
     native kernels, DDP hooks, fused SGD) captured once and replayed gives bitwise the parameters of
@@ -571,77 +534,3 @@ def test_resnet_graph_replay_matches_eager():
     assert torch.equal(out[0], out[1])
 
 
-@pytest.mark.parametrize("impl", ["x3", "bf16"])
-def test_resnet_staged_epilogue_bitwise(monkeypatch, impl):
-    """Conv epilogues staged through LDS (DPA_OB_EPI=1, DPA_STREAM_EPI=1: 16-byte row stores of bf16 / fp32
-    outputs) store exactly the values the direct 2/4-byte stores do: a ResNet step's loss and
-    every gradient are bitwise equal."""
-    from distributed_pytorch_amd.models import resnet as R
-
-    torch.manual_seed(0)
-    sd = R.ResNet([1, 2, 1, 1], 10, impl=impl).state_dict()
-    g = torch.Generator().manual_seed(12)
-    x = torch.randn(8, 64, 64, 3, generator=g).cuda()
-    t = torch.randint(0, 10, (8,), generator=g).cuda()
-    out = []
-    for epi in ("0", "1"):
-        monkeypatch.setenv("DPA_OB_EPI", epi)
-        monkeypatch.setenv("DPA_STREAM_EPI", epi)
-        m = R.ResNet([1, 2, 1, 1], 10, impl=impl)
-        m.load_state_dict(sd)
-        m = m.cuda()
-        loss = m(x, t)
-        loss.backward()
-        torch.cuda.synchronize()
-        out.append((loss.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
-    assert torch.equal(out[0][0], out[1][0])
-    for n in out[0][1]:
-        assert torch.equal(out[0][1][n], out[1][1][n]), n
-
-
-@pytest.mark.parametrize("graph", [False, True])
-def test_wgrad_side_stream_bitwise(monkeypatch, graph):
-    """Weight gradients on the side stream (functional.WGRAD_STREAM) give bitwise the gradients of
-    the one-stream backward, eager and replayed as a captured HIP graph (bench_resnet.py's step),
-    and the compute stream has joined the side stream when backward returns."""
-    from distributed_pytorch_amd.models.resnet import ResNet
-    from distributed_pytorch_amd.ops import functional as Fn
-    from distributed_pytorch_amd.parallel.ddp import DistributedDataParallel, FlatSGD
-
-    g = torch.Generator(device="cuda").manual_seed(5)
-    x = torch.randn(16, 64, 64, 3, device="cuda", generator=g)
-    t = torch.randint(0, 10, (16,), device="cuda", generator=g)
-    out = []
-    for side in (False, True):
-        monkeypatch.setattr(Fn, "WGRAD_STREAM", side)
-        torch.manual_seed(0)
-        m = ResNet([1, 1, 1, 1], 10, impl="bf16").cuda()
-        ddp = DistributedDataParallel(m)
-        opt = FlatSGD(ddp, lr=0.01, momentum=0.9)
-        one = torch.ones((), device="cuda")
-
-        def step():
-            opt.zero_grad()
-            loss = F.cross_entropy(ddp(x), t)
-            loss.backward(one)
-            opt.step(ddp.finish())
-            return loss
-
-        for _ in range(2):
-            step()
-        if graph:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                step()
-            torch.cuda.current_stream().wait_stream(s)
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                step()
-            gr.replay()
-        else:
-            step()
-        torch.cuda.synchronize()
-        out.append((ddp.flat_grads.clone(), ddp.flat_params.clone()))
-    assert torch.equal(out[0][0], out[1][0])
-    assert torch.equal(out[0][1], out[1][1])

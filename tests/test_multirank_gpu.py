@@ -119,12 +119,14 @@ def test_main_ddp_training_two_ranks(tmp_path):
     assert (ck / "rank0.pt").exists() and (ck / "rank1.pt").exists()
 
 
-@pytest.mark.parametrize("world,stage", [(2, None), (4, None), (2, 65536)])
-def test_ipc_allreduce_ranks_share_one_gpu(world, stage):
-    """the peer-memory all-reduce (HIP IPC mappings + one two-shot kernel per
-    collective) between 2 / 4 processes on one GPU: bitwise the rank-order fp32 sum, slices with
-    odd tails, nothing outside the slice touched, no wait timed out (tests/ipc_worker.py).  stage: a
-    staging buffer smaller than a collective's slice (the collective runs as several pieces)."""
+@pytest.mark.parametrize("world,stage,inbox", [(2, 0, 0), (3, 0, 0), (4, 0, 0), (8, 0, 0), (2, 65536, 40000)])
+def test_ipc_collectives_ranks_share_one_gpu(world, stage, inbox):
+    """every peer-memory collective (all-reduce sum/max/min, broadcast, gather,
+    reduce-scatter, all-gather, barrier) between 2 / 3 / 4 / 8 processes on one GPU, through the
+    registered (in place) and the bounced (inbox) input paths: bitwise the rank-order fp32 reduction
+    or the exact copy, nothing outside the target touched, no wait timed out, no tensor through the
+    host (tests/ipc_worker.py; native-store rendezvous, no torch.distributed group at all).
+    stage / inbox: buffers smaller than the collectives (every one runs as several pieces)."""
     from distributed_pytorch_amd.parallel.spawn import free_port
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
@@ -132,25 +134,91 @@ def test_ipc_allreduce_ranks_share_one_gpu(world, stage):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     if stage:
         env["DPA_IPC_TEST_STAGE"] = str(stage)
+    if inbox:
+        env["DPA_IPC_TEST_INBOX"] = str(inbox)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPA_STORE_PORT"):
         env.pop(k, None)
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert d["world"] == world and d["bitwise_ok"] and not d["timeout"] and d["ipc_ops"] >= 5, d
+    assert d["world"] == world and d["bitwise_ok"] and not d["timeout"], d
+    assert d["inner_tensor_ops"] == 0 and len(d["results"]) >= 12, d
+
+
+def _bench(args, script="bench.py", timeout=110):
+    cmd = [sys.executable, os.path.join(ROOT, script)] + args + ["--launch-timeout", str(timeout - 10)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, r.stdout[-2000:]
+    return json.loads(lines[-1])
+
+
+# the collectives each mode must have run on the peer kernels (after start-up)
+_MODE_OPS = {"ddp": {"all_reduce", "broadcast"}, "allreduce": {"all_reduce"}, "gather": {"gather", "broadcast"},
+             "zero1": {"reduce_scatter", "all_gather", "broadcast"}}
+
+
+@pytest.fixture(scope="module")
+def ipc_runs():
+    return {}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("mode", MODES)
+def test_modes_on_peer_kernels(ipc_runs, mode, world):
+    """every sync mode with EVERY collective on the peer-memory kernels (--comm
+    ipc: mode A's gather -> mean -> broadcast, DDP's bucket all-reduces and BN-buffer broadcasts,
+    ZeRO-1's reduce-scatter / all-gather, the start-up broadcast): replicas bitwise identical, and no
+    tensor byte through gloo or the host (the communicator wraps nothing)."""
+    d = _bench(["--gpus", str(world), "--comm", "ipc", "--mode", mode, "--steps", "3", "--warmup", "2",
+                "--solo-steps", "0", "--diag-steps", "1"] + (["--batch", "64"] if world > 2 else []))
+    ipc_runs[(mode, world)] = d
+    assert d["n_gpus"] == world and d["config"]["sync_mode"] == mode and d["config"]["comm"] == "ipc-standalone", d
+    assert d["replicas_identical"] is True and d["replica_param_max_diff"] == 0.0, d
+    assert d["ipc_inner_tensor_ops"] == 0, d
+    assert _MODE_OPS[mode] <= set(d["ipc_ops_by_kind"]), d["ipc_ops_by_kind"]
+
+
+def test_peer_kernel_modes_agree_bitwise(ipc_runs, runs):
+    """The reference oracle (same seed, same parameters in every mode) on the peer
+    kernels: at W=2 all four modes agree bitwise (a sum of two and its halving are exact in any
+    order), and equal the gloo (host-staged) runs of the same configuration; at W=4 the three modes that reduce in rank order and scale in the update (ddp,
+    allreduce, zero1) agree bitwise."""
+    need = [(m, 2) for m in MODES] + [(m, 4) for m in ("ddp", "allreduce", "zero1")]
+    if not all(k in ipc_runs for k in need):
+        pytest.skip("needs every mode's run")
+    w2 = {m: ipc_runs[(m, 2)]["param_checksum"] for m in MODES}
+    w2.update({f"{m}-gloo": runs[m]["param_checksum"] for m in runs})  # the host-staged runs, same config
+    assert len(set(w2.values())) == 1, w2
+    w4 = {m: ipc_runs[(m, 4)]["param_checksum"] for m in ("ddp", "allreduce", "zero1")}
+    assert len(set(w4.values())) == 1, w4
+
+
+def test_ddp_eight_ranks_share_one_gpu():
+    """W = 8 (the node size the driver's scaling run uses) of the DDP mode on the
+    peer kernels, batch 32 per rank, eight processes on one GPU."""
+    d = _bench(["--gpus", "8", "--comm", "ipc", "--mode", "ddp", "--steps", "2", "--warmup", "1", "--solo-steps", "0",
+                "--diag-steps", "0", "--batch", "32"])
+    assert d["n_gpus"] == 8 and d["replicas_identical"] is True and d["ipc_inner_tensor_ops"] == 0, d
+
+
+def test_resnet_generic_ddp_on_peer_kernels():
+    """The hook-based generic DDP (parallel/ddp.py, ResNet-50) with every collective on the peer
+    kernels, 2 ranks on one GPU: replicas bitwise identical."""
+    d = _bench(["--gpus", "2", "--comm", "ipc", "--steps", "2", "--warmup", "1", "--batch", "8", "--image", "64"],
+               script="bench_resnet.py")
+    assert d["n_gpus"] == 2 and d["replicas_identical"] is True, d
 
 
 def test_ipc_ddp_matches_gloo(runs):
-    """Bucketed DDP with the bucket all-reduces on the peer-memory kernel (--ipc on, 2 ranks on one
-    GPU): replicas identical and -- a sum of two is exact in any order -- bitwise the parameters of
-    the gloo run of the same mode."""
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc",
-           "on", "--steps", "3", "--warmup", "2", "--solo-steps", "0", "--diag-steps", "1", "--launch-timeout", "100"]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    env.pop("WORLD_SIZE", None)
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    """Bucketed DDP with the collectives on the peer-memory kernels wrapped around the gloo
+    communicator (--ipc on, 2 ranks on one GPU): replicas identical and -- a sum of two is exact in
+    any order -- bitwise the parameters of the gloo run of the same mode."""
+    d = _bench(["--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc", "on", "--steps", "3", "--warmup", "2",
+                "--solo-steps", "0", "--diag-steps", "1"])
     assert d["replicas_identical"] is True and d["ipc_allreduce_ops"] and d["ipc_allreduce_ops"] > 0, d
     if "ddp" in runs:
         assert d["param_checksum"] == runs["ddp"]["param_checksum"], (d["param_checksum"], runs["ddp"]["param_checksum"])

@@ -493,40 +493,6 @@ def test_wgrad_stream_matches_single_stream(monkeypatch, impl):
     assert torch.equal(outs[0], outs[2])
 
 
-@pytest.mark.parametrize("stream", ["0", "1"])
-def test_wgrad_fixup_engine(monkeypatch, stream):
-    """Weight gradients whose split-K slabs are summed inside the conv kernel (DPA_WGRAD_FIXUP_MAX,
-    conv_x3.hip splitk_fixup) train to the same parameters as the separate reduce kernel (up to
-    the summation order) and bitwise reproducibly run to run, on one or two streams."""
-    from distributed_pytorch_amd.engine import VGGEngine
-
-    g = torch.Generator().manual_seed(9)
-    xs = [torch.randn(128, 32, 32, 4, generator=g) for _ in range(3)]
-    ts = [torch.randint(0, 10, (128,), generator=g) for _ in range(3)]
-    monkeypatch.setenv("DPA_WGRAD_STREAM", stream)
-    outs = []
-    for fx in ("0", "64", "64"):
-        monkeypatch.setenv("DPA_WGRAD_FIXUP_MAX", fx)
-        e = VGGEngine("VGG11", "cuda", max_batch=128, impl="x3", lr=0.01)
-        e.init_parameters(seed=3)
-        for x, t in zip(xs, ts):
-            x = x.cuda()
-            x[..., 3] = 0
-            e.forward_backward(x, t.cuda())
-            e.sgd_step()
-            e.finish_step()
-        torch.cuda.synchronize()
-        e.check_signals()
-        if fx != "0":
-            assert any(e.conv_config(i, "wgrad", 128)[1] > 1 for i in range(1, len(e.spec.convs)))
-            fix = e.wfix_side if stream == "1" else e.wfix_main
-            assert int(fix.abs().sum()) == 0
-        outs.append(e.params.flat.clone())
-    assert torch.equal(outs[1], outs[2])
-    d = (outs[1] - outs[0]).norm().item()
-    assert d <= 1e-5 * outs[0].norm().item(), d
-
-
 @pytest.mark.parametrize("impl", ["x3", "bf16"])
 def test_graphed_step_matches_eager(impl):
     """The captured HIP-graph step (both streams, fused SGD) replays to bit-identical parameters,
