@@ -63,9 +63,11 @@ def parse(argv=None):
                          "eager fallback).  Off by default: same throughput on MI355X (host enqueue 0.67 -> 0.27 "
                          "ms hides behind 1.7 ms of GPU work) and the graph executor reorders the two-stream "
                          "backward")
-    ap.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
-                    help="conv kernels: x3 = fp32-grade results from bf16 matrix cores (3 bf16 planes per "
-                         "operand, 6 plane products; default) | fp32 = fp32 MFMA | bf16 = mixed precision")
+    ap.add_argument("--impl", default="h2", choices=["fp32", "x3", "h2", "bf16"],
+                    help="conv kernels: h2 = fp32-grade results from fp16 matrix cores (fp16 pairs of scaled "
+                         "operands, 3 products; default) | x3 = fp32-grade from bf16 matrix cores (3 planes, "
+                         "6 products) | fp32 = fp32 MFMA | bf16 = mixed precision.  h2 and x3 are pinned "
+                         "against fp64 at this exact config by tests/test_parity256_gpu.py")
     ap.add_argument("--solo-steps", type=int, default=None,
                     help="N>1: steps rank 0 times alone first (same-run 1-GPU figure; 0 = skip; default "
                          "min(steps, 30))")

@@ -34,7 +34,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val,
-               const void* g2, const unsigned char* mask);
+               const void* g2, const unsigned char* mask, unsigned* bound);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -60,7 +60,8 @@ int dpa_fc_ce_eval(const float* x, const float* w, const float* b, const long lo
 int dpa_x3_splits(int Kred, int splits);
 int dpa_conv_x3_fprop(const unsigned short* x, long xps, const unsigned short* w, long wps, void* out, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
-                      int reduce, int posmajor, int np, int obf, hipStream_t st, float* stats);
+                      int reduce, int posmajor, int np, int obf, hipStream_t st, float* stats, float oscale,
+                      const unsigned* obound);
 int dpa_conv_stats_rows(int tile);
 long dpa_ipc_slice(long n, int world);
 int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const float* gamma, const float* beta,
@@ -68,13 +69,17 @@ int dpa_bn_finalize_cm(const float* part, int nblk, int rpb, int M, int C, const
                        float* scale, float* shift, float momentum, float eps, hipStream_t st);
 int dpa_conv_x3_wgrad(const unsigned short* x, long xps, const unsigned short* dz, long dzps, float* dw, float* slab,
                       int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad, int splits, int tile,
-                      int posmajor, int np, hipStream_t st);
-int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, hipStream_t st);
+                      int posmajor, int np, hipStream_t st, float oscale, const unsigned* obound);
+int dpa_split_planes(const float* x, unsigned short* out, long n, long ps, int np, float scale, hipStream_t st);
+int dpa_h2_ovf_conv(int clear);
+int dpa_h2_ovf_bn(int clear);
+int dpa_h2_ovf_sgd(int clear);
+int dpa_h2_ovf_fused(int clear);
 int dpa_pad_split8(const float* x, unsigned short* out, long npix, int cin, long ps, int np, hipStream_t st);
 int dpa_conv_x3_dgrad(const unsigned short* dz, long dzps, const unsigned short* w, long wps, void* dx, float* slab,
                       int N, int Hd, int Wd, int K, int C, int R, int S, int stride, int pad, int H, int W, int splits,
                       int tile, int reduce, int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig,
-                      int sig_val);
+                      int sig_val, float oscale, const unsigned* obound);
 int dpa_wait_signal(const int* sig, int val, long long timeout_us, int* tmo, hipStream_t st);
 int dpa_bn_fused_geo(int Mo, int C, int pool, int bwd, int rmax, long* part_floats, long* cnt_words, int* blocks);
 int dpa_bn_fused_fwd(const float* src, int nsplit, float* zw, int N, int H, int W, int C, int pool, int rmax,
@@ -165,12 +170,13 @@ void sgd_flat(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double
   int np = 0;
   if (planes.has_value() && planes->defined()) {
     const Tensor& t = *planes;
-    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 &&
-                    (t.size(0) == 1 || t.size(0) == 3) && t.size(1) == p.numel(),
-                "sgd_flat: planes must be contiguous bfloat16 [NP, p.numel()]");
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 2 && t.size(1) == p.numel() &&
+                    ((t.scalar_type() == at::kBFloat16 && (t.size(0) == 1 || t.size(0) == 3)) ||
+                     (t.scalar_type() == at::kHalf && t.size(0) == 2)),
+                "sgd_flat: planes must be contiguous bfloat16 [1 or 3, p.numel()] or float16 [2, p.numel()]");
     np = t.size(0);
     ps = t.stride(0);
-    pl = reinterpret_cast<unsigned short*>(t.data_ptr<at::BFloat16>()) + offset;
+    pl = reinterpret_cast<unsigned short*>(t.data_ptr()) + offset;
   }
   chk(dpa_sgd_flat(fp(p) + offset, fp(g) + offset, fp(buf) + offset, count, (float)lr, (float)momentum, (float)wd,
                    (float)gscale, first ? 1 : 0, pl, ps, np, cur_stream()),
@@ -293,14 +299,27 @@ void wflip(Tensor w, Tensor wd) {
 // ---------------- bf16-plane (fp32 via bf16x6, or plain bf16) convolution ----------------
 // Plane tensors are bfloat16 [NP, ...] (NP = 1 or 3), contiguous.
 using u16 = unsigned short;
-u16* up(const Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr<at::BFloat16>()); }
+u16* up(const Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr()); }
+
+// operand planes: bfloat16 [1 or 3, ...] (bf16 / bf16-triple operands) or float16 [2, ...] (fp16
+// pairs, impl "h2"); plane_count of a tensor that is one of them
+bool is_plane_dtype(const Tensor& t) { return t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf; }
+
+// a data-gradient bound word (int32 [>= 1], written by bn_bwd) or nullptr
+const unsigned* bound_ptr(const OptT& b, const char* what) {
+  if (!b.has_value() || !b->defined()) return nullptr;
+  TORCH_CHECK(b->is_cuda() && b->scalar_type() == torch::kInt32 && b->numel() >= 1, what,
+              ": bound must be an int32 GPU tensor");
+  return reinterpret_cast<const unsigned*>(b->data_ptr<int32_t>());
+}
 
 // Each plane must be contiguous and 16-byte aligned; planes may be strided views of a larger
 // buffer (e.g. the engine's weight-plane arena) as long as the plane stride keeps that alignment.
 void need_planes(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16 planes");
-  TORCH_CHECK(t.size(0) == 1 || t.size(0) == 3, name, " must have 1 or 3 planes in dim 0");
+  TORCH_CHECK(is_plane_dtype(t), name, " must be bfloat16 or float16 planes");
+  TORCH_CHECK(t.scalar_type() == at::kHalf ? t.size(0) == 2 : (t.size(0) == 1 || t.size(0) == 3), name,
+              ": bfloat16 planes come in 1 or 3, float16 pairs in 2 (dim 0)");
   TORCH_CHECK(t.select(0, 0).is_contiguous(), name, ": each plane must be contiguous");
   TORCH_CHECK(t.size(0) == 1 || t.stride(0) % 8 == 0, name, ": plane stride must be a multiple of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, ": planes must be 16-byte aligned");
@@ -322,8 +341,10 @@ void* conv_out_ptr(const Tensor& out, int np, const char* name, int& obf) {
 }
 
 // x3 [NP,N,H,W,C], w3 [NP,K,R,S,C], out [N,P,Q,K] fp32 (or bf16 when NP == 1)
+// np 2 (float16 pairs): the output is multiplied by oscale (1 / (s_x s_w)) and, with obound, by
+// 1 / the scale of that data-gradient bound word
 void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, int64_t posmajor, OptT stats) {
+                   int64_t tile, bool reduce, int64_t posmajor, OptT stats, double oscale, OptT obound) {
   need_planes(x3, "x3");
   need_planes(w3, "w3");
   const int np = x3.size(0);
@@ -352,7 +373,8 @@ void conv_x3_fprop(Tensor x3, Tensor w3, Tensor out, OptT slab, int64_t stride, 
     stp = fp(*stats);
   }
   chk(dpa_conv_x3_fprop(up(x3), x3.stride(0), up(w3), w3.stride(0), op, sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf, cur_stream(), stp),
+                        (int)pad, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf, cur_stream(), stp,
+                        (float)oscale, bound_ptr(obound, "conv_x3_fprop")),
       "conv_x3_fprop");
 }
 
@@ -377,7 +399,7 @@ void bn_finalize(Tensor part, int64_t nblk, int64_t rpb, int64_t M, Tensor gamma
 
 // x3 [NP,N,H,W,C], dz3 [NP,N,P,Q,K], dw [K,R,S,C] fp32
 void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, int64_t posmajor) {
+                   int64_t tile, int64_t posmajor, double oscale, OptT obound) {
   need_planes(x3, "x3");
   need_planes(dz3, "dz3");
   need(dw, "dw");
@@ -397,14 +419,16 @@ void conv_x3_wgrad(Tensor x3, Tensor dz3, Tensor dw, OptT slab, int64_t stride, 
     sl = fp(*slab);
   }
   chk(dpa_conv_x3_wgrad(up(x3), x3.stride(0), up(dz3), dz3.stride(0), fp(dw), sl, N, H, W, C, K, R, S, (int)stride,
-                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream()),
+                        (int)pad, (int)splits, (int)tile, (int)posmajor, np, cur_stream(), (float)oscale,
+                        bound_ptr(obound, "conv_x3_wgrad")),
       "conv_x3_wgrad");
 }
 
 // dz3 [NP,N,Hd,Wd,K], w3 [NP,K,R,S,C] (forward weight planes), dx [N,H,W,C] fp32: data gradient of
 // conv(x, w, stride, pad); stride a power of two.
 void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, int64_t pad, int64_t splits,
-                   int64_t tile, bool reduce, int64_t posmajor, OptT add, OptT sig, int64_t sig_val) {
+                   int64_t tile, bool reduce, int64_t posmajor, OptT add, OptT sig, int64_t sig_val, double oscale,
+                   OptT obound) {
   need_planes(dz3, "dz3");
   need_planes(w3, "w3");
   const int np = dz3.size(0);
@@ -436,7 +460,7 @@ void conv_x3_dgrad(Tensor dz3, Tensor w3, Tensor dx, OptT slab, int64_t stride, 
   int* sp = opt_signal(sig, "conv_x3_dgrad");
   chk(dpa_conv_x3_dgrad(up(dz3), dz3.stride(0), up(w3), w3.stride(0), op, sl, N, Hd, Wd, K, C, R, S, (int)stride,
                         (int)pad, H, W, (int)splits, (int)tile, reduce ? 1 : 0, (int)posmajor, np, obf,
-                        cur_stream(), ap, sp, (int)sig_val),
+                        cur_stream(), ap, sp, (int)sig_val, (float)oscale, bound_ptr(obound, "conv_x3_dgrad")),
       "conv_x3_dgrad");
 }
 
@@ -450,12 +474,25 @@ void pad_split8(Tensor x, Tensor out) {
   chk(dpa_pad_split8(fp(x), up(out), npix, x.size(-1), out.stride(0), out.size(0), cur_stream()), "pad_split8");
 }
 
-// x fp32 (any shape) -> out [NP, *x.shape] bf16 planes
-void split_planes(Tensor x, Tensor out) {
+// x fp32 (any shape) -> out [NP, *x.shape] bf16 planes, or float16 pairs of x * scale
+void split_planes(Tensor x, Tensor out, double scale) {
   need(x, "x");
   need_planes(out, "out");
   TORCH_CHECK(out.numel() == out.size(0) * x.numel(), "split_planes: out must be [NP, *x.shape]");
-  chk(dpa_split_planes(fp(x), up(out), x.numel(), out.stride(0), out.size(0), cur_stream()), "split_planes");
+  chk(dpa_split_planes(fp(x), up(out), x.numel(), out.stride(0), out.size(0), (float)scale, cur_stream()),
+      "split_planes");
+}
+
+// the fp16-pair overflow words of every kernel file (a split saw |x s| beyond float16's range);
+// clear: reset them
+bool h2_overflow(bool clear) {
+  int any = 0;
+  for (int (*f)(int) : {dpa_h2_ovf_conv, dpa_h2_ovf_bn, dpa_h2_ovf_sgd, dpa_h2_ovf_fused}) {
+    const int v = f(clear ? 1 : 0);
+    TORCH_CHECK(v >= 0, "h2_overflow: could not read an overflow word");
+    any |= v;
+  }
+  return any != 0;
 }
 
 
@@ -545,9 +582,9 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t
   }
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
   const int64_t outn = (int64_t)N * (pool ? (H / 2) * (W / 2) : H * W) * C;
-  if (a.scalar_type() == at::kBFloat16) {
+  if (is_plane_dtype(a)) {
     int np = 1;
-    if (a.numel() != outn) {
+    if (a.numel() != outn || a.scalar_type() == at::kHalf) {
       need_planes(a, "a3");
       TORCH_CHECK(a.numel() == a.size(0) * outn, "bn_apply: a3 shape");
       np = a.size(0);
@@ -698,7 +735,7 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask, OptT bound) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
@@ -720,8 +757,8 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   float* dzf = nullptr;
   u16* dz3 = nullptr;
   int np = 0;
-  if (dz.scalar_type() == at::kBFloat16) {
-    if (dz.numel() == z.numel()) {  // one plane, [N,H,W,C]
+  if (is_plane_dtype(dz)) {
+    if (dz.numel() == z.numel() && dz.scalar_type() == at::kBFloat16) {  // one plane, [N,H,W,C]
       TORCH_CHECK(dz.is_cuda() && dz.is_contiguous(), "bn_bwd: dz must be contiguous");
       np = 1;
     } else {
@@ -748,7 +785,8 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   }
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
-                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp),
+                 bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp,
+                 const_cast<unsigned*>(bound_ptr(bound, "bn_bwd"))),
       "bn_bwd");
 }
 
@@ -772,8 +810,8 @@ OutPtrs out_ptrs(const OptT& out, int64_t n, const char* what) {
   OutPtrs o;
   if (!out.has_value() || !out->defined()) return o;
   const Tensor& t = *out;
-  if (t.scalar_type() == at::kBFloat16) {
-    if (t.numel() == n) {
+  if (is_plane_dtype(t)) {
+    if (t.numel() == n && t.scalar_type() == at::kBFloat16) {
       TORCH_CHECK(t.is_cuda() && t.is_contiguous(), what, ": out must be contiguous");
       o.np = 1;
     } else {
@@ -1136,18 +1174,23 @@ PYBIND11_MODULE(_C, m) {
   m.def("x3_splits", &x3_splits);
   m.def("conv_x3_fprop", &conv_x3_fprop, py::arg("x3"), py::arg("w3"), py::arg("out"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
-        py::arg("posmajor") = 0, py::arg("stats") = py::none());
+        py::arg("posmajor") = 0, py::arg("stats") = py::none(), py::arg("oscale") = 1.0,
+        py::arg("obound") = py::none());
   m.def("conv_stats_rows", [](int64_t tile) { return (int64_t)dpa_conv_stats_rows((int)tile); });
   m.def("bn_finalize", &bn_finalize);
   m.def("conv_x3_wgrad", &conv_x3_wgrad, py::arg("x3"), py::arg("dz3"), py::arg("dw"), py::arg("slab"),
-        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0);
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("posmajor") = 0,
+        py::arg("oscale") = 1.0, py::arg("obound") = py::none());
   m.def("conv_x3_dgrad", &conv_x3_dgrad, py::arg("dz3"), py::arg("w3"), py::arg("dx"), py::arg("slab"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 1, py::arg("tile") = 0, py::arg("reduce") = true,
         py::arg("posmajor") = 0, py::arg("add") = py::none(), py::arg("sig") = py::none(),
-        py::arg("sig_val") = 0);
+        py::arg("sig_val") = 0, py::arg("oscale") = 1.0, py::arg("obound") = py::none());
   m.def("wait_signal", &wait_signal, py::arg("sig"), py::arg("val"), py::arg("timeout_us"), py::arg("tmo"));
   m.def("set_signal", &set_signal, py::arg("sig"), py::arg("val"));
-  m.def("split_planes", &split_planes);
+  m.def("split_planes", &split_planes, py::arg("x"), py::arg("out"), py::arg("scale") = 1.0);
+  m.def("h2_overflow", &h2_overflow, py::arg("clear") = false);
+  m.attr("H2_SW") = 256.0;  // fp16-pair plane scales (kernels/common.h)
+  m.attr("H2_SA") = 16.0;
   m.def("pad_split8", &pad_split8);
   m.def("bn_part_floats", &bn_part_floats);
   m.def("bn_fwd_stats", &bn_fwd_stats);
@@ -1160,7 +1203,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
-        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none());
+        py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none(),
+        py::arg("bound") = py::none());
   m.def("bn_fused_geo", &bn_fused_geo, py::arg("Mo"), py::arg("C"), py::arg("pool"), py::arg("bwd"),
         py::arg("rmax"));
   m.def("bn_fused_fwd", &bn_fused_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),

@@ -125,33 +125,44 @@ __device__ __forceinline__ void tree_rows(float4 (*sh)[T], int t, int lane_r, in
   }
 }
 
+// as tree_rows, maxima instead of sums
+template <int T = RT>
+__device__ __forceinline__ void tree_rows_max(float4 (*sh)[T], int t, int lane_r, int TPR, int RPI) {
+  int p2 = 1;
+  while (p2 < RPI) p2 <<= 1;
+  for (int o = p2 >> 1; o >= 1; o >>= 1) {
+    if (lane_r < o && lane_r + o < RPI) {
+      const float4 a = sh[0][t], b = sh[0][t + o * TPR];
+      sh[0][t] = make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
+    }
+    __syncthreads();
+  }
+}
+
 #define F4GET(v, k) ((k) == 0 ? (v).x : (k) == 1 ? (v).y : (k) == 2 ? (v).z : (v).w)
 
 
-// ---- output writer: NP == 0 -> fp32 float4 store; NP in {1,3} -> bf16 planes x = x0 (+ x1 + x2)
-// (round-to-nearest-even splits, conv_x3.hip header) so the next conv reads MFMA-ready operands.
+// ---- output writer: NP == 0 -> fp32 float4 store; NP in {1,3} -> bf16 planes x = x0 (+ x1 + x2);
+// NP 2 -> the fp16 pair of x * s (common.h split_val) -- the next conv reads MFMA-ready operands.
 
 template <int NP>
-__device__ __forceinline__ void store4(float* f, u16* pl, long ps, long i4, float4 v) {
+__device__ __forceinline__ void store4(float* f, u16* pl, long ps, long i4, float4 v, float s = 1.f) {
   if constexpr (NP == 0) {
     reinterpret_cast<float4*>(f)[i4] = v;
   } else {
     const float vv[4] = {v.x, v.y, v.z, v.w};
-    u16 o[3][4];
+    u16 o[4][3];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u16 h0 = bf16_rne(vv[k]);
-      o[0][k] = h0;
-      if (NP == 3) {
-        const float r1 = vv[k] - bf16_f(h0);
-        const u16 h1 = bf16_rne(r1);
-        o[1][k] = h1;
-        o[2][k] = bf16_rne(r1 - bf16_f(h1));
-      }
-    }
+    for (int k = 0; k < 4; ++k) split_val<NP>(vv[k], o[k], s);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) reinterpret_cast<ushort4*>(pl + p * ps)[i4] = make_ushort4(o[p][0], o[p][1], o[p][2], o[p][3]);
+    for (int p = 0; p < NP; ++p)
+      reinterpret_cast<ushort4*>(pl + p * ps)[i4] = make_ushort4(o[0][p], o[1][p], o[2][p], o[3][p]);
   }
+}
+// activation planes: the fixed scale of fp16 pairs
+template <int NP>
+__device__ __forceinline__ void store4a(float* f, u16* pl, long ps, long i4, float4 v) {
+  store4<NP>(f, pl, ps, i4, v, NP == 2 ? H2_SA : 1.f);
 }
 
 // ---- forward statistics: per (row-block, channel) (mean, M2) via sums shifted by the block's
@@ -383,7 +394,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
   auto body = [&](long i, int c4, float4 sc, float4 sh) {
     if (!POOL) {
       if constexpr (ACT == 0) {
-        store4<NP>(a, a3, ps, i, affine_relu(ld4(z, i), sc, sh));
+        store4a<NP>(a, a3, ps, i, affine_relu(ld4(z, i), sc, sh));
       } else {
         const float4 v = ld4(z, i);
         float4 u = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
             mask[i] = (unsigned char)((t.x > 0.f) | ((t.y > 0.f) << 1) | ((t.z > 0.f) << 2) | ((t.w > 0.f) << 3));
           u = make_float4(fmaxf(t.x, 0.f), fmaxf(t.y, 0.f), fmaxf(t.z, 0.f), fmaxf(t.w, 0.f));
         }
-        store4<NP>(a, a3, ps, i, u);
+        store4a<NP>(a, a3, ps, i, u);
       }
     } else {
       const unsigned t = (unsigned)(i / C4);  // pooled pixel (VGG sizes: < 2^32)
@@ -406,11 +417,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TZ* __restrict__ z,
       const float4 v01 = affine_relu(ld4(z, base + C4), sc, sh);
       const float4 v10 = affine_relu(ld4(z, base + (long)W * C4), sc, sh);
       const float4 v11 = affine_relu(ld4(z, base + (long)W * C4 + C4), sc, sh);
-      store4<NP>(a, a3, ps, i,
-                 make_float4(fmaxf(fmaxf(v00.x, v01.x), fmaxf(v10.x, v11.x)),
-                             fmaxf(fmaxf(v00.y, v01.y), fmaxf(v10.y, v11.y)),
-                             fmaxf(fmaxf(v00.z, v01.z), fmaxf(v10.z, v11.z)),
-                             fmaxf(fmaxf(v00.w, v01.w), fmaxf(v10.w, v11.w))));
+      store4a<NP>(a, a3, ps, i,
+                  make_float4(fmaxf(fmaxf(v00.x, v01.x), fmaxf(v10.x, v11.x)),
+                              fmaxf(fmaxf(v00.y, v01.y), fmaxf(v10.y, v11.y)),
+                              fmaxf(fmaxf(v00.z, v01.z), fmaxf(v10.z, v11.z)),
+                              fmaxf(fmaxf(v00.w, v01.w), fmaxf(v10.w, v11.w))));
     }
   };
   const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -460,8 +471,9 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
   d11 = (arg == 3 && y11 > 0.f) ? g : 0.f;
 }
 
-// Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat.  Rows are OUTPUT rows of
-// the layer (pooled positions when POOL).  If nsplit > 1, gsrc holds the split-K slabs of g and
+// Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat and maxima of |dy|, |z| (the
+// data-gradient bound of fp16-pair planes, bn_bwd_finalize_kernel).  Rows are OUTPUT rows of
+// the layer (pooled positions when POOL).  part: [block][5][C].  If nsplit > 1, gsrc holds the split-K slabs of g and
 // the summed g is written to gout (consumed by the apply pass).  g2 (optional, nsplit == 1): a second
 // contribution to the same gradient, summed on load here and in the apply pass instead of by a
 // separate add pass (ResNet: a block input's two gradient contributions, ops/functional.GradJoin).
@@ -481,8 +493,10 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             int rpb, int* sig, int sig_val,
                                                             const TZ* __restrict__ g2,
                                                             const unsigned char* __restrict__ mask,
-                                                            TZ* __restrict__ dyout) {
+                                                            TZ* __restrict__ dyout, unsigned* __restrict__ bound) {
   start_signal(sig, sig_val);
+  if (bound != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *bound = 0u;  // re-armed for this layer's
+                                                                               // finalize (the next kernel)
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
   const int lane_c = t % gg.TPR, lane_r = t / gg.TPR;
@@ -497,6 +511,7 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
     const int c4 = lane_c + cg * gg.TPR;
     const bool cval = active && c4 < gg.C4;
     float sdy[4] = {0, 0, 0, 0}, sdx[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
+    float mdy[4] = {0, 0, 0, 0}, mz[4] = {0, 0, 0, 0};  // max |dy|, max |z|
     if (cval) {
       const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
       const float4 sh = reinterpret_cast<const float4*>(shift)[c4];
@@ -535,6 +550,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
               sdy[k] += dy;
               sdx[k] = fmaf(dy, xh, sdx[k]);
               sx[k] += xh;
+              mdy[k] = fmaxf(mdy[k], fabsf(dy));
+              mz[k] = fmaxf(mz[k], fabsf(zz));
               dyu[k] = dy;
             }
             if (ACT == 2 && dyout) st4(dyout, gi[u], make_float4(dyu[0], dyu[1], dyu[2], dyu[3]));
@@ -566,6 +583,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             sdy[k] += dy;
             sdx[k] = fmaf(dy, xh, sdx[k]);
             sx[k] += xh;
+            mdy[k] = fmaxf(mdy[k], fabsf(dy));
+            mz[k] = fmaxf(mz[k], fabsf(zz));
             dyv[k] = dy;
           }
           if (ACT == 2 && dyout) st4(dyout, gi, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
@@ -588,18 +607,25 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             sdy[k] += (d00 + d01) + (d10 + d11);
             sdx[k] += (d00 * x00 + d01 * x01) + (d10 * x10 + d11 * x11);
             sx[k] += (x00 + x01) + (x10 + x11);
+            mdy[k] = fmaxf(mdy[k], fmaxf(fmaxf(fabsf(d00), fabsf(d01)), fmaxf(fabsf(d10), fabsf(d11))));
+            mz[k] = fmaxf(mz[k], fmaxf(fmaxf(fabsf(F4GET(z00, k)), fabsf(F4GET(z01, k))),
+                                       fmaxf(fabsf(F4GET(z10, k)), fabsf(F4GET(z11, k)))));
           }
         }
       }
     }
-    const float4 vals[3] = {make_float4(sdy[0], sdy[1], sdy[2], sdy[3]), make_float4(sdx[0], sdx[1], sdx[2], sdx[3]),
-                            make_float4(sx[0], sx[1], sx[2], sx[3])};
-    float* o = part + (long)blockIdx.x * 3 * C + c4 * 4;
+    const float4 vals[5] = {make_float4(sdy[0], sdy[1], sdy[2], sdy[3]), make_float4(sdx[0], sdx[1], sdx[2], sdx[3]),
+                            make_float4(sx[0], sx[1], sx[2], sx[3]), make_float4(mdy[0], mdy[1], mdy[2], mdy[3]),
+                            make_float4(mz[0], mz[1], mz[2], mz[3])};
+    float* o = part + (long)blockIdx.x * 5 * C + c4 * 4;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < 5; ++q) {
       sh[0][t] = vals[q];
       __syncthreads();
-      tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
+      if (q < 3)
+        tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
+      else
+        tree_rows_max<RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
       if (cval && lane_r == 0) *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
       __syncthreads();
     }
@@ -608,19 +634,25 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
 
 // Per channel: sum the block partials (fixed order -> deterministic), emit dgamma, dbeta, dbias and
 // the dz coefficients: dz = k1*dy + k2*z + k3.   8 channels x 32 groups per block.
+// Q: rows per block partial (5: with the maxima of |dy| and |z|, bn_bwd_reduce_kernel; 3: bn_wide.hip's
+// reduce).  bound (Q 5, optional): |dz| <= |k1| max|dy| + |k2| max|z| + |k3| per channel, maximised over
+// the channels into the word (an fp32 bit pattern; non-negative floats order like their bits), the
+// scale of the fp16-pair dz planes and of the convs that read them.
 // Backward finalize: BF_CPB channels per 256-thread block, 256/BF_CPB partial rows of each in
 // flight (a thread's loads are issued 16 rows at a time), fixed-order LDS tree.
-template <int BF_CPB>
+template <int BF_CPB, int Q>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                               float Mfull, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                              float* __restrict__ dbias, float* __restrict__ coef) {
+                                                              float* __restrict__ dbias, float* __restrict__ coef,
+                                                              unsigned* __restrict__ bound) {
   constexpr int G = 256 / BF_CPB;  // partial-row groups per channel
   const int cl = threadIdx.x % BF_CPB, grp = threadIdx.x / BF_CPB;
   const int c = blockIdx.x * BF_CPB + cl;
-  float a = 0.f, b = 0.f, x = 0.f;
+  const bool mx = Q == 5 && bound != nullptr;
+  float a = 0.f, b = 0.f, x = 0.f, mdy = 0.f, mz = 0.f;
   if (c < C) {
     // 16 partial rows per thread in flight (one memory latency for the engine's 512-row partials
     // instead of two); out-of-range rows add +0.f (exact: the sums start at +0), same order
@@ -629,10 +661,14 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const bool v = k + G * u < nblk;
-        const float* p = part + (long)(v ? k + G * u : 0) * 3 * C + c;
+        const float* p = part + (long)(v ? k + G * u : 0) * Q * C + c;
         pa[u] = v ? p[0] : 0.f;
         pb[u] = v ? p[C] : 0.f;
         px[u] = v ? p[2 * C] : 0.f;
+        if (Q == 5 && mx && v) {
+          mdy = fmaxf(mdy, p[3 * C]);
+          mz = fmaxf(mz, p[4 * C]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -642,31 +678,52 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
       }
     }
   }
-  __shared__ float sh[3][256];
+  __shared__ float sh[5][256];
   sh[0][threadIdx.x] = a;
   sh[1][threadIdx.x] = b;
   sh[2][threadIdx.x] = x;
+  sh[3][threadIdx.x] = mdy;
+  sh[4][threadIdx.x] = mz;
   __syncthreads();
   for (int o = 128; o >= BF_CPB; o >>= 1) {
     if ((int)threadIdx.x < o) {
       sh[0][threadIdx.x] += sh[0][threadIdx.x + o];
       sh[1][threadIdx.x] += sh[1][threadIdx.x + o];
       sh[2][threadIdx.x] += sh[2][threadIdx.x + o];
+      if (mx) {
+        sh[3][threadIdx.x] = fmaxf(sh[3][threadIdx.x], sh[3][threadIdx.x + o]);
+        sh[4][threadIdx.x] = fmaxf(sh[4][threadIdx.x], sh[4][threadIdx.x + o]);
+      }
     }
     __syncthreads();
   }
+  float B = 0.f;
   if (grp == 0 && c < C) {
     const float sdy = sh[0][cl], sdx = sh[1][cl], sx = sh[2][cl];
     const float iv = invstd[c], gm = gamma[c];
     const float k1 = gm * iv;
     const float k2x = -k1 * sdx / Mfull;  // coefficient of xhat
     const float k3 = -k1 * sdy / Mfull;
+    const float c2 = k2x * iv, c3 = k3 - k2x * iv * mean[c];
     dgamma[c] = sdx;
     dbeta[c] = sdy;
     if (dbias) dbias[c] = k2x * sx;  // = sum over rows of dz (analytically 0)
     coef[c] = k1;
-    coef[C + c] = k2x * iv;                     // coefficient of z
-    coef[2 * C + c] = k3 - k2x * iv * mean[c];  // constant
+    coef[C + c] = c2;      // coefficient of z
+    coef[2 * C + c] = c3;  // constant
+    // (rounding of the fma chain stays far inside the 2^14 -> 65504 headroom of the scale)
+    if (mx) B = fabsf(k1) * sh[3][cl] + fabsf(c2) * sh[4][cl] + fabsf(c3);
+  }
+  if (mx) {  // the block's channels' largest bound, one atomic per block
+    __syncthreads();
+    if (grp == 0) sh[0][cl] = B;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = 0.f;
+      for (int q = 0; q < BF_CPB; ++q) m = fmaxf(m, sh[0][q]);
+      if (!(m < 3.0e38f)) m = 3.0e38f;  // inf / NaN gradients: the largest finite bound (scale 2^-114)
+      atomicMax(bound, __float_as_uint(m));
+    }
   }
 }
 
@@ -678,11 +735,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
                                                            u16* __restrict__ dz3, long ps,
                                                            const TZ* __restrict__ res, TZ* __restrict__ dres,
                                                            int N, int H, int W, int C, const TZ* __restrict__ g2,
-                                                           const unsigned char* __restrict__ mask) {
+                                                           const unsigned char* __restrict__ mask,
+                                                           const unsigned* __restrict__ bound) {
   const int C4 = C >> 2;
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const long total = (long)N * Ho * Wo * C4;
   const long stride = (long)gridDim.x * blockDim.x;
+  // fp16-pair planes (NP 2): the scale of the bound the finalize wrote
+  const float dsc = NP == 2 ? h2_scale_of_bound(__uint_as_float(*bound)) : 1.f;
   struct Co {
     float4 sc, sh, k1, k2, k3;
   };
@@ -710,7 +770,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
         // bitwise the ACT 2 one it replaces)
         r[k] = fmaf(F4GET(q.k1, k), dy, fmaf(F4GET(q.k2, k), zz, F4GET(q.k3, k)));
       }
-      store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]));
+      store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]), dsc);
       if constexpr (ACT == 2) st4(dres, i, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
     } else {
       const unsigned t = (unsigned)(i / C4);  // pooled pixel (VGG sizes: < 2^32)
@@ -733,7 +793,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        store4<NP>(dz, dz3, ps, idx[u], make_float4(out[u][0], out[u][1], out[u][2], out[u][3]));
+        store4<NP>(dz, dz3, ps, idx[u], make_float4(out[u][0], out[u][1], out[u][2], out[u][3]), dsc);
     }
   };
   const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -817,6 +877,16 @@ int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, co
   const long total = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   const long ps = total * 4;
   const int grid = grid_ch(total, C / 4);
+  if (np == 2) {  // fp16-pair activation planes (the fp32 VGG engine: fp32 z, ReLU)
+    if constexpr (sizeof(TZ) == 4) {
+      if (act != 0) return -2;
+      if (pool) bn_apply_launch<true, 2, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
+      else bn_apply_launch<false, 2, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
+      return (int)hipGetLastError();
+    } else {
+      return -2;
+    }
+  }
   if (pool) {
     if (np == 0) bn_apply_launch<true, 0, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
     else if (np == 1) bn_apply_launch<true, 1, TZ>(act, grid, st, z, a, a3, ps, scale, shift, res, N, H, W, C, mask);
@@ -832,20 +902,21 @@ int bn_apply_host(const TZ* z, float* a, u16* a3, int np, const float* scale, co
 template <bool POOL, int NP, typename TZ>
 void bn_bwd_apply_launch(int act, int grid, hipStream_t st, const TZ* g, const TZ* z, const float* scale,
                          const float* shift, const float* coef, float* dz, u16* dz3, long ps, const TZ* res, TZ* dres,
-                         int N, int H, int W, int C, const TZ* g2, const unsigned char* mask) {
+                         int N, int H, int W, int C, const TZ* g2, const unsigned char* mask,
+                         const unsigned* bound = nullptr) {
   if constexpr (POOL) {
     bn_bwd_apply_kernel<true, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H,
-                                                                W, C, g2, mask);
+                                                                W, C, g2, mask, bound);
   } else {
     if (act == 0)
       bn_bwd_apply_kernel<false, NP, 0, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C, g2, mask);
+                                                                   H, W, C, g2, mask, bound);
     else if (act == 1)
       bn_bwd_apply_kernel<false, NP, 1, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C, g2, mask);
+                                                                   H, W, C, g2, mask, bound);
     else
       bn_bwd_apply_kernel<false, NP, 2, TZ><<<grid, 256, 0, st>>>(g, z, scale, shift, coef, dz, dz3, ps, res, dres, N,
-                                                                   H, W, C, g2, mask);
+                                                                   H, W, C, g2, mask, bound);
   }
 }
 
@@ -856,7 +927,7 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
                  const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                  float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
                  hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
-                 const unsigned char* mask = nullptr, TZ* dyout = nullptr) {
+                 const unsigned char* mask = nullptr, TZ* dyout = nullptr, unsigned* bound = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   constexpr bool bf = sizeof(TZ) == 2;
@@ -874,10 +945,10 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
 #define RED(P, A)                                                                                               \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
-                                                            N, H, W, C, rpb, sig, sig_val, g2, mask, dyout);            \
+                                                            N, H, W, C, rpb, sig, sig_val, g2, mask, dyout, bound);     \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
-                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout)
+                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout, bound)
   if (nw > 0) {
     nblk = nw;
   } else if (pool) {
@@ -890,8 +961,12 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
     RED(false, 2);
   }
 #undef RED
-  bn_bwd_finalize_kernel<8><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd, dgamma,
-                                                        dbeta, dbias, coef);
+  if (nw > 0)  // (bn_wide.hip's rows: the three sums)
+    bn_bwd_finalize_kernel<8, 3><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
+                                                             dgamma, dbeta, dbias, coef, nullptr);
+  else
+    bn_bwd_finalize_kernel<8, 5><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
+                                                             dgamma, dbeta, dbias, coef, bound);
   return (int)hipGetLastError();
 }
 
@@ -1041,13 +1116,15 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                 const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2,
-                const unsigned char* mask) {
+                const unsigned char* mask, unsigned* bound) {
   if (nsplit < 1) nsplit = 1;
+  if (np == 2 && (sizeof(TZ) != 4 || bound == nullptr || act != 0)) return -2;  // fp16 pairs: the VGG engine
   // add+ReLU: the reduce pass stores dy (= dres) and the apply pass reads it alone as an identity
   // activation (measured faster than re-reading g, g2 and the mask / residual)
   const bool dyp = act == 2 && nsplit == 1 && !pool && dres != nullptr;
   const int rc0 = bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta,
-                                   dbias, N, H, W, C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr);
+                                   dbias, N, H, W, C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr,
+                                   np == 2 ? bound : nullptr);
   if (rc0) return rc0;
   if (dyp) {
     act = 1;
@@ -1071,6 +1148,17 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
   const int grid = grid_ch(total, C / 4);
 #define BAP(P, NPT) \
   bn_bwd_apply_launch<P, NPT, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C, g2, mask)
+  if (np == 2) {
+    if constexpr (sizeof(TZ) == 4) {
+      if (pool)
+        bn_bwd_apply_launch<true, 2, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W, C,
+                                         g2, mask, bound);
+      else
+        bn_bwd_apply_launch<false, 2, TZ>(act, grid, st, gg, z, scale, shift, coef, dz, dz3, ps, res, dres, N, H, W,
+                                          C, g2, mask, bound);
+    }
+    return (int)hipGetLastError();
+  }
   if (pool) {
     if (np == 0) BAP(true, 0);
     else if (np == 1) BAP(true, 1);
@@ -1087,7 +1175,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
 }  // namespace
 
 extern "C" {
-// floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (3 per ...)
+// floats of partial workspace needed by fwd stats (2 per (block, channel)) / bwd (5 per ...)
 // (backward: rows of the fp32 or the bf16 geometry, whichever has more; the bf16 wide reduce of
 // bn_wide.hip uses the bf16 geometry's rows per block)
 long dpa_bn_part_floats(int M, int C, int bwd) {
@@ -1097,7 +1185,7 @@ long dpa_bn_part_floats(int M, int C, int bwd) {
   }
   const int r32 = bwd_rows_per_block(M, C, false), r16 = bwd_rows_per_block(M, C, true);
   const long nblk = std::max((M + r32 - 1) / r32, (M + r16 - 1) / r16);
-  return nblk * C * 3;
+  return nblk * C * 5;  // [block][5][C]: the three sums and the two maxima
 }
 
 // z [M][C] (or nsplit fp32 slabs of it in src; then z is written) -> partials -> finalize.
@@ -1138,7 +1226,7 @@ int dpa_bn_eval_params(const float* gamma, const float* beta, const float* bias,
   return (int)hipGetLastError();
 }
 
-// out: fp32 a (np == 0) or bf16 planes a3 [np][...] (np in {1, 3}).  act: 0 relu (pool allowed),
+// out: fp32 a (np == 0), bf16 planes a3 [np][...] (np in {1, 3}) or fp16 pairs (np 2, scale H2_SA).  act: 0 relu (pool allowed),
 // 1 none, 2 relu(. + res).  zbf: z and res are bf16.
 int dpa_bn_apply(const void* z, float* a, u16* a3, int np, const float* scale, const float* shift, int N, int H,
                  int W, int C, int pool, int act, const void* res, int zbf, hipStream_t st, unsigned char* mask) {
@@ -1159,7 +1247,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2,
-               const unsigned char* mask) {
+               const unsigned char* mask, unsigned* bound) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && ((!res && !mask) || !dres))) return -2;
   if (mask && act != 2) return -2;
   if (zbf && nsplit > 1) return -2;
@@ -1167,10 +1255,10 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask);
+                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask, bound);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st, sig, sig_val, (const float*)g2, mask);
+                            (float*)dres, st, sig, sig_val, (const float*)g2, mask, bound);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.
@@ -1192,5 +1280,7 @@ int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, c
   wgrad0_reduce_kernel<<<64, 1024, 0, st>>>(wpart, nblk, 64, dw, CP);
   return (int)hipGetLastError();
 }
+
+DPA_H2_OVF_ACCESSOR(dpa_h2_ovf_bn)
 
 }  // extern "C"

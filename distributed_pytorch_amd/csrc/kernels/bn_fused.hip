@@ -88,10 +88,11 @@ __device__ __forceinline__ void store_out(const FArgs& a, long i4, float4 v) {
     reinterpret_cast<float4*>(a.out)[i4] = v;
   } else {
     u16 o[4][3];
-    split_val<NP>(v.x, o[0]);
-    split_val<NP>(v.y, o[1]);
-    split_val<NP>(v.z, o[2]);
-    split_val<NP>(v.w, o[3]);
+    constexpr float s = NP == 2 ? H2_SA : 1.f;  // (fp16 pairs: activation planes only, forward)
+    split_val<NP>(v.x, o[0], s);
+    split_val<NP>(v.y, o[1], s);
+    split_val<NP>(v.z, o[2], s);
+    split_val<NP>(v.w, o[3], s);
 #pragma unroll
     for (int p = 0; p < NP; ++p)
       reinterpret_cast<ushort4*>(a.out3 + p * a.ps)[i4] = make_ushort4(o[0][p], o[1][p], o[2][p], o[3][p]);
@@ -514,11 +515,13 @@ void launch_fwd(bool pool, int np, int grid, const FArgs& a, hipStream_t st) {
     if constexpr (U <= UMAX_FWD_POOL) {
       if (np == 0) LF(true, 0);
       else if (np == 1) LF(true, 1);
+      else if (np == 2) LF(true, 2);
       else LF(true, 3);
     }
   } else {
     if (np == 0) LF(false, 0);
     else if (np == 1) LF(false, 1);
+    else if (np == 2) LF(false, 2);
     else LF(false, 3);
   }
 #undef LF
@@ -619,6 +622,9 @@ bool pick_geo_resident(int Mo, int C, bool pool, bool bwd, int rmax, Geo& g) {
 
 template <int CL>
 int dispatch(bool bwd, bool pool, int np, const Geo& g, const FArgs& a, hipStream_t st) {
+  // fp16-pair data-gradient planes need the bound of the whole tensor before the apply phase, which
+  // this kernel's per-slice rendezvous cannot give: the three-kernel BN backward carries them
+  if (bwd && np == 2) return -2;
   const int grid = g.slices * g.R;
   switch (g.U) {
 #define CASE(UU)                                   \
@@ -725,3 +731,5 @@ int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H
   return g.CL == 16 ? dispatch<16>(true, pool != 0, np, g, a, st) : dispatch<8>(true, pool != 0, np, g, a, st);
 }
 }  // extern "C"
+
+DPA_H2_OVF_ACCESSOR(dpa_h2_ovf_fused)

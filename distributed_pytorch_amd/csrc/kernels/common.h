@@ -60,17 +60,71 @@ __device__ __forceinline__ u16 bf16_rne(float f) {
 }
 __device__ __forceinline__ float bf16_f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
 
+// ---- fp16 operand pairs (NP = 2, impl "h2"): x * s = h0 + h1 ----
+// h0 = fp16(x s), h1 = fp16(x s - h0), both round-to-nearest-even: 22 significant bits in two
+// planes, and a product a * b from THREE plane products a0 b0 + a0 b1 + a1 b0 (the dropped a1 b1
+// is below 2^-21 of it) on the fp16 matrix cores -- half the MFMA work of the bf16 triple's six
+// products at the same fp32-level error (docs/PERF_NOTES.md, round 5).  fp16's exponent range
+// needs a per-tensor power-of-two scale s, undone exactly in the consuming conv's epilogue:
+//  * weights and activations (BatchNorm outputs) use fixed scales, H2_SW and H2_SA: their
+//    magnitudes are bounded by construction; a split that would leave fp16's range raises the
+//    translation unit's overflow word (g_h2_ovf, read by dpa_h2_overflow), which fails the step;
+//  * data gradients use a scale from a bound the BatchNorm backward computes for every step
+//    (bn.hip): |dz s| < 2^14 always.
+// Values below 2^-14 / s keep an absolute error under 2^-25 / s: negligible against the
+// fp32-rounding error of the sums they enter.
+constexpr float H2_SW = 256.f;  // weight planes: |w| < 255
+constexpr float H2_SA = 16.f;   // activation planes: |a| < 4093
+constexpr float H2_FP16_MAX = 65504.f;
+static __device__ int g_h2_ovf;  // per translation unit
+__device__ __forceinline__ u16 f16_bits(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
+__device__ __forceinline__ float f16_f(u16 h) { return (float)__builtin_bit_cast(_Float16, h); }
+// the scale of a tensor bounded by B: the power of two s with B s < 2^14 (1 for B = 0 / non-finite)
+__device__ __forceinline__ float h2_scale_of_bound(float B) {
+  if (!(B > 0.f) || !(B < 3.0e38f)) return 1.f;
+  int e;
+  frexpf(B, &e);  // B = m 2^e, m in [0.5, 1): B < 2^e
+  return ldexpf(1.f, min(126, 14 - e));
+}
+// the conv epilogue's factor 1 / (s_a s_b): a constant part and, for a data-gradient operand, the
+// scale of its bound (a device word written by the BatchNorm backward)
+__device__ __forceinline__ float h2_out_scale(float c, const unsigned* bound) {
+  return bound != nullptr ? c / h2_scale_of_bound(__uint_as_float(*bound)) : c;
+}
+
+// NP 1 / 3: bf16 planes of v (s unused); NP 2: the fp16 pair of v * s
 template <int NP>
-__device__ __forceinline__ void split_val(float v, u16* o) {
-  const u16 h0 = bf16_rne(v);
-  o[0] = h0;
-  if (NP == 3) {
-    const float r1 = v - bf16_f(h0);
-    const u16 h1 = bf16_rne(r1);
-    o[1] = h1;
-    o[2] = bf16_rne(r1 - bf16_f(h1));
+__device__ __forceinline__ void split_val(float v, u16* o, float s = 1.f) {
+  if constexpr (NP == 2) {
+    const float xs = v * s;
+    if (fabsf(xs) > H2_FP16_MAX) g_h2_ovf = 1;
+    const u16 h0 = f16_bits(xs);
+    o[0] = h0;
+    o[1] = f16_bits(xs - f16_f(h0));
+  } else {
+    const u16 h0 = bf16_rne(v);
+    o[0] = h0;
+    if (NP == 3) {
+      const float r1 = v - bf16_f(h0);
+      const u16 h1 = bf16_rne(r1);
+      o[1] = h1;
+      o[2] = bf16_rne(r1 - bf16_f(h1));
+    }
   }
 }
+
+// host accessor of a translation unit's overflow word (read, optionally clear)
+#define DPA_H2_OVF_ACCESSOR(fn)                                                    \
+  extern "C" int fn(int clear) {                                                   \
+    int v = 0;                                                                     \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_h2_ovf), sizeof(int)) != hipSuccess) \
+      return -1;                                                                   \
+    if (clear && v) {                                                              \
+      const int z = 0;                                                             \
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_h2_ovf), &z, sizeof(int));              \
+    }                                                                              \
+    return v;                                                                      \
+  }
 
 // ---- deterministic split-K reduction: out[i] = sum_k slabs[k * n4 + i] over float4 elements ----
 // Block = 64 float4 columns x G split lanes: lane g sums splits g, g+G, ... and the G partials are

@@ -34,6 +34,16 @@
 extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipStream_t s);  // sgd.hip
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// one 16-bit MFMA step: bf16 planes (NP 1 / 3) or fp16 pairs (NP 2; fragments carry fp16 bits)
+template <int NP>
+__device__ __forceinline__ f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (NP == 2)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
@@ -93,6 +103,8 @@ struct Args {
   // dx pixel (img, 2i + ph, 2j + pw) of the outH x outW output.
   int sepi;  // OB outputs: 1 = stores staged through LDS as 16-byte row pieces (DPA_OB_EPI)
   int nph, outH, outW;
+  float oscale;            // NP 2: 1 / (s_a s_b) of the operands' constant scales ...
+  const unsigned* obound;  // ... times 1 / s of a data-gradient operand's bound word (or nullptr)
   struct Phase {
     int Ktot, S, r0, s0, padh, padw;
     FastDiv fd_S;
@@ -134,18 +146,38 @@ enum { XM_FPROP = 0, XM_DGRAD = 1, XM_WGRAD = 2 };
 // The plane products of one k-slice over a TM x TN register tile, product-major: the TM*TN
 // accumulators are independent, so back-to-back MFMAs never wait on each other's result (an
 // accumulator-major order gives chains of six dependent MFMAs).  Each accumulator still sees its
-// products smallest-first, so results are unchanged bit for bit.
+// products smallest-first, so results are unchanged bit for bit.  NP 3: the six bf16 products
+// a2b0 a1b1 a0b2 a1b0 a0b1 a0b0; NP 2: the three fp16 products a1b0 a0b1 a0b0; NP 1: a0b0.
+template <int NP>
+struct PlaneProducts {
+  static constexpr int Q0 = NP == 3 ? 0 : (NP == 2 ? 3 : 5);  // first product of the list below
+  static constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};  // (A plane, B plane)
+};
 template <int TM, int TN, int NP>
 __device__ __forceinline__ void mfma_tile(f32x16 (&acc)[TM][TN], const bf16x8 (&fa)[TM][NP],
                                           const bf16x8 (&fb)[TN][NP]) {
-  constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};  // (A plane, B plane)
+  using PP = PlaneProducts<NP>;
 #pragma unroll
-  for (int q = NP == 3 ? 0 : 5; q < 6; ++q)
+  for (int q = PP::Q0; q < 6; ++q)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<NP>(fa[i][PP::PA[q]], fb[j][PP::PB[q]], acc[i][j]);
+}
+
+// fp16 pairs (NP 2): the accumulators hold (a s_a)(b s_b); one exact power-of-two multiply returns
+// them to the product's own scale before anything is stored or reduced
+template <int NP, int TM, int TN>
+__device__ __forceinline__ void unscale_acc(f32x16 (&acc)[TM][TN], float oscale, const unsigned* obound) {
+  if constexpr (NP == 2) {
+    const float f = h2_out_scale(oscale, obound);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][PA[q]], fb[j][PB[q]], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= f;
+  }
 }
 
 // ---- BatchNorm statistics in the forward conv's epilogue ----
@@ -685,6 +717,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_x3_kernel(Args a) 
   }
 
   // ---------------- epilogue (fp32; FPROP rows stored at their NHWC memory row) ----------------
+  unscale_acc<NP>(acc, a.oscale, a.obound);
   float* out = a.out + (long)split * a.slab;
   const int ldc = WG ? a.Ktot : a.Nout;
   const int nrows = WG ? a.Nout : a.M;
@@ -992,7 +1025,9 @@ struct HArgs {
   int* sig;                 // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
   float2* stats;            // FPROP, one split: per (row tile, output channel) BN (mean, M2)
-  int sepi;                 // OB: stores staged through LDS (DPA_OB_EPI)
+  int sepi;                 // OB: stores staged through LDS
+  float oscale;             // NP 2: output scale (Args::oscale / obound)
+  const unsigned* obound;
 };
 
 // staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
@@ -1220,6 +1255,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   }
 
   // ---------------- epilogue (rows are NHWC pixels) ----------------
+  unscale_acc<NP>(acc, a.oscale, a.obound);
   float* out = a.out + (long)blockIdx.y * a.slab;
   bool staged = false;
   {  // outputs through LDS as 16-byte row pieces (conv_x3_kernel's epilogue)
@@ -1292,6 +1328,8 @@ struct WHArgs {
   int N, H, W, C, K, M;
   int gk, gc, nchunks, cps;
   FastDiv fd_HW, fd_W;
+  float oscale;  // NP 2: output scale (Args::oscale / obound)
+  const unsigned* obound;
 };
 
 __host__ __device__ constexpr int halo_wslots(int P) { return 2 * P + 4; }  // P + 2W + 2 (W <= P/2) + zero slot
@@ -1424,14 +1462,9 @@ __global__ __launch_bounds__(256) void conv_halo_wgrad_kernel(WHArgs a) {
           const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           fb[p] = __builtin_bit_cast(bf16x8, v);
         }
-        if constexpr (NP == 3) {
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[tap], 0, 0, 0);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[tap], 0, 0, 0);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[tap], 0, 0, 0);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[tap], 0, 0, 0);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[tap], 0, 0, 0);
-        }
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[tap], 0, 0, 0);
+        using PP = PlaneProducts<NP>;
+#pragma unroll
+        for (int q = PP::Q0; q < 6; ++q) acc[tap] = mfma16<NP>(fa[PP::PA[q]], fb[PP::PB[q]], acc[tap]);
       }
     }
   };
@@ -1452,6 +1485,13 @@ __global__ __launch_bounds__(256) void conv_halo_wgrad_kernel(WHArgs a) {
     }
   }
 
+  if constexpr (NP == 2) {
+    const float f = h2_out_scale(a.oscale, a.obound);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] *= f;
+  }
   float* out = a.out + (long)blockIdx.y * a.slab;
   const int col = c0 + li;
   if (col < a.C) {
@@ -1499,6 +1539,8 @@ struct PArgs {
   unsigned perm;         // position slot k -> local position, 4 bits per slot
   int* sig;              // optional kernel-start stream signal (common.h start_signal)
   int sig_val;
+  float oscale;          // NP 2: output scale (Args::oscale / obound)
+  const unsigned* obound;
 };
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, int NI, int NSPX, int PD>
@@ -1672,7 +1714,6 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_pos_kernel(PArgs a
     }
     if (!any) return;
     const u16* Bst = Bs + stage * NP * B_PLANE;
-    constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};  // as mfma_tile
 #pragma unroll
     for (int ks = 0; ks < BC / 16; ++ks) {
       bf16x8 fb[TN][NP];
@@ -1691,12 +1732,11 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_pos_kernel(PArgs a
         bf16x8 fa[NP];
 #pragma unroll
         for (int p = 0; p < NP; ++p) fa[p] = frag_k(As + p * A_PLANE, sl[i], ks);
+        using PP = PlaneProducts<NP>;
 #pragma unroll
-        for (int q = NP == 3 ? 0 : 5; q < 6; ++q)
+        for (int q = PP::Q0; q < 6; ++q)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[NP == 3 ? PA[q] : 0], fb[j][NP == 3 ? PB[q] : 0],
-                                                                acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<NP>(fa[PP::PA[q]], fb[j][PP::PB[q]], acc[i][j]);
       }
     }
   };
@@ -1739,6 +1779,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_pos_kernel(PArgs a
   }
 
   // ---------------- epilogue: sub-tile rows are (image, position) -> NHWC row image * HW + position
+  unscale_acc<NP>(acc, a.oscale, a.obound);
   float* out = a.out + (long)blockIdx.y * a.slab;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -1757,19 +1798,19 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_pos_kernel(PArgs a
   }
 }
 
-// ---------------- fp32 -> bf16 planes ----------------
-// x [n] fp32 -> planes [NP][n] (n % 4 == 0)
+// ---------------- fp32 -> operand planes ----------------
+// x [n] fp32 -> planes [NP][n] (n % 4 == 0); NP 2: the fp16 pairs of x * s
 template <int NP>
 __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, u16* __restrict__ out, long n4,
-                                                    long ps) {
+                                                    long ps, float s) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float4 v = reinterpret_cast<const float4*>(x)[i];
     u16 o[4][3];
-    split_val<NP>(v.x, o[0]);
-    split_val<NP>(v.y, o[1]);
-    split_val<NP>(v.z, o[2]);
-    split_val<NP>(v.w, o[3]);
+    split_val<NP>(v.x, o[0], s);
+    split_val<NP>(v.y, o[1], s);
+    split_val<NP>(v.z, o[2], s);
+    split_val<NP>(v.w, o[3], s);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       ushort4 w = make_ushort4(o[0][p], o[1][p], o[2][p], o[3][p]);
@@ -1782,12 +1823,12 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x,
 // to the 8-channel operand granularity, one 16-byte chunk per pixel per plane.
 template <int NP>
 __global__ __launch_bounds__(256) void pad_split_kernel(const float* __restrict__ x, u16* __restrict__ out, long npix,
-                                                        int cin, long ps) {
+                                                        int cin, long ps, float s) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < npix; i += stride) {
     u16 o[8][3];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) split_val<NP>(c < cin ? x[i * cin + c] : 0.f, o[c]);
+    for (int c = 0; c < 8; ++c) split_val<NP>(c < cin ? x[i * cin + c] : 0.f, o[c], s);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       uint4 v;
@@ -1840,6 +1881,7 @@ int launch_tile(const Args& a, int tile, hipStream_t st) {
 template <int MODE>
 int launch_any(const Args& a, int tile, int np, int obf, hipStream_t st) {
   if (obf) return launch_tile<MODE, 1, true>(a, tile, st);
+  if (np == 2) return launch_tile<MODE, 2>(a, tile, st);
   return np == 3 ? launch_tile<MODE, 3>(a, tile, st) : launch_tile<MODE, 1>(a, tile, st);
 }
 // epilogue stores staged through LDS as 16-byte row pieces (conv_x3_kernel / conv_halo_kernel): measured
@@ -1941,6 +1983,8 @@ int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void*
     rc = launch_halo_tile<DG, 1, true>(a, tile, splits, st);
   else if (np == 3)
     rc = launch_halo_tile<DG, 3, false>(a, tile, splits, st);
+  else if (np == 2)
+    rc = launch_halo_tile<DG, 2, false>(a, tile, splits, st);
   else
     rc = launch_halo_tile<DG, 1, false>(a, tile, splits, st);
   if (rc) return rc;
@@ -1982,6 +2026,8 @@ int run_halo_wgrad(WHArgs& a, int tile, int splits, int np, float* dw, float* sl
   int rc;
   if (np == 3)
     rc = P == 64 ? launch_halo_wgrad<3, 64>(a, splits, st) : launch_halo_wgrad<3, 32>(a, splits, st);
+  else if (np == 2)
+    rc = P == 64 ? launch_halo_wgrad<2, 64>(a, splits, st) : launch_halo_wgrad<2, 32>(a, splits, st);
   else
     rc = P == 64 ? launch_halo_wgrad<1, 64>(a, splits, st) : launch_halo_wgrad<1, 32>(a, splits, st);
   if (rc || splits == 1) return rc;
@@ -2107,7 +2153,9 @@ int run_pos(PArgs& a, int tile, int splits, int np, int obf, float* slab, void* 
   a.cps = cdiv(a.C / BC, splits);
   a.out = splits > 1 ? slab : (float*)out;
   a.slab = splits > 1 ? M * a.Nout : 0;
-  const int rc = np == 3 ? launch_pos_tile<DG, 3>(a, tile, splits, st) : launch_pos_tile<DG, 1>(a, tile, splits, st);
+  const int rc = np == 3   ? launch_pos_tile<DG, 3>(a, tile, splits, st)
+                 : np == 2 ? launch_pos_tile<DG, 2>(a, tile, splits, st)
+                           : launch_pos_tile<DG, 1>(a, tile, splits, st);
   if (rc) return rc;
   if (splits == 1) return add ? dpa_add_inplace(out, add, M * a.Nout, 0, st) : 0;
   if (!reduce) return 0;
@@ -2127,14 +2175,16 @@ int dpa_conv_stats_rows(int tile) {
 
 // x planes [NP][N,H,W,C] (plane stride xps), w planes [NP][Kout][R][S][C] (stride wps; for a data
 // gradient pass the flipped/transposed Wd planes), out fp32 [N,P,Q,Kout] (or slabs, see
-// conv_gemm.hip).  np: 1 (bf16) or 3 (fp32 via bf16x6).  tile: 0 = 128x128, 1 = 64x64.
+// conv_gemm.hip).  np: 1 (bf16), 3 (fp32 via bf16x6) or 2 (fp32 via fp16 pairs; outputs times
+// h2_out_scale(oscale, obound)).  tile: 0 = 128x128, 1 = 64x64.
 // posmajor: bit 0 = position-major GEMM rows, bit 1 = column-tile-outer block order (Args.nmajor;
 // implicit-GEMM tiles only, the halo kernels ignore it).
 // stats (optional, one split, implicit-GEMM or halo tiles): float2 [Kout][row tiles of conv_stats_rows]
 // BN (mean, M2) partials of the output, channel-major (epi_col_stats), for dpa_bn_finalize_cm.
 int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int reduce,
-                      int posmajor, int np, int obf, hipStream_t st, float* stats) {
+                      int posmajor, int np, int obf, hipStream_t st, float* stats, float oscale,
+                      const unsigned* obound) {
   if (stats && (is_pos(tile) || (is_halo(tile) ? xsplits(9 * C, splits) : xsplits(R * S * C, splits)) > 1)) return -7;
   if (is_stream(tile)) {
     if (R != 1 || S != 1 || stride != 1 || pad != 0) return -6;
@@ -2143,6 +2193,8 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     HArgs h{};
+    h.oscale = oscale;
+    h.obound = obound;
     h.x = x;
     h.xps = xps;
     h.w = w;
@@ -2159,6 +2211,8 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
   if (is_pos(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     PArgs q{};
+    q.oscale = oscale;
+    q.obound = obound;
     q.x = x;
     q.xps = xps;
     q.w = w;
@@ -2172,6 +2226,8 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
     return run_pos<false>(q, tile, xsplits(9 * C, splits), np, obf, slab, out, reduce, st);
   }
   Args a{};
+  a.oscale = oscale;
+  a.obound = obound;
   a.x = x;
   a.xps = xps;
   a.w = w;
@@ -2210,7 +2266,8 @@ int dpa_conv_x3_fprop(const u16* x, long xps, const u16* w, long wps, void* out,
 // in front of the stores).
 int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx, float* slab, int N, int Hd, int Wd,
                       int K, int C, int R, int S, int stride, int pad, int H, int W, int splits, int tile, int reduce,
-                      int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig, int sig_val) {
+                      int posmajor, int np, int obf, hipStream_t st, const void* add, int* sig, int sig_val,
+                      float oscale, const unsigned* obound) {
   if (is_stream(tile)) {  // dX = dZ W for a 1x1 / stride-1 conv (W [K][C] read row-contiguous)
     if (R != 1 || S != 1 || stride != 1 || pad != 0 || sig) return -6;
     const int rc = run_stream(dz, w, dx, N * H * W, C, K, np, obf, xsplits(K, splits), nullptr, st, true);
@@ -2220,6 +2277,8 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
     HArgs h{};
+    h.oscale = oscale;
+    h.obound = obound;
     h.sig = sig;
     h.sig_val = sig_val;
     h.x = dz;
@@ -2237,6 +2296,8 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
   if (is_pos(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3 || Hd != H || Wd != W) return -6;
     PArgs q{};
+    q.oscale = oscale;
+    q.obound = obound;
     q.sig = sig;
     q.sig_val = sig_val;
     q.x = dz;
@@ -2252,6 +2313,8 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
     return run_pos<true>(q, tile, xsplits(9 * K, splits), np, obf, slab, dx, reduce, st, add);
   }
   Args a{};
+  a.oscale = oscale;
+  a.obound = obound;
   a.sig = sig;
   a.sig_val = sig_val;
   a.x = dz;
@@ -2327,10 +2390,12 @@ int dpa_conv_x3_dgrad(const u16* dz, long dzps, const u16* w, long wps, void* dx
 // dW[Kout][R*S*C] = sum_m dZ[m][kout] Xcol[m][rsc]; x planes [NP][N,H,W,C], dz planes [NP][N,P,Q,Kout]
 int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* dw, float* slab, int N, int H, int W,
                       int C, int Kout, int R, int S, int stride, int pad, int splits, int tile, int posmajor, int np,
-                      hipStream_t st) {
+                      hipStream_t st, float oscale, const unsigned* obound) {
   if (is_halo(tile)) {
     if (stride != 1 || pad != 1 || R != 3 || S != 3) return -6;
     WHArgs h{};
+    h.oscale = oscale;
+    h.obound = obound;
     h.x = x;
     h.xps = xps;
     h.dz = dz;
@@ -2343,6 +2408,8 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
     return run_halo_wgrad(h, tile, xsplits(N * H * W, splits), np, dw, slab, st);
   }
   Args a{};
+  a.oscale = oscale;
+  a.obound = obound;
   a.x = x;
   a.xps = xps;
   a.w = dz;
@@ -2359,7 +2426,9 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   a.out = a.splits > 1 ? slab : dw;
   a.slab = a.splits > 1 ? (long)Kout * a.Ktot : 0;
   a.sepi = ob_epi();
-  const int rc = np == 3 ? launch_tile<XM_WGRAD, 3>(a, tile, st) : launch_tile<XM_WGRAD, 1>(a, tile, st);
+  const int rc = np == 3   ? launch_tile<XM_WGRAD, 3>(a, tile, st)
+                 : np == 2 ? launch_tile<XM_WGRAD, 2>(a, tile, st)
+                           : launch_tile<XM_WGRAD, 1>(a, tile, st);
   if (rc) return rc;
   if (a.splits > 1) {
     const long n4 = (long)Kout * a.Ktot / 4;
@@ -2368,22 +2437,30 @@ int dpa_conv_x3_wgrad(const u16* x, long xps, const u16* dz, long dzps, float* d
   return 0;
 }
 
-int dpa_split_planes(const float* x, u16* out, long n, long ps, int np, hipStream_t st) {
+// np 2: the fp16 pairs of x * scale (scale a power of two; conv outputs divide it out)
+int dpa_split_planes(const float* x, u16* out, long n, long ps, int np, float scale, hipStream_t st) {
   if (n % 4) return -2;
   if (np == 3)
-    split_kernel<3><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
+    split_kernel<3><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps, 1.f);
+  else if (np == 2)
+    split_kernel<2><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps, scale);
   else
-    split_kernel<1><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps);
+    split_kernel<1><<<grid_1d(n / 4), 256, 0, st>>>(x, out, n / 4, ps, 1.f);
   return (int)hipGetLastError();
 }
 
+// np 2: activation planes (scale H2_SA)
 int dpa_pad_split8(const float* x, u16* out, long npix, int cin, long ps, int np, hipStream_t st) {
   if (cin > 8) return -2;
   if (np == 3)
-    pad_split_kernel<3><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps);
+    pad_split_kernel<3><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps, 1.f);
+  else if (np == 2)
+    pad_split_kernel<2><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps, H2_SA);
   else
-    pad_split_kernel<1><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps);
+    pad_split_kernel<1><<<grid_1d(npix), 256, 0, st>>>(x, out, npix, cin, ps, 1.f);
   return (int)hipGetLastError();
 }
+
+DPA_H2_OVF_ACCESSOR(dpa_h2_ovf_conv)
 
 }  // extern "C"

@@ -41,10 +41,11 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, co
     reinterpret_cast<float4*>(p)[i] = pv;
     if constexpr (NP > 0) {
       u16 o[4][3];
-      split_val<NP>(pv.x, o[0]);
-      split_val<NP>(pv.y, o[1]);
-      split_val<NP>(pv.z, o[2]);
-      split_val<NP>(pv.w, o[3]);
+      constexpr float s = NP == 2 ? H2_SW : 1.f;  // fp16 pairs: the weight planes' scale
+      split_val<NP>(pv.x, o[0], s);
+      split_val<NP>(pv.y, o[1], s);
+      split_val<NP>(pv.z, o[2], s);
+      split_val<NP>(pv.w, o[3], s);
 #pragma unroll
       for (int q = 0; q < NP; ++q)
         reinterpret_cast<ushort4*>(planes + q * ps)[i] = make_ushort4(o[0][q], o[1][q], o[2][q], o[3][q]);
@@ -71,7 +72,8 @@ static int grid_for(long n, int block) {
   return (int)g;
 }
 
-// planes: NP bf16 planes of the same arena slice (plane stride ps), or nullptr / np = 0
+// planes: NP operand planes of the same arena slice (plane stride ps; np 2: fp16 pairs of p * H2_SW),
+// or nullptr / np = 0
 extern "C" int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float lr, float momentum, float wd,
                             float gscale, int first, u16* planes, long ps, int np, hipStream_t s) {
   if (n % 4) return -1;
@@ -79,6 +81,8 @@ extern "C" int dpa_sgd_flat(float* p, const float* g, float* buf, long n, float 
   const int grid = grid_for(n4, 256);
   if (planes && np == 3)
     sgd_flat_kernel<3><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, planes, ps);
+  else if (planes && np == 2)
+    sgd_flat_kernel<2><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, planes, ps);
   else if (planes && np == 1)
     sgd_flat_kernel<1><<<grid, 256, 0, s>>>(p, g, buf, n4, lr, momentum, wd, gscale, first, planes, ps);
   else
@@ -111,3 +115,5 @@ extern "C" int dpa_add_inplace(void* out, const void* add, long n, int bf, hipSt
     add_inplace_kernel<float4><<<grid_for(n4, 256), 256, 0, s>>>((float4*)out, (const float4*)add, n4);
   return (int)hipGetLastError();
 }
+
+DPA_H2_OVF_ACCESSOR(dpa_h2_ovf_sgd)

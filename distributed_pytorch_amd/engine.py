@@ -72,7 +72,7 @@ def conv_cfg(kind: str, M: int, N: int, K: int):
     return 0, s
 
 
-IMPLS = ("fp32", "x3", "bf16")
+IMPLS = ("fp32", "x3", "bf16", "h2")
 _TUNING = None
 
 
@@ -141,6 +141,11 @@ class VGGEngine:
     * ``"fp32"`` — fp32 MFMA implicit GEMM (v_mfma_f32_32x32x2_f32), exact fp32 products;
     * ``"x3"``   — fp32-grade results on bf16 MFMA: operands kept as three bf16 planes, six plane
                    products per multiply (conv_x3.hip); error at fp32 rounding level;
+    * ``"h2"``   — fp32-grade results on fp16 MFMA: operands kept as fp16 pairs of a power-of-two
+                   scaled value (22 significant bits), three plane products per multiply -- half the
+                   matrix work and two thirds of the operand bytes of ``"x3"`` at the same error
+                   (kernels/common.h: fixed weight / activation scales with an overflow check, data
+                   gradients scaled by a bound the BatchNorm backward computes every step);
     * ``"bf16"`` — one bf16 plane (mixed precision: bf16 operands, fp32 accumulation/BN/SGD).
     """
 
@@ -154,7 +159,11 @@ class VGGEngine:
         if self.K is cpu_ref:
             impl = "fp32"  # the CPU oracle backend implements the fp32 kernel API only
         self.impl = impl
-        self.np = {"fp32": 0, "x3": 3, "bf16": 1}[impl]
+        self.np = {"fp32": 0, "x3": 3, "bf16": 1, "h2": 2}[impl]
+        pdt = torch.float16 if self.np == 2 else torch.bfloat16  # operand-plane storage
+        # fp16 pairs: fixed weight / activation scales (the kernels' H2_SW / H2_SA) and per-layer
+        # data-gradient bound words (bn_bwd writes them, the convs that read dz divide the scale out)
+        self.h2_sw, self.h2_sa = 256.0, 16.0
         # plane kernels take the 3-channel input padded to 8 (one 16-B chunk per pixel)
         self.spec = VGGSpec.from_name(name, num_classes, in_hw, in_pad=8 if self.np else 4)
         self.max_batch = max_batch
@@ -184,10 +193,10 @@ class VGGEngine:
         f32 = dict(device=dev, dtype=torch.float32)
         self.x0 = torch.zeros(N, in_hw, in_hw, 4, **f32)
         # bf16 planes of the (padded) network input when layer 0 runs the plane kernels
-        self.x0p = (torch.zeros(self.np, N, in_hw, in_hw, L[0].cin_pad, dtype=torch.bfloat16, device=dev)
+        self.x0p = (torch.zeros(self.np, N, in_hw, in_hw, L[0].cin_pad, dtype=pdt, device=dev)
                     if self.np and L[0].cin_pad % 8 == 0 else None)
         self.target = torch.zeros(N, dtype=torch.int64, device=dev)
-        bf = dict(device=dev, dtype=torch.bfloat16)
+        bf = dict(device=dev, dtype=pdt)
         # planes(i): layer i runs the bf16-plane kernels (needs cin % 8 == 0)
         self.planes = [self.np > 0 and l.cin_pad % 8 == 0 for l in L]
         self.z, self.a, self.g, self.dz = [], [], [], []
@@ -198,6 +207,7 @@ class VGGEngine:
         # (forward and, read transposed in place, data gradient)
         self.wplanes = torch.zeros(self.np, self.params.flat.numel(), **bf) if any(self.planes) else None
         self.w3: List[Optional[torch.Tensor]] = []
+        self.dzb = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.np == 2 else None
         self.stats = []  # per layer dict(mean, invstd, scale, shift)
         self.eval_ss = []
         part_need = 1
@@ -287,8 +297,10 @@ class VGGEngine:
         # (layers 4-7 at batch 256), backward only for the 2x2 layers (<= 0.6M; beside the weight-
         # gradient convs the 4x4 layers' rendezvous waits for CUs and loses to the three kernels).
         self.bn_fused_max = int(os.environ.get("DPA_BN_FUSED_MAX", "2200000")) if dev.type == "cuda" else 0
+        # (fp16 pairs: the data-gradient bound needs the whole tensor before the apply, which the
+        # one-launch kernel's per-slice rendezvous cannot give -- the three-kernel backward runs)
         self.bn_fused_bwd_max = (int(os.environ.get("DPA_BN_FUSED_BWD_MAX", "600000"))
-                                 if dev.type == "cuda" else 0)
+                                 if dev.type == "cuda" and self.np != 2 else 0)
         self.bn_fused_rmax = int(os.environ.get("DPA_BN_FUSED_RMAX", "64"))
         self._fgeo: Dict[tuple, bool] = {}
         fpart, fcnt = 0, 0
@@ -374,7 +386,7 @@ class VGGEngine:
         parameters change outside ``sgd_step`` (load, broadcast); the SGD kernel refreshes them
         itself."""
         if self.wplanes is not None:
-            self.K.split_planes(self.params.flat, self.wplanes)
+            self.K.split_planes(self.params.flat, self.wplanes, self.h2_sw if self.np == 2 else 1.0)
 
     @torch.no_grad()
     def state_dict(self, prefix: str = "") -> "OrderedDict[str, torch.Tensor]":
@@ -478,6 +490,8 @@ class VGGEngine:
         else:
             gm, gn, gk = M, l.cout, 9 * l.cin_pad
         t = tuning_table().get(conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout))
+        if t is None and impl == "h2":  # the fp16-pair kernels share x3's tiles: its measured plan
+            t = tuning_table().get(conv_key("x3", kind, n, l.hw, l.cin_pad, l.cout))
         if t is not None:
             tile, s, pm = int(t[0]), int(t[1]), int(t[2])  # pm: bit 0 position-major, bit 1 column-tile order
         elif impl == "fp32":
@@ -598,7 +612,8 @@ class VGGEngine:
         z = self.z[i][:n]
         slab = self.slab if s > 1 else None
         if self.planes[i]:
-            self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm, stats)
+            self.K.conv_x3_fprop(self._in_planes(i, n), self.w3[i], z, slab, 1, 1, s, tile, reduce, pm, stats,
+                                 **self._h2(1.0 / (self.h2_sa * self.h2_sw)))
         else:
             xin = x if i == 0 else self.a[i - 1][:n]
             self.K.conv_fprop(xin, self.params[f"{l.conv_key}.weight"], z, slab, 1, 1, s, tile, False, reduce, pm)
@@ -613,11 +628,12 @@ class VGGEngine:
         slab = self.slab if s > 1 else None
         out = self.g[i - 1][:n]
         if self.planes[i]:
+            h2 = self._h2(1.0 / self.h2_sw, i)
             if sig_val > 0:
                 self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm,
-                                     sig=self.ksig[i:i + 1], sig_val=sig_val)
+                                     sig=self.ksig[i:i + 1], sig_val=sig_val, **h2)
             else:
-                self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm)
+                self.K.conv_x3_dgrad(self.dz3[i][:, :n], self.w3[i], out, slab, 1, 1, s, tile, False, pm, **h2)
         else:
             self.K.conv_fprop(self.dz[i][:n], self.params[f"{l.conv_key}.weight"], out, slab, 1, 1, s, tile, True,
                               False, pm)
@@ -635,10 +651,21 @@ class VGGEngine:
         slab = (self.wslab if side else self.slab) if s > 1 else None
         dw = self.grads[f"{l.conv_key}.weight"]
         if self.planes[i]:
-            self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm)
+            self.K.conv_x3_wgrad(self._in_planes(i, n), self.dz3[i][:, :n], dw, slab, 1, 1, s, tile, pm,
+                                 **self._h2(1.0 / self.h2_sa, i))
         else:
             xin = x if i == 0 else self.a[i - 1][:n]
             self.K.conv_wgrad(xin, self.dz[i][:n], dw, slab, 1, 1, s, tile, pm)
+
+    def _h2(self, oscale: float, dz_layer: Optional[int] = None) -> dict:
+        """fp16-pair conv keywords: the output scale 1 / (s_a s_b) of the constant scales, and the
+        bound word of layer ``dz_layer``'s data gradient when dz is an operand (empty otherwise)."""
+        if self.np != 2:
+            return {}
+        kw = {"oscale": oscale}
+        if dz_layer is not None:
+            kw["obound"] = self.dzb[dz_layer:dz_layer + 1]
+        return kw
 
     def _act_out(self, i: int, n: int) -> torch.Tensor:
         """Where bn_apply of layer i writes: bf16 planes if layer i+1 consumes planes, else fp32."""
@@ -816,9 +843,10 @@ class VGGEngine:
                                G[f"{l.bn_key}.weight"], G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf,
                                self.bn_tmo, self.bn_fused_timeout_us, **bsig)
             else:
+                bnd = {"bound": self.dzb[i:i + 1]} if self.np == 2 and self.planes[i] else {}
                 K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                          st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig)
+                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig, **bnd)
             after_bn(i)
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
@@ -895,6 +923,10 @@ class VGGEngine:
         if self.ksig_tmo is not None and int(self.ksig_tmo.item()) != 0:
             raise RuntimeError("VGGEngine: a wgrad-stream signal wait timed out "
                                f"(DPA_KSIGNAL_TIMEOUT_US={self.ksig_timeout_us}); weight gradients are invalid")
+        if self.np == 2 and self.K.h2_overflow(True):
+            raise RuntimeError("VGGEngine: an fp16-pair operand split left float16's range (a weight beyond "
+                               f"{65504 / self.h2_sw:g} or an activation beyond {65504 / self.h2_sa:g}); "
+                               "this step's convolutions are invalid")
         if int(self.bn_tmo.item()) != 0:
             raise RuntimeError("VGGEngine: a one-launch BatchNorm slice rendezvous timed out "
                                f"(DPA_BN_FUSED_TIMEOUT_US={self.bn_fused_timeout_us}); this step's "

@@ -170,8 +170,9 @@ def add_common_args(ap: argparse.ArgumentParser):
     g.add_argument("--test-size", type=int, default=10000)
     g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     g.add_argument("--comm", default="rccl", choices=["rccl", "ipc", "torch", "gloo"])
-    g.add_argument("--impl", default="x3", choices=["fp32", "x3", "bf16"],
-                   help="GPU conv kernels: x3 (fp32-grade via bf16 planes, default) | fp32 MFMA | bf16")
+    g.add_argument("--impl", default="h2", choices=["fp32", "x3", "h2", "bf16"],
+                   help="GPU conv kernels: h2 (fp32-grade via fp16 pairs, default) | x3 (fp32-grade via "
+                        "bf16 planes) | fp32 MFMA | bf16")
     g.add_argument("--bucket-mb", type=float, default=None)
     g.add_argument("--no-overlap", action="store_true", help="sync after backward (reference placement)")
     g.add_argument("--checkpoint-dir", default=None)

@@ -110,6 +110,32 @@ def test_bn_three_kernel_forward(shape):
     assert int(nbt_d.item()) == 1
 
 
+def _h2_act(a):
+    """Activation value of fp16-pair planes (fixed scale 16)."""
+    return (a[0].float() + a[1].float()) / 16.0
+
+
+@pytest.mark.parametrize("shape", BN_SHAPES)
+def test_bn_apply_fp16_pair_planes(shape):
+    """bn_apply into fp16-pair activation planes (impl "h2"), pooled and not: the pair holds
+    a * 16 to 2^-21 relative (vs the fp32 apply of the same z, scale and shift)."""
+    C_ = _C()
+    N, H, W, C, pool = shape
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(N, H, W, C, generator=g).cuda()
+    scale = (torch.rand(C, generator=g) + 0.5).cuda()
+    shift = torch.randn(C, generator=g).cuda() * 0.1
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    a32 = torch.empty(N, Ho, Wo, C, device="cuda")
+    C_.bn_apply(z, a32, scale, shift, pool)
+    a2 = torch.empty(2, N, Ho, Wo, C, device="cuda", dtype=torch.float16)
+    C_.bn_apply(z, a2, scale, shift, pool)
+    torch.cuda.synchronize()
+    err = (_h2_act(a2).double() - a32.double()).abs()
+    tol = torch.maximum(a32.double().abs() * 2.0 ** -21, torch.full_like(err, 2.0 ** -29))
+    assert (err <= tol).all(), (err / tol).max().item()
+
+
 @pytest.mark.parametrize("shape", BN_SHAPES + [(256, 16, 16, 128, True), (256, 8, 8, 256, False)])
 @pytest.mark.parametrize("nsplit", [1, 2])
 def test_bn_three_kernel_backward(shape, nsplit):
@@ -140,6 +166,52 @@ def test_bn_three_kernel_backward(shape, nsplit):
     assert out[2].abs().max().item() < 1e-3 * ref["dbeta"].abs().max().item() + 1e-4  # dbias ~ 0
 
 
+@pytest.mark.parametrize("shape", BN_SHAPES + [(256, 8, 8, 256, False)])
+@pytest.mark.parametrize("nsplit", [1, 2])
+def test_bn_backward_fp16_pair_planes(shape, nsplit):
+    """fp16-pair dz planes (impl "h2"): the reduce pass tracks max|dy| and max|z|, the finalize writes
+    the bound |k1| max|dy| + |k2| max|z| + |k3| (maximised over the channels) into the bound word,
+    and the apply pass stores the pair of dz * s with s = 2^(14 - e), bound < 2^e.  The pair must
+    hold dz to 2^-21 relative of the tensor's scale (the fp32 apply's own dz, bitwise the same
+    statistics), the bound must cover every |dz|, and |dz s| stay below 2^14."""
+    import math
+
+    C_ = _C()
+    N, H, W, C, pool = shape
+    g, z, gamma, beta, bias, rm, rv, gout = _inputs(shape, 1)
+    ref = oracle(z, gamma, beta, bias, rm, rv, pool, gout)
+    mean, invstd = ref["mean"].float(), ref["invstd"].float()
+    scale, shift = gamma * invstd, beta - mean * gamma * invstd
+    d = lambda t: t.cuda()
+    Ho, Wo = gout.shape[1:3]
+    part = torch.zeros(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
+    outs = []
+    for kind in ("fp32", "h2"):
+        coef = torch.empty(3 * C, device="cuda")
+        o = [torch.zeros(C, device="cuda") for _ in range(3)]
+        dz = (torch.empty(z.shape, device="cuda") if kind == "fp32"
+              else torch.empty((2,) + tuple(z.shape), device="cuda", dtype=torch.float16))
+        bound = torch.full((1,), -1, dtype=torch.int32, device="cuda")  # the reduce re-arms it
+        if nsplit == 1:
+            src = gbuf = d(gout)
+        else:
+            half = torch.randn(gout.shape, generator=torch.Generator().manual_seed(5))
+            src, gbuf = d(torch.stack([half, gout - half]).reshape(-1)), torch.empty(gout.shape, device="cuda")
+        C_.bn_bwd(src, nsplit, gbuf, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef, o[0], o[1],
+                  o[2], dz, pool, **({"bound": bound} if kind == "h2" else {}))
+        torch.cuda.synchronize()
+        outs.append((dz, coef, o, bound))
+    dz32, coef32, o32, _ = outs[0]
+    dzh, coefh, oh, bound = outs[1]
+    assert torch.equal(coef32, coefh) and all(torch.equal(a_, b_) for a_, b_ in zip(o32, oh))
+    B = float(bound.view(torch.float32).item())
+    s = 2.0 ** (14 - math.frexp(B)[1])
+    rec = (dzh[0].float().double() + dzh[1].float().double()) / s
+    assert B >= dz32.abs().max().item() > 0
+    assert dzh.float().abs().max().item() * 1.0 <= 2.0 ** 14 + 1
+    assert (rec - dz32.double()).abs().max().item() <= 2.0 ** -21 * dz32.abs().max().item()
+
+
 # ---------------------------------------------------------------- one-launch BN (bn_fused.hip)
 # VGG-11's tail at batch 256 (layers 2-7) and small odd batches; rmax 64 = the engine default
 FUSED_SHAPES = [(256, 8, 8, 256, False), (256, 8, 8, 256, True), (256, 4, 4, 512, False), (256, 4, 4, 512, True),
@@ -159,7 +231,7 @@ def _fused_ws(C_, shape, bwd, rmax):
 
 @pytest.mark.parametrize("shape", FUSED_SHAPES)
 @pytest.mark.parametrize("nsplit", [1, 3])
-@pytest.mark.parametrize("out_kind", ["planes", "fp32", "none"])
+@pytest.mark.parametrize("out_kind", ["planes", "fp32", "none", "h2"])
 def test_bn_fused_forward(shape, nsplit, out_kind):
     C_ = _C()
     N, H, W, C, pool = shape
@@ -183,6 +255,8 @@ def test_bn_fused_forward(shape, nsplit, out_kind):
         tmo = torch.zeros(1, dtype=torch.int32, device="cuda")
         if out_kind == "planes":
             a = torch.empty(3, *ref["a"].shape, device="cuda", dtype=torch.bfloat16)
+        elif out_kind == "h2":
+            a = torch.empty(2, *ref["a"].shape, device="cuda", dtype=torch.float16)
         elif out_kind == "fp32":
             a = torch.empty(ref["a"].shape, device="cuda")
         else:
@@ -199,15 +273,11 @@ def test_bn_fused_forward(shape, nsplit, out_kind):
         close(rv_d, ref["rv"], 1e-5, "running_var")
         assert int(nbt_d.item()) == 1
         if a is not None:
-            close(_planes_sum(a) if out_kind == "planes" else a, ref["a"], 1e-5, "a")
+            close(_planes_sum(a) if out_kind == "planes" else _h2_act(a) if out_kind == "h2" else a, ref["a"], 1e-5,
+                  "a")
         outs.append([t.clone() for t in (mean, invstd, scale, shift) + ((a,) if a is not None else ())])
     for x, y in zip(*outs):
         assert torch.equal(x, y), "one-launch BN forward is not deterministic"
-
-
-# channels) and small odd shapes; (256, 8, 8, 256) is beyond its register tile and must be refused
-COLS_SHAPES = [(256, 4, 4, 512, False), (256, 4, 4, 512, True), (256, 2, 2, 512, False), (256, 2, 2, 512, True),
-               (16, 2, 2, 512, True), (32, 4, 4, 64, True), (64, 2, 2, 96, False), (3, 6, 6, 16, True)]
 
 
 @pytest.mark.parametrize("shape", FUSED_SHAPES)

@@ -189,7 +189,7 @@ def test_augment_matches_reference():
         assert torch.equal(td.cpu(), tr)
 
 
-@pytest.mark.parametrize("impl", ["fp32", "x3"])
+@pytest.mark.parametrize("impl", ["fp32", "x3", "h2"])
 def test_engine_step_matches_torch(impl):
     """One full training step (fwd, CE, bwd) of the HIP engine vs torch autograd (fp64) on the
     reference module, from the same weights and data.  Both fp32 paths must match to fp32-level."""
@@ -276,7 +276,7 @@ def test_engine_trajectory_tracks_fp64():
         assert abs(a - c) <= 4.0 * abs(b - c) + 1e-4 * abs(c), (le, l32, l64)
 
 
-@pytest.mark.parametrize("impl", ["fp32", "x3", "bf16"])
+@pytest.mark.parametrize("impl", ["fp32", "x3", "bf16", "h2"])
 def test_engine_training_converges_and_evaluates(impl):
     """A few steps on a learnable synthetic set: loss goes down, eval runs, x3 tracks fp32 closely."""
     from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_cifar
@@ -393,7 +393,7 @@ def test_rccl_watchdog_tracks_and_retires_ops():
         c.all_reduce(t, "sum")
 
 
-@pytest.mark.parametrize("impl", ["fp32", "x3"])
+@pytest.mark.parametrize("impl", ["fp32", "x3", "h2"])
 def test_engine_eval_matches_torch_after_training(impl):
     """After real training steps (running stats moved, weights updated), the engine's eval forward
     equals stock torch eval on its exported state_dict."""
