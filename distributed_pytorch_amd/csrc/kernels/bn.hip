@@ -657,17 +657,22 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     // 16 partial rows per thread in flight (one memory latency for the engine's 512-row partials
     // instead of two); out-of-range rows add +0.f (exact: the sums start at +0), same order
     for (int k = grp; k < nblk; k += 16 * G) {
-      float pa[16], pb[16], px[16];
+      // (the maxima are loaded like the sums, without a branch: a conditional load per row would
+      // wait for each row's load in turn -- 16 memory latencies instead of one)
+      float pa[16], pb[16], px[16], pm[16], pz[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
+        // out-of-range rows load row 0 (always valid) and are masked after the load: no branch
         const bool v = k + G * u < nblk;
         const float* p = part + (long)(v ? k + G * u : 0) * Q * C + c;
-        pa[u] = v ? p[0] : 0.f;
-        pb[u] = v ? p[C] : 0.f;
-        px[u] = v ? p[2 * C] : 0.f;
-        if (Q == 5 && mx && v) {
-          mdy = fmaxf(mdy, p[3 * C]);
-          mz = fmaxf(mz, p[4 * C]);
+        const float l0 = p[0], l1 = p[C], l2 = p[2 * C];
+        pa[u] = v ? l0 : 0.f;
+        pb[u] = v ? l1 : 0.f;
+        px[u] = v ? l2 : 0.f;
+        if constexpr (Q == 5) {
+          const float l3 = p[3 * C], l4 = p[4 * C];
+          pm[u] = v ? l3 : 0.f;  // maxima of magnitudes: 0 is their identity
+          pz[u] = v ? l4 : 0.f;
         }
       }
 #pragma unroll
@@ -675,6 +680,10 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
         a += pa[u];
         b += pb[u];
         x += px[u];
+        if constexpr (Q == 5) {
+          mdy = fmaxf(mdy, pm[u]);
+          mz = fmaxf(mz, pz[u]);
+        }
       }
     }
   }
