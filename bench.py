@@ -36,6 +36,7 @@ from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_c
 from distributed_pytorch_amd.engine import VGGEngine  # noqa: E402
 from distributed_pytorch_amd.graph_step import GraphedStep  # noqa: E402
 from distributed_pytorch_amd.parallel import NullComm, init_env, make_sync  # noqa: E402
+from distributed_pytorch_amd.parallel.ipc import IpcComm  # noqa: E402
 from distributed_pytorch_amd.parallel.spawn import is_spawned_child  # noqa: E402
 from distributed_pytorch_amd.utils import benchlib  # noqa: E402
 from distributed_pytorch_amd.utils.profiling import EventProbe, step_comm_report  # noqa: E402
@@ -219,8 +220,6 @@ def ipc_comm(ctx, dev, engine, cache: dict, blocks: int = 0):
     """The peer-memory communicator over ctx.comm with the engine's arenas registered (collective).
     Plans with different workgroup budgets share it (``blocks`` is a per-collective launch size)."""
     if "ipc" not in cache:
-        from distributed_pytorch_amd.parallel.ipc import IpcComm
-
         store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
         c = IpcComm(ctx.comm, store, dev, timeout_s=20.0)
         c.prepare([engine.grads.flat, engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt])
@@ -228,18 +227,10 @@ def ipc_comm(ctx, dev, engine, cache: dict, blocks: int = 0):
     return cache["ipc"]
 
 
-def ipc_agrees(ipc, flat: torch.Tensor, dev) -> bool:
-    """All-reduce the gradient arena (as the last tuning step left it) through the peer kernel and,
-    from a copy, through the wrapped communicator; True when they agree to rounding."""
-    ref = flat.clone()
-    with ipc.region():
-        ipc.inner.all_reduce(ref)
-        ipc.all_reduce(flat)
-    ipc.wait()
-    torch.cuda.synchronize(dev)
-    err = (flat - ref).abs().max().item()
-    scale = ref.abs().max().item()
-    return err <= 1e-5 * max(scale, 1e-30) and not ipc.timed_out()
+def ipc_live_checks(ipc, engine, checks: list):
+    """After a diagnostic step: all-reduce the live gradient arena once more through the peer kernel
+    and check it through the store (IpcComm.verify_all_reduce); the verdicts go into the JSON."""
+    checks.append(ipc.verify_all_reduce(engine.grads.flat))
 
 
 def tune_comm(a, engine, sync, ctx, dev, batches):
@@ -251,7 +242,6 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     tuning steps draw their own batches and the training state is restored afterwards, so the
     run that follows is the same as without tuning."""
     from distributed_pytorch_amd.parallel.comm import RcclComm
-    from distributed_pytorch_amd.parallel.ipc import IpcComm
 
     if isinstance(ctx.comm, IpcComm):  # --ipc on: the transport is fixed
         return sync, None
@@ -298,13 +288,17 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
             el = ctx.all_max(time.perf_counter() - t0) / n * 1e3
             score[p] = min(score.get(p, el), el)
     # a plan whose peer-memory waits timed out (any rank), or whose all-reduce of the real gradient
-    # arena disagrees with the communicator's (beyond summation-order rounding), is disqualified
+    # arena fails the store-side agreement check (IpcComm.verify_all_reduce: same verdict on every
+    # rank), is disqualified
+    ipc_check = None
     if "ipc" in comms:
         bad = ctx.all_max(1.0 if comms["ipc"].timed_out() else 0.0) > 0
         if not bad:
-            bad = ctx.all_max(0.0 if ipc_agrees(comms["ipc"], engine.grads.flat, dev) else 1.0) > 0
+            ipc_check = comms["ipc"].verify_all_reduce(engine.grads.flat)
+            bad = not ipc_check["ok"]
         if bad:
-            print(f"[rank {ctx.rank}] comm tuner: IPC all-reduce timed out or disagreed; plan dropped", flush=True)
+            print(f"[rank {ctx.rank}] comm tuner: IPC all-reduce timed out or disagreed ({ipc_check}); plan dropped",
+                  flush=True)
             plans = [p for p in plans if not p[4]]
     # the first plan is the default: another one must beat it by 1 % (run-to-run noise of a few
     # steps), so the choice does not flap between equivalent plans
@@ -323,6 +317,7 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
             sy._bufs_fresh = False  # the next forward broadcasts rank 0's (restored) buffers again
     report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2],
                          "rccl_channels": best[3] or None, "ipc_blocks": best[4] or None},
+              "ipc_check": ipc_check,
               "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else "")
                               + (f"_ipc{p[4]}" if p[4] else ""): round(score[p], 4) for p in plans}}
     if best[4]:  # the peer-memory communicator carries the run from here on
@@ -383,8 +378,6 @@ def main(argv=None):
         ctx.barrier()
 
     if a.ipc == "on" and ipc_possible(ctx, dev):
-        from distributed_pytorch_amd.parallel.ipc import IpcComm
-
         store = ctx.store if ctx.store is not None else torch.distributed.distributed_c10d._get_default_store()
         ctx.comm = IpcComm(ctx.comm, store, dev)
     engine, sync, batches = build_parts(a, dev, ctx.rank, ctx.world, ctx.comm)
@@ -399,6 +392,7 @@ def main(argv=None):
     img_s = a.batch * ctx.world * a.steps / el
 
     diag = None
+    live = [] if isinstance(ctx.comm, IpcComm) else None
     if a.diag_steps > 0 and dev.type == "cuda":
         probe = EventProbe(dev)
         sync.probe = probe
@@ -409,6 +403,8 @@ def main(argv=None):
             probe.mark("start")
             step()
             samples.append(probe.times())
+            if live is not None:  # (after the step's own timing: the check re-reduces the arena)
+                ipc_live_checks(ctx.comm, engine, live)
         sync.probe = None
         sync.__dict__.pop("finish", None)  # drop make_step's probe wrapper
         diag = step_comm_report(samples, len(sync.buckets))
@@ -456,6 +452,11 @@ def main(argv=None):
             # communicator it wraps (0 with --comm ipc: no tensor byte through gloo / the host)
             "ipc_ops_by_kind": dict(ctx.comm.ops) if hasattr(ctx.comm, "ops") else None,
             "ipc_inner_tensor_ops": getattr(ctx.comm, "inner_tensor_ops", None),
+            # store-side agreement checks of the peer all-reduce on the live gradient arena, one per
+            # diagnostic step (None: no peer-memory communicator)
+            "ipc_live_check": (None if live is None else
+                               {"checks": len(live), "ok": all(c["ok"] for c in live),
+                                "max_rel_err": max((c["rel_err"] for c in live), default=None)}),
             "replicas_identical": pdiff == 0.0,
             "replica_param_max_diff": pdiff,
             "comm_diag": diag,

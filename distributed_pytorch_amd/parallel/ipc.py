@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import contextlib
 import datetime
+import json
 import os
 import time
 from collections import Counter
@@ -295,6 +296,46 @@ class IpcComm(Comm):
             self.inner.close()
         else:
             self.synchronize()
+
+    # ---- live agreement check ----
+    def verify_all_reduce(self, t: torch.Tensor, rtol: float = 1e-6) -> dict:
+        """Collective: all-reduce ``t`` (sum) through the peer kernel and check the result by a path
+        that shares nothing with the device collectives -- three float64 checksums per rank (sum,
+        a position-weighted sum, sum of magnitudes) through the store.  ``ok`` when every rank holds
+        the same result, its checksums equal the sums of the inputs' to rounding (``rtol`` of the
+        magnitude sum; an fp32 sum of W values is off by at most ~W 2^-24 of it), and no peer wait
+        timed out.  A stale or torn read of a peer's memory (a cross-GPU visibility failure)
+        changes the checksums by far more.  Every rank returns the same verdict.
+        DPA_IPC_TEST_DISAGREE=1 (tests only) corrupts the last rank's result first."""
+        n = t.numel()
+        w = getattr(self, "_vw", None)
+        if w is None or w.numel() < n:
+            # weights 1 .. 1.875 by a multiplicative hash of the index: a permutation of elements
+            # (a slice landing at the wrong offset) changes the weighted sum
+            idx = torch.arange(n, device=self.device, dtype=torch.int64)
+            w = self._vw = 1.0 + ((idx * 2654435761) % 8).double() / 8.0
+        wt = w[:n]
+
+        def sums(x):
+            xd = x.double()
+            return [float(xd.sum()), float((xd * wt).sum()), float(xd.abs().sum())]
+
+        cin = sums(t)
+        with self.region():
+            self.all_reduce(t)
+        self.wait()
+        torch.cuda.synchronize(self.device)
+        tmo = self.timed_out()
+        if os.environ.get("DPA_IPC_TEST_DISAGREE") == "1" and self.rank == self.world - 1:
+            t.view(-1)[0] += 1.0
+        cout = sums(t)
+        self._nreg += 1
+        rows = [json.loads(v) for v in self._exchange(f"verify{self._nreg}", json.dumps([cin, cout, tmo]).encode())]
+        same = all(r[1] == rows[0][1] for r in rows)
+        scale = max(sum(r[0][2] for r in rows), 1e-30)
+        err = max(abs(rows[0][1][k] - sum(r[0][k] for r in rows)) for k in range(2)) / scale
+        ok = same and not any(r[2] for r in rows) and err <= rtol
+        return {"ok": bool(ok), "ranks_identical": bool(same), "rel_err": err, "timed_out": any(r[2] for r in rows)}
 
     # ---- bootstrap check ----
     def _self_check(self) -> bool:

@@ -145,9 +145,9 @@ def test_ipc_collectives_ranks_share_one_gpu(world, stage, inbox):
     assert d["inner_tensor_ops"] == 0 and len(d["results"]) >= 12, d
 
 
-def _bench(args, script="bench.py", timeout=110):
+def _bench(args, script="bench.py", timeout=110, env_extra=None):
     cmd = [sys.executable, os.path.join(ROOT, script)] + args + ["--launch-timeout", str(timeout - 10)]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
     env.pop("WORLD_SIZE", None)
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -222,3 +222,30 @@ def test_ipc_ddp_matches_gloo(runs):
     assert d["replicas_identical"] is True and d["ipc_allreduce_ops"] and d["ipc_allreduce_ops"] > 0, d
     if "ddp" in runs:
         assert d["param_checksum"] == runs["ddp"]["param_checksum"], (d["param_checksum"], runs["ddp"]["param_checksum"])
+
+
+def test_ipc_live_agreement_checks():
+    """with the peer kernels carrying the run, every diagnostic step re-reduces
+    the live gradient arena and checks it through the store (checksums, nothing shared with the
+    device path); the verdicts are in the JSON."""
+    d = _bench(["--gpus", "2", "--comm", "ipc", "--mode", "ddp", "--steps", "2", "--warmup", "1", "--solo-steps", "0",
+                "--diag-steps", "3"])
+    chk = d["ipc_live_check"]
+    assert chk["checks"] == 3 and chk["ok"] is True and chk["max_rel_err"] < 1e-6, chk
+
+
+def test_ipc_forced_disagreement_drops_plan():
+    """a peer all-reduce that disagrees (injected: the last rank's result is
+    corrupted before the check) makes the comm tuner drop every IPC plan on every rank -- the run
+    finishes on the wrapped communicator, replicas identical, no hang -- and a live check reports
+    the failure instead of raising."""
+    env = {"DPA_IPC_TEST_DISAGREE": "1"}
+    d = _bench(["--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc", "auto", "--steps", "2", "--warmup", "1",
+                "--solo-steps", "0", "--diag-steps", "0", "--comm-tune-steps", "1"], env_extra=env, timeout=200)
+    tune = d["config"]["comm_tune"]
+    assert tune is not None and tune["ipc_check"] is not None and tune["ipc_check"]["ok"] is False, tune
+    assert tune["chosen"]["ipc_blocks"] is None and not any("ipc" in k for k in tune["ms_per_step"]), tune
+    assert d["replicas_identical"] is True, d
+    d2 = _bench(["--gpus", "2", "--comm", "ipc", "--mode", "ddp", "--steps", "2", "--warmup", "1", "--solo-steps", "0",
+                 "--diag-steps", "1"], env_extra=env)
+    assert d2["ipc_live_check"]["ok"] is False and d2["ipc_live_check"]["checks"] == 1, d2["ipc_live_check"]
