@@ -249,6 +249,7 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
                        ipc=a.ipc == "auto" and ipc_possible(ctx, dev))
     if ctx.world <= 1 or a.comm_tune == "off" or len(plans) < 2 or a.no_overlap:
         return sync, None
+    t_tune = time.perf_counter()
     it = batches()
     snap = [t.clone() for t in (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt,
                                 engine.loss_accum)]
@@ -318,6 +319,8 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2],
                          "rccl_channels": best[3] or None, "ipc_blocks": best[4] or None},
               "ipc_check": ipc_check,
+              # the whole tuner (communicator creation, every plan, the agreement check), max over ranks
+              "tune_seconds": round(ctx.all_max(time.perf_counter() - t_tune), 3),
               "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else "")
                               + (f"_ipc{p[4]}" if p[4] else ""): round(score[p], 4) for p in plans}}
     if best[4]:  # the peer-memory communicator carries the run from here on
