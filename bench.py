@@ -410,6 +410,7 @@ def main(argv=None):
                 ipc_live_checks(ctx.comm, engine, live)
         sync.probe = None
         sync.__dict__.pop("finish", None)  # drop make_step's probe wrapper
+        engine.check_signals()  # (the diagnostic steps' bounded waits too)
         diag = step_comm_report(samples, len(sync.buckets))
         diag["exposed_comm_ms"] = ctx.all_max(diag["exposed_comm_ms"] or 0.0)
     benchlib.device_barrier(ctx, dev)

@@ -249,3 +249,35 @@ def test_ipc_forced_disagreement_drops_plan():
     d2 = _bench(["--gpus", "2", "--comm", "ipc", "--mode", "ddp", "--steps", "2", "--warmup", "1", "--solo-steps", "0",
                  "--diag-steps", "1"], env_extra=env)
     assert d2["ipc_live_check"]["ok"] is False and d2["ipc_live_check"]["checks"] == 1, d2["ipc_live_check"]
+
+
+def test_ipc_allreduce_stress_ranks_share_one_gpu():
+    """The training pattern on the peer all-reduce, 300 times with new data each time (a kernel on
+    the compute stream rewrites the registered arena, the collective runs right behind it, the next
+    iteration overlaps): every sum exact (tests/ipc_stress_worker.py)."""
+    from distributed_pytorch_amd.parallel.spawn import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "ipc_stress_worker.py")]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DPA_IPC_STRESS_ITERS="300")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPA_STORE_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = [json.loads(l) for l in r.stdout.replace("}{", "}\n{").splitlines() if l.startswith("{")]
+    assert len(rows) == 4 and all(d["bad_iters"] == 0 and not d["timeout"] for d in rows), rows
+
+
+def test_four_rank_training_is_run_to_run_deterministic():
+    """Regression test of the round-5 stream-event finding: four DDP ranks sharing one GPU on the
+    peer kernels, the same run three times -- bitwise the same parameters every time.  With
+    device-scope cross-stream events (hipEventReleaseToDevice) ~30 % of such runs computed a step
+    from partly stale data (utils/streams.py)."""
+    sums = set()
+    for _ in range(3):
+        d = _bench(["--gpus", "4", "--comm", "ipc", "--mode", "ddp", "--steps", "3", "--warmup", "2",
+                    "--solo-steps", "0", "--diag-steps", "0", "--batch", "64"])
+        assert d["replicas_identical"] is True, d
+        sums.add(d["param_checksum"])
+    assert len(sums) == 1, sums
