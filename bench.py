@@ -79,9 +79,11 @@ def parse(argv=None):
                          "tail bucket, per-bucket update inside backward) on the real fabric and keep the fastest "
                          "(max over ranks, so every rank picks the same plan); off = --bucket-mb / defaults")
     ap.add_argument("--comm-tune-steps", type=int, default=8, help="timed steps per plan and repetition")
-    ap.add_argument("--ipc", default="auto", choices=["auto", "on", "off"],
-                    help="N>1 on one node: bucket all-reduces on the peer-memory kernel (parallel/ipc.py). "
-                         "auto = one more comm-tuner plan; on = always (any --comm; several ranks may share a GPU)")
+    ap.add_argument("--ipc", default="off", choices=["auto", "on", "off"],
+                    help="N>1 on one node: collectives on the peer-memory kernels (parallel/ipc.py). auto = "
+                         "extra comm-tuner plans; on = always (any --comm; several ranks may share a GPU); off "
+                         "(default): ranks sharing one GPU through them are not run-to-run reproducible "
+                         "(docs/PERF_NOTES.md round 5), so the default path is RCCL")
     ap.add_argument("--ipc-blocks", default="32,16,64",
                     help="workgroups per rank of the peer-memory collectives the comm tuner tries (comma list; the "
                          "first is the --ipc on / --comm ipc default unless DPA_IPC_BLOCKS is set)")

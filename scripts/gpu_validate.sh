@@ -11,6 +11,10 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 gpurun_out/val_smoke.log
 timeout -k 10 150 python bench.py --steps 50 --warmup 10 > gpurun_out/val_bench.log 2>&1 || { tail -20 gpurun_out/val_bench.log; exit 1; }
 tail -1 gpurun_out/val_bench.log
+timeout -k 10 150 python bench.py --steps 20 --warmup 5 > gpurun_out/val_bench_driver.log 2>&1 || { tail -20 gpurun_out/val_bench_driver.log; exit 1; }
+tail -1 gpurun_out/val_bench_driver.log
+timeout -k 10 300 python bench.py --steps 50 --warmup 10 --torch-baseline 30 > gpurun_out/val_bench_torch.log 2>&1 || { tail -20 gpurun_out/val_bench_torch.log; exit 1; }
+tail -1 gpurun_out/val_bench_torch.log
 DPA_FORCE_COMM=1 timeout -k 10 150 python bench.py --steps 50 --warmup 10 > gpurun_out/val_bench_rccl1.log 2>&1 || { tail -20 gpurun_out/val_bench_rccl1.log; exit 1; }
 tail -1 gpurun_out/val_bench_rccl1.log
 timeout -k 10 200 python bench_resnet.py --steps 20 --warmup 5 > gpurun_out/val_resnet.log 2>&1 || { tail -20 gpurun_out/val_resnet.log; exit 1; }
