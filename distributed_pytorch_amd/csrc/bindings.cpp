@@ -117,8 +117,10 @@ void chk(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " failed: rc=", rc, (rc > 0 ? std::string(" ") + hipGetErrorString((hipError_t)rc) : ""));
 }
 
-// Cross-stream dependency event with caller-chosen flags (utils/streams.py: timing disabled, the
-// default system-scope release -- device-scope records were found to let consumers read stale data).
+// Cross-stream dependency event with caller-chosen flags.  torch.cuda.Event records with a
+// system-scope release (L2 writeback + invalidate at every record); dependencies between streams of
+// ONE device only need device scope (hipEventReleaseToDevice), which keeps L2 warm and lets the
+// next kernel on the recording stream start sooner.
 struct DevEvent {
   hipEvent_t ev{};
   explicit DevEvent(int64_t flags) {

@@ -32,10 +32,10 @@ int RcclComm::version() {
 }
 
 namespace {
-// Fence / completion events (stream ordering, and the watchdog's view of completion) record with the
-// default system-scope release: device-scope records (hipEventReleaseToDevice) let a consumer stream
-// read stale data on MI355X (utils/streams.py, docs/PERF_NOTES.md round 5), at no measured gain.
-unsigned event_flags() { return hipEventDisableTiming; }
+// Fence / completion events only order streams of this device (and let the watchdog observe
+// completion), so they record with a device-scope release: a system-scope one writes back and
+// invalidates L2 under the compute kernels running beside the collective.
+unsigned event_flags() { return hipEventDisableTiming | hipEventReleaseToDevice; }
 }  // namespace
 
 RcclComm::RcclComm(int rank, int world, const std::string& uid, int device, hipStream_t comm_stream,

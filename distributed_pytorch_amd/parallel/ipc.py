@@ -86,7 +86,6 @@ class IpcComm(Comm):
         self.ops: Counter = Counter()
         self.inner_tensor_ops = 0  # collectives handed to the wrapped communicator after creation
         self.side = None
-        self._sysev = None
         if self.inner is None and self.device.type == "cuda":
             self.side = torch.cuda.Stream(self.device)
             self._join_in, self._join_out = StreamJoin(), StreamJoin()
@@ -173,18 +172,6 @@ class IpcComm(Comm):
         return (t.is_cuda and t.is_contiguous() and (t.numel() * t.element_size()) % 4 == 0
                 and t.data_ptr() % 4 == 0)
 
-    def _release(self):
-        """System-scope release on the current stream, right before a collective kernel: peers read
-        this rank's memory directly, so everything the compute kernels wrote must have left every
-        XCD's L2 first.  The framework's own stream dependencies are device-scope events
-        (utils/streams.py), and the kernel's per-block release fence only writes back the L2 of the
-        XCD its block runs on -- lines another XCD still holds dirty (written by an earlier kernel)
-        would reach a peer stale.  A torch event records with a system-scope release (the whole
-        device's L2 written back); its cost is one cache writeback per collective."""
-        if self._sysev is None:
-            self._sysev = torch.cuda.Event()
-        self._sysev.record(torch.cuda.current_stream(self.device))
-
     def _guard(self):
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("IpcComm collectives cannot be captured in a HIP graph (per-launch signal epochs)")
@@ -228,7 +215,6 @@ class IpcComm(Comm):
             return self._inner(f"all_reduce({op}, {t.dtype})").all_reduce(t, op)
         self._guard()
         rid, off = self._loc(t)
-        self._release()
         self._c.all_reduce(rid, off, t, _RED[o], self.blocks, self._tmo_us)
         self.ops["all_reduce" if rid >= 0 else "all_reduce_bounced"] += 1
         if op == "avg":
@@ -245,7 +231,6 @@ class IpcComm(Comm):
             return self._inner(f"broadcast({t.dtype})").broadcast(t, root)
         self._guard()
         rid, off = self._loc(t)
-        self._release()
         self._c.broadcast(rid, off, t, int(root), self.blocks, self._tmo_us)
         self.ops["broadcast"] += 1
 
@@ -254,7 +239,6 @@ class IpcComm(Comm):
             return self._inner("gather").gather(send, recv, root)
         self._guard()
         rid, off = self._loc(send)
-        self._release()
         self._c.gather(rid, off, send, recv if self.rank == root else None, int(root), self.blocks, self._tmo_us)
         self.ops["gather"] += 1
 
@@ -264,7 +248,6 @@ class IpcComm(Comm):
             return self._inner("reduce_scatter").reduce_scatter(send, recv, op)
         self._guard()
         rid, off = self._loc(send)
-        self._release()
         self._c.reduce_scatter(rid, off, send, recv, _RED[op], self.blocks, self._tmo_us)
         self.ops["reduce_scatter"] += 1
 
@@ -273,7 +256,6 @@ class IpcComm(Comm):
             return self._inner("all_gather").all_gather(send, recv)
         self._guard()
         rid, off = self._loc(send)
-        self._release()
         self._c.all_gather(rid, off, send, recv, self.blocks, self._tmo_us)
         self.ops["all_gather"] += 1
 
@@ -290,7 +272,6 @@ class IpcComm(Comm):
             return
         self._guard()
         with self.region():
-            self._release()
             self._c.barrier(self.blocks, self._tmo_us)
         self.ops["barrier"] += 1
         self.wait()

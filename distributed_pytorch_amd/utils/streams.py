@@ -1,13 +1,12 @@
 """Cross-stream dependencies between the compute, wgrad and comm HIP streams of one GPU.
 
-Events record with the default (system-scope) release.  Rounds 2-4 recorded them with a
-device-scope release (hipEventReleaseToDevice: no L2 writeback at the record), measured neutral
-to +1 % at the time.  Round 5 found it unsafe on MI355X: with four ranks sharing one GPU through the
-peer-memory collectives, ~30 % of runs computed the first layer of a step from partly stale input
-(15-17 of conv0's 256 workgroups produced different output for the same input and weights,
-after the compute stream had waited on a device-scope event of the comm stream); with system-scope
-events 10 of 10 runs were bitwise identical, at the same speed (1 GPU: 222.4k vs 222.3k img/s, 1-rank
-RCCL: 217.9k vs 217.8k; docs/PERF_NOTES.md round 5).
+``torch.cuda.Event`` records with a system-scope release: every record writes back and
+invalidates L2, and the next kernel on the recording stream starts only after that (measured with
+``tools/event_overhead.py``).  The step's dependencies are all between streams of one device, so
+the framework records native events (``_C.DevEvent``) with a device-scope release instead.
+
+(hipEventReleaseToDevice; torch events and hipEventDisableSystemFence were measured slower,
+docs/PERF_NOTES.md.)
 """
 from __future__ import annotations
 
@@ -15,11 +14,11 @@ from typing import Optional
 
 import torch
 
-
 def _native_flags() -> Optional[int]:
     from .. import _ext
 
-    return _ext.require().EVENT_DISABLE_TIMING
+    C = _ext.require()
+    return C.EVENT_DISABLE_TIMING | C.EVENT_RELEASE_TO_DEVICE
 
 
 class DevEvent:
