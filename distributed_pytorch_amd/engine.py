@@ -247,6 +247,12 @@ class VGGEngine:
         self.ksig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None
         self.bsig = torch.zeros(len(L), dtype=torch.int32, device=dev) if self.ksignal else None  # BN bwd starts
         self.ksig_tmo = torch.zeros(1, dtype=torch.int32, device=dev) if self.ksignal else None
+        # the end-of-backward join (main waits for the wgrad stream) as a signal too: a one-wave
+        # kernel on the wgrad stream stores the epoch, the main stream polls it -- an event wait on
+        # the main stream idles it ~13 us even when the wgrad stream has long finished
+        # (profiles/r5_h2_step_timeline.txt: the gap in front of sgd_flat).  DPA_SIGNAL_JOIN=0: event.
+        self.jsig = (torch.zeros(1, dtype=torch.int32, device=dev)
+                     if self.ksignal and os.environ.get("DPA_SIGNAL_JOIN", "1") == "1" else None)
         self._sig_epoch = 0
         # A wait may legitimately last as long as the main stream is held behind the previous step's
         # collectives (a slow peer: up to the communicator's DPA_COMM_TIMEOUT, after which the RCCL
@@ -713,6 +719,10 @@ class VGGEngine:
                 K.bn_apply(z, self._act_out(i, n), st["scale"], st["shift"], l.pool)
                 continue
             erows = self._epi_rows(i, n)
+            if erows and self.epart.numel() < 2 * ((n * l.hw * l.hw + erows - 1) // erows) * l.cout:
+                # a conv plan changed after construction (tools/tune_step.py): more partial rows
+                self.epart = torch.empty(2 * ((n * l.hw * l.hw + erows - 1) // erows) * l.cout,
+                                         dtype=torch.float32, device=self.device)
             ns = self._conv_fwd(i, x, n, reduce=False, stats=self.epart if erows else None)
             if buffers_wait is not None:  # BN buffers (being broadcast) are first touched here
                 buffers_wait()
@@ -798,7 +808,7 @@ class VGGEngine:
             if side_later is not None:
                 side_work(*side_later)
                 side_later = None
-            self._join(main, ws)
+            self._end_join(main, ws, epoch)
             joined = True
 
         def after_bn(i: int):
@@ -901,9 +911,18 @@ class VGGEngine:
         if side_later is not None:
             side_work(*side_later)
         if ws is not None and not joined:
-            self._join(main, ws)
+            self._end_join(main, ws, epoch)
         self._eval_dirty = True
         return self.loss
+
+    def _end_join(self, main, ws, epoch: int):
+        """The main stream waits for everything queued so far on the wgrad stream."""
+        if self.jsig is None or not epoch:
+            self._join(main, ws)
+            return
+        with torch.cuda.stream(ws):
+            self.K.set_signal(self.jsig, epoch)
+        self.K.wait_signal(self.jsig, epoch, self.ksig_timeout_us, self.ksig_tmo)
 
     def sgd_step(self, grad_scale: float = 1.0, offset: int = 0, count: int = -1, first: Optional[bool] = None):
         """Fused SGD over the arena (or the [offset, offset+count) slice of it)."""
