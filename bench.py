@@ -114,7 +114,8 @@ def build_parts(a, dev, rank, world, comm):
     loader = DeviceLoader(train, a.batch, dev, sampler=sampler, train=True, seed=7919 + rank, drop_last=True)
     engine = VGGEngine(a.model, dev, max_batch=a.batch, impl=a.impl)
     engine.init_parameters(seed=1)
-    sync = make_sync(a.mode, engine, comm, bucket_mb=a.bucket_mb, overlap=not a.no_overlap)
+    sync = make_sync(a.mode, engine, comm, bucket_mb=a.bucket_mb, overlap=not a.no_overlap,
+                     tail_mb=float(os.environ.get("DPA_TAIL_MB", "2.0")))  # (env: A/B of the tail bucket)
 
     def batches():
         ep = 0
