@@ -16,7 +16,9 @@ it, runs of several processes sharing ONE GPU are not run-to-run reproducible on
 docs/PERF_NOTES.md round 5, tracked by test_four_rank_training_run_to_run).  Serialised, 22 of 23
 runs of the four modes at W=2 (gloo and peer kernels) and W=4 (peer kernels) were bitwise identical
 and the 23rd differed by 2e-6 of the checksum (unserialised misses move it by ~1-2 %), so the
-cross-mode checks allow 1e-4 of the checksum (RTOL): a wrong sync mode is off by far more."""
+cross-mode checks allow 1e-4 of the checksum (RTOL); serialised misses still occur now and then (one
+W=2 gloo run 0.3 % off in a later suite), so a run off the majority is re-run once and must then
+agree (_agree): a wrong sync mode reproduces its error, the platform's misses do not."""
 import json
 import os
 import subprocess
@@ -34,6 +36,21 @@ RTOL = 1e-4
 
 def _same(a, b):
     return abs(a - b) <= RTOL * abs(b)
+
+
+def _agree(sums, rerun):
+    """The cross-mode oracle over {label: checksum}: every run within RTOL of the majority value.
+    A run off the majority is re-run ONCE and must then agree: the engine is deterministic, so a
+    wrong sync mode reproduces its error, while the platform's multi-process misses (module
+    docstring) do not repeat on the same run.  Returns the labels that needed the re-run."""
+    vals = list(sums.values())
+    best = max(vals, key=lambda v: sum(_same(u, v) for u in vals))
+    assert sum(_same(u, best) for u in vals) >= 2, sums
+    redo = [k for k, v in sums.items() if not _same(v, best)]
+    for k in redo:
+        v = rerun(k)
+        assert _same(v, best), (k, sums[k], v, best, sums)
+    return redo
 
 
 def _run(mode):
@@ -69,7 +86,7 @@ def test_modes_agree(runs):
     if len(runs) < len(MODES):
         pytest.skip("needs every mode's run")
     sums = {m: runs[m]["param_checksum"] for m in MODES}
-    assert all(_same(v, sums["allreduce"]) for v in sums.values()), sums
+    _agree(sums, lambda m: _run(m)["param_checksum"])
 
 
 def test_four_ranks_ddp_share_one_gpu():
@@ -182,6 +199,12 @@ def ipc_runs():
     return {}
 
 
+def _ipc_run(mode, world):
+    return _bench(["--gpus", str(world), "--comm", "ipc", "--mode", mode, "--steps", "3", "--warmup", "2",
+                   "--solo-steps", "0", "--diag-steps", "1"] + (["--batch", "64"] if world > 2 else []),
+                  env_extra=SERIAL)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("mode", MODES)
 def test_modes_on_peer_kernels(ipc_runs, mode, world):
@@ -189,8 +212,7 @@ def test_modes_on_peer_kernels(ipc_runs, mode, world):
     ipc: mode A's gather -> mean -> broadcast, DDP's bucket all-reduces and BN-buffer broadcasts,
     ZeRO-1's reduce-scatter / all-gather, the start-up broadcast): replicas bitwise identical, and no
     tensor byte through gloo or the host (the communicator wraps nothing)."""
-    d = _bench(["--gpus", str(world), "--comm", "ipc", "--mode", mode, "--steps", "3", "--warmup", "2",
-                "--solo-steps", "0", "--diag-steps", "1"] + (["--batch", "64"] if world > 2 else []), env_extra=SERIAL)
+    d = _ipc_run(mode, world)
     ipc_runs[(mode, world)] = d
     assert d["n_gpus"] == world and d["config"]["sync_mode"] == mode and d["config"]["comm"] == "ipc-standalone", d
     assert d["replicas_identical"] is True and d["replica_param_max_diff"] == 0.0, d
@@ -206,11 +228,11 @@ def test_peer_kernel_modes_agree(ipc_runs, runs):
     need = [(m, w) for m in MODES for w in (2, 4)]
     if not all(k in ipc_runs for k in need) or not runs:
         pytest.skip("needs every mode's run")
-    ref = runs[sorted(runs)[0]]["param_checksum"]  # W=2 gloo (every mode the same)
-    w2 = {m: ipc_runs[(m, 2)]["param_checksum"] for m in MODES}
-    assert all(_same(v, ref) for v in w2.values()), (ref, w2)
+    w2 = {("ipc", m): ipc_runs[(m, 2)]["param_checksum"] for m in MODES}
+    w2.update({("gloo", m): d["param_checksum"] for m, d in runs.items()})
+    _agree(w2, lambda k: (_ipc_run(k[1], 2) if k[0] == "ipc" else _run(k[1]))["param_checksum"])
     w4 = {m: ipc_runs[(m, 4)]["param_checksum"] for m in MODES}
-    assert all(_same(v, w4["allreduce"]) for v in w4.values()), w4
+    _agree(w4, lambda m: _ipc_run(m, 4)["param_checksum"])
 
 
 def test_ddp_eight_ranks_share_one_gpu():
@@ -233,11 +255,15 @@ def test_ipc_ddp_matches_gloo(runs):
     """Bucketed DDP with the collectives on the peer-memory kernels wrapped around the gloo
     communicator (--ipc on, 2 ranks on one GPU): replicas identical and -- a sum of two is exact in
     any order -- the parameters of the gloo run of the same mode (to RTOL, module docstring)."""
-    d = _bench(["--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc", "on", "--steps", "3", "--warmup", "2",
-                "--solo-steps", "0", "--diag-steps", "1"], env_extra=SERIAL)
+    args = ["--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc", "on", "--steps", "3", "--warmup", "2",
+            "--solo-steps", "0", "--diag-steps", "1"]
+    d = _bench(args, env_extra=SERIAL)
     assert d["replicas_identical"] is True and d["ipc_allreduce_ops"] and d["ipc_allreduce_ops"] > 0, d
-    if "ddp" in runs:
-        assert _same(d["param_checksum"], runs["ddp"]["param_checksum"]), (d["param_checksum"], runs["ddp"])
+    if "ddp" in runs and not _same(d["param_checksum"], runs["ddp"]["param_checksum"]):
+        # one re-run of each side (see _agree): a real difference reproduces
+        again = _bench(args, env_extra=SERIAL)["param_checksum"]
+        ref = _run("ddp")["param_checksum"]
+        assert _same(again, ref), (d["param_checksum"], again, runs["ddp"]["param_checksum"], ref)
 
 
 def test_ipc_live_agreement_checks():
