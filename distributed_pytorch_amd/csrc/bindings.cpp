@@ -94,6 +94,11 @@ int dpa_bn_fused_bwd(const float* gsrc, int nsplit, const float* z, int N, int H
                      int sig_val);
 
 int dpa_set_signal(int* sig, int val, hipStream_t st);
+int dpa_health_copy(const int* const* w, int n, int* out, int tag, hipStream_t st);
+int* dpa_h2_ovf_conv_addr();
+int* dpa_h2_ovf_bn_addr();
+int* dpa_h2_ovf_sgd_addr();
+int* dpa_h2_ovf_fused_addr();
 int dpa_bn_apply_wide(const unsigned short* z, const unsigned short* res, unsigned short* out, unsigned char* mask,
                       const float* scale, const float* shift, long M, int C, int act, hipStream_t st,
                       const float* rscale, const float* rshift);
@@ -205,6 +210,32 @@ void wait_signal(Tensor sig, int64_t val, int64_t timeout_us, Tensor tmo) {
 
 void set_signal(Tensor sig, int64_t val) {
   chk(dpa_set_signal(signal_ptr(sig, "set_signal"), (int)val, cur_stream()), "set_signal");
+}
+
+// device addresses of the fp16-pair overflow words of every kernel file (per-step health snapshot)
+std::vector<int64_t> h2_overflow_addrs() {
+  std::vector<int64_t> out;
+  for (int* (*f)() : {dpa_h2_ovf_conv_addr, dpa_h2_ovf_bn_addr, dpa_h2_ovf_sgd_addr, dpa_h2_ovf_fused_addr}) {
+    int* p = f();
+    TORCH_CHECK(p != nullptr, "h2_overflow_addrs: hipGetSymbolAddress failed");
+    out.push_back(reinterpret_cast<int64_t>(p));
+  }
+  return out;
+}
+
+// ptrs: int64 GPU tensor of n word addresses; out: pinned host int32 tensor of >= 64 words.  One
+// one-wave kernel on the current stream copies the words (and `tag` into out[63]).
+void health_copy(Tensor ptrs, Tensor out, int64_t tag) {
+  TORCH_CHECK(ptrs.is_cuda() && ptrs.scalar_type() == at::kLong && ptrs.is_contiguous() && ptrs.numel() <= 63,
+              "health_copy: ptrs must be a contiguous int64 GPU tensor of <= 63 addresses");
+  TORCH_CHECK(!out.is_cuda() && out.is_pinned() && out.scalar_type() == at::kInt && out.is_contiguous() &&
+                  out.numel() >= 64,
+              "health_copy: out must be a pinned host int32 tensor of >= 64 words");
+  void* dptr = nullptr;
+  chk((int)hipHostGetDevicePointer(&dptr, out.data_ptr(), 0), "health_copy: hipHostGetDevicePointer");
+  chk(dpa_health_copy(reinterpret_cast<const int* const*>(ptrs.data_ptr()), (int)ptrs.numel(), static_cast<int*>(dptr),
+                      (int)tag, cur_stream()),
+      "health_copy");
 }
 
 void spin(int64_t usec, Tensor done) {
@@ -1104,6 +1135,7 @@ class PyIpcComm {
   PyIpcComm(int rank, int world, int device, int64_t stage_words, int64_t inbox_words)
       : c_(rank, world, device, (long)stage_words, (long)inbox_words) {}
   py::bytes sig_handle() { return py::bytes(c_.sig_handle()); }
+  int64_t tmo_ptr() { return reinterpret_cast<int64_t>(c_.tmo_word()); }
   py::bytes stage_handle() { return py::bytes(c_.stage_handle()); }
   py::bytes inbox_handle() { return py::bytes(c_.inbox_handle()); }
   static py::bytes tensor_handle(const Tensor& t) {
@@ -1187,6 +1219,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("sig_val") = 0, py::arg("oscale") = 1.0, py::arg("obound") = py::none());
   m.def("wait_signal", &wait_signal, py::arg("sig"), py::arg("val"), py::arg("timeout_us"), py::arg("tmo"));
   m.def("set_signal", &set_signal, py::arg("sig"), py::arg("val"));
+  m.def("h2_overflow_addrs", &h2_overflow_addrs);
+  m.def("health_copy", &health_copy, py::arg("ptrs"), py::arg("out"), py::arg("tag"));
   m.def("split_planes", &split_planes, py::arg("x"), py::arg("out"), py::arg("scale") = 1.0);
   m.def("h2_overflow", &h2_overflow, py::arg("clear") = false);
   m.attr("H2_SW") = 256.0;  // fp16-pair plane scales (kernels/common.h)
@@ -1299,6 +1333,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<int, int, int, int64_t, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("stage_words"), py::arg("inbox_words"))
       .def("sig_handle", &PyIpcComm::sig_handle)
+      .def("tmo_ptr", &PyIpcComm::tmo_ptr)
       .def("stage_handle", &PyIpcComm::stage_handle)
       .def("inbox_handle", &PyIpcComm::inbox_handle)
       .def_static("tensor_handle", &PyIpcComm::tensor_handle)

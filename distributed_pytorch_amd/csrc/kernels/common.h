@@ -124,6 +124,11 @@ __device__ __forceinline__ void split_val(float v, u16* o, float s = 1.f) {
       (void)hipMemcpyToSymbol(HIP_SYMBOL(g_h2_ovf), &z, sizeof(int));              \
     }                                                                              \
     return v;                                                                      \
+  }                                                                                \
+  extern "C" int* fn##_addr() {                                                    \
+    void* p = nullptr;                                                             \
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_h2_ovf)) != hipSuccess) return nullptr; \
+    return static_cast<int*>(p);                                                   \
   }
 
 // ---- deterministic split-K reduction: out[i] = sum_k slabs[k * n4 + i] over float4 elements ----

@@ -57,7 +57,9 @@ __device__ __forceinline__ void ipc_barrier(const DpaIpcArgs& a, int phase) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t < 64) {
-    if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: visible to every peer
+    // every lane that stores a flag or polls one runs the fences itself (system scope: visible to
+    // every peer), so the ordering does not depend on a fence in lane 0 acting for the whole wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (t < a.world && t != a.rank)
       __hip_atomic_store((gu32*)(a.sig[t] + (phase * DPA_IPC_MAXW + a.rank) * DPA_IPC_MAXB + b), a.epoch,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -72,7 +74,7 @@ __device__ __forceinline__ void ipc_barrier(const DpaIpcArgs& a, int phase) {
         __builtin_amdgcn_s_sleep(2);
       }
     }
-    if (t == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
 }

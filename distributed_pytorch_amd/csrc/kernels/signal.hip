@@ -33,6 +33,22 @@ __global__ __launch_bounds__(64) void wait_signal_kernel(const int* __restrict__
 // a kernel that only signals (tests; and a producer stream whose next kernel cannot carry it)
 __global__ __launch_bounds__(64) void set_signal_kernel(int* __restrict__ sig, int val) { start_signal(sig, val); }
 
+// Per-step health snapshot (engine.py VGGEngine.health_mark): lane i copies the device word *w[i]
+// (an fp16-pair overflow word, a bounded-wait timeout word, a peer-collective timeout word) into
+// out[i] -- pinned host memory, read by the host once the step's event has completed, so a step
+// that went wrong fails the run one step later without a synchronising read inside the step.
+// The words were written by kernels ordered before this one (stream order, or the joins that
+// precede the optimizer step), so plain agent-scope loads see them.
+__global__ __launch_bounds__(64) void health_kernel(const int* const* __restrict__ w, int n, int* __restrict__ out,
+                                                    int tag) {
+  const int t = threadIdx.x;
+  if (t < n) {
+    const int* p = w[t];
+    out[t] = p != nullptr ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  }
+  if (t == 63) out[63] = tag;  // which step this slot describes
+}
+
 }  // namespace
 
 extern "C" {
@@ -48,6 +64,13 @@ int dpa_wait_signal(const int* sig, int val, long long timeout_us, int* tmo, hip
 
 int dpa_set_signal(int* sig, int val, hipStream_t st) {
   set_signal_kernel<<<1, 64, 0, st>>>(sig, val);
+  return (int)hipGetLastError();
+}
+
+// w: device array of n (<= 63) word pointers; out: 64 ints of host-pinned (device-mapped) memory
+int dpa_health_copy(const int* const* w, int n, int* out, int tag, hipStream_t st) {
+  if (n < 0 || n > 63) return -2;
+  health_kernel<<<1, 64, 0, st>>>(w, n, out, tag);
   return (int)hipGetLastError();
 }
 }  // extern "C"

@@ -67,6 +67,8 @@ class IpcComm {
   void all_gather(int rid, long off, const void* in, void* out, long n, int blocks, long long tmo_us,
                   hipStream_t st);
   void barrier(int blocks, long long tmo_us, hipStream_t st);
+  // the device word a timed-out peer wait raises (per-step health snapshot reads it)
+  int* tmo_word() const { return tmo_; }
 
   // [offset, words) pieces of a collective of n words (one rank's words for gather / reduce-scatter /
   // all-gather): the piece sizes the staging buffer and the inbox allow, multiples of 4 words

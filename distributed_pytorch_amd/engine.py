@@ -340,6 +340,13 @@ class VGGEngine:
         self.correct = torch.zeros(N, dtype=torch.int32, device=dev)
         self.eval_acc = torch.zeros(2, **f32)
         self._eval_dirty = True
+        self.health = (dev.type == "cuda" and hasattr(self.K, "health_copy")
+                       and os.environ.get("DPA_STEP_HEALTH", "1") == "1")
+        self._health_extra: List[tuple] = []
+        self._health_ptrs = None
+        self._health_out = None
+        self._health_slot = 0
+        self._health_pending = [False, False]
         self.init_parameters(seed=None)
 
     def _make_wgrad_stream(self, dev: torch.device):
@@ -939,6 +946,7 @@ class VGGEngine:
     def check_signals(self):
         """Raise if a wgrad-stream wait gave up (its producer's signal never arrived: the weight
         gradients of that step were computed from an unfinished BN backward).  Synchronises."""
+        self.health_flush()
         if self.ksig_tmo is not None and int(self.ksig_tmo.item()) != 0:
             raise RuntimeError("VGGEngine: a wgrad-stream signal wait timed out "
                                f"(DPA_KSIGNAL_TIMEOUT_US={self.ksig_timeout_us}); weight gradients are invalid")
@@ -954,6 +962,72 @@ class VGGEngine:
     def finish_step(self):
         self.steps_taken += 1
         self._eval_dirty = True
+        self.health_mark()
+
+    # ------------------------------------------------------------------ per-step health
+    # Every step ends with a one-wave kernel (signal.hip health_kernel) that copies the device-side
+    # error words -- the fp16-pair overflow words of every kernel file, the wgrad-stream wait
+    # timeout, the one-launch BN rendezvous timeout, and any word a communicator registered
+    # (add_health_word: the peer-collective timeout) -- into one of two pinned host slots.  After
+    # enqueueing step k the host reads step k-1's slot (its event: by then the GPU is working on
+    # step k, so the host stays one step ahead and the device never idles) and raises if any word
+    # is set: a step that went wrong stops the run at the next step, before its parameters are
+    # used for more than one further step or saved.  DPA_STEP_HEALTH=0 turns it off.
+    def add_health_word(self, name: str, addr: int):
+        """Register one more device int word (by address) for the per-step health snapshot."""
+        if all(a != int(addr) for _, a in self._health_extra):
+            self._health_extra.append((name, int(addr)))
+            self._health_ptrs = None
+
+    def _health_setup(self):
+        names, addrs = [], []
+        if self.np == 2:
+            for nm, a in zip(("conv", "bn", "sgd", "bn_fused"), self.K.h2_overflow_addrs()):
+                names.append(f"fp16-pair overflow ({nm} kernels)")
+                addrs.append(a)
+        if self.ksig_tmo is not None:
+            names.append("wgrad-stream signal wait timeout")
+            addrs.append(self.ksig_tmo.data_ptr())
+        names.append("one-launch BatchNorm rendezvous timeout")
+        addrs.append(self.bn_tmo.data_ptr())
+        for nm, a in self._health_extra:
+            names.append(nm)
+            addrs.append(a)
+        self._health_names = names
+        self._health_ptrs = torch.tensor(addrs, dtype=torch.int64, device=self.device)
+        if self._health_out is None:
+            self._health_out = [torch.zeros(64, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self._health_ev = [torch.cuda.Event() for _ in range(2)]
+
+    def health_mark(self):
+        """Snapshot this step's error words (async) and check the previous step's snapshot."""
+        if not self.health or torch.cuda.is_current_stream_capturing():
+            return
+        if self._health_ptrs is None:
+            self._health_setup()
+        k = self._health_slot
+        self._health_slot ^= 1
+        self.K.health_copy(self._health_ptrs, self._health_out[k], self.steps_taken)
+        self._health_ev[k].record()
+        self._health_pending[k] = True
+        self._health_check(k ^ 1)
+
+    def _health_check(self, j: int):
+        if not self._health_pending[j]:
+            return
+        self._health_ev[j].synchronize()
+        self._health_pending[j] = False
+        v = self._health_out[j].tolist()
+        bad = [nm for nm, x in zip(self._health_names, v) if x != 0]
+        if bad:
+            raise RuntimeError(f"VGGEngine: step {v[63]} failed its health check: {', '.join(bad)} "
+                               "(that step's results are invalid; the run stops here)")
+
+    def health_flush(self):
+        """Check every snapshot still pending (synchronises with the last marked step)."""
+        if self.health and self._health_ptrs is not None:
+            for j in (self._health_slot ^ 1, self._health_slot):
+                self._health_check(j)
 
     # ------------------------------------------------------------------ evaluation
     def begin_eval(self):

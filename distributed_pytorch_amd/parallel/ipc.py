@@ -81,6 +81,7 @@ class IpcComm(Comm):
         self.boot_timeout_s = float(os.environ.get("DPA_IPC_BOOT_TIMEOUT", "120"))
         self._tmo_us = int(self.timeout_s * 1e6)
         self._nreg = 0
+        self._verify = os.environ.get("DPA_IPC_VERIFY", "0") == "1"
         self._regions: List[Tuple[int, int, int]] = []  # (data ptr, bytes, region id)
         self._keep: List[torch.Tensor] = []
         self.ops: Counter = Counter()
@@ -160,13 +161,28 @@ class IpcComm(Comm):
             if t is not None and t.is_cuda and t.numel() > 0:
                 self.register(t)
 
-    def _loc(self, t: torch.Tensor) -> Tuple[int, int]:
-        """(region id, word offset) of the registered region holding t, or (-1, 0): bounced."""
+    def _loc(self, t: torch.Tensor, kind: str = "") -> Tuple[int, int]:
+        """(region id, word offset) of the registered region holding t, or (-1, 0): bounced.
+
+        A registered collective reads every peer's copy at the SAME (region, offset); nothing in
+        the kernel can tell if a peer resolved its tensor differently.  ``DPA_IPC_VERIFY=1`` (tests,
+        debugging) agrees (kind, region, offset) across the ranks through the store before every
+        collective and raises on a mismatch (a host round trip per collective: debug only)."""
         p, nb = t.data_ptr(), t.numel() * t.element_size()
+        loc = (-1, 0)
         for b, m, rid in self._regions:
             if b <= p and p + nb <= b + m and (p - b) % 4 == 0:
-                return rid, (p - b) // 4
-        return -1, 0
+                loc = (rid, (p - b) // 4)
+                break
+        if self._verify and kind:
+            self._nreg += 1
+            mine = f"{kind}:{loc[0]}:{loc[1] if loc[0] >= 0 else 0}".encode()
+            vals = self._exchange(f"loc{self._nreg}", mine)
+            if any(v != mine for v in vals):
+                raise RuntimeError(f"IpcComm rank {self.rank}: ranks resolved the {kind} input differently "
+                                   f"({[v.decode() for v in vals]}); a registered collective would read the "
+                                   "wrong peer memory")
+        return loc
 
     def _words_ok(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.is_contiguous() and (t.numel() * t.element_size()) % 4 == 0
@@ -214,7 +230,7 @@ class IpcComm(Comm):
         if not self.ipc_eligible(t, o):
             return self._inner(f"all_reduce({op}, {t.dtype})").all_reduce(t, op)
         self._guard()
-        rid, off = self._loc(t)
+        rid, off = self._loc(t, "all_reduce")
         self._c.all_reduce(rid, off, t, _RED[o], self.blocks, self._tmo_us)
         self.ops["all_reduce" if rid >= 0 else "all_reduce_bounced"] += 1
         if op == "avg":
@@ -230,7 +246,7 @@ class IpcComm(Comm):
         if not self._words_ok(t):
             return self._inner(f"broadcast({t.dtype})").broadcast(t, root)
         self._guard()
-        rid, off = self._loc(t)
+        rid, off = self._loc(t, "broadcast")
         self._c.broadcast(rid, off, t, int(root), self.blocks, self._tmo_us)
         self.ops["broadcast"] += 1
 
@@ -238,7 +254,7 @@ class IpcComm(Comm):
         if not self._words_ok(send) or (recv is not None and not self._words_ok(recv)):
             return self._inner("gather").gather(send, recv, root)
         self._guard()
-        rid, off = self._loc(send)
+        rid, off = self._loc(send, "gather")
         self._c.gather(rid, off, send, recv if self.rank == root else None, int(root), self.blocks, self._tmo_us)
         self.ops["gather"] += 1
 
@@ -247,7 +263,7 @@ class IpcComm(Comm):
                 and op in _RED):
             return self._inner("reduce_scatter").reduce_scatter(send, recv, op)
         self._guard()
-        rid, off = self._loc(send)
+        rid, off = self._loc(send, "reduce_scatter")
         self._c.reduce_scatter(rid, off, send, recv, _RED[op], self.blocks, self._tmo_us)
         self.ops["reduce_scatter"] += 1
 
@@ -255,7 +271,13 @@ class IpcComm(Comm):
         if not (self._words_ok(send) and self._words_ok(recv)):
             return self._inner("all_gather").all_gather(send, recv)
         self._guard()
-        rid, off = self._loc(send)
+        rid, off = self._loc(send, "all_gather")
+        n = send.numel() * send.element_size() // 4
+        if rid >= 0 and send.data_ptr() != recv.data_ptr() + self.rank * n * 4:
+            # registered but not in place: the peers' inputs need not sit at this rank's offset
+            # (e.g. arena[rank * n:]), so the input goes through the inbox instead
+            rid, off = -1, 0
+            self.ops["all_gather_bounced"] += 1
         self._c.all_gather(rid, off, send, recv, self.blocks, self._tmo_us)
         self.ops["all_gather"] += 1
 
@@ -284,6 +306,10 @@ class IpcComm(Comm):
     def timed_out(self) -> bool:
         """A bounded peer wait gave up since the last call (clears the flag)."""
         return bool(self._c.take_timeout())
+
+    def health_words(self):
+        """(name, device address) of this communicator's error words (engine per-step health)."""
+        return [(f"peer-collective wait timeout (IPC, rank {self.rank})", int(self._c.tmo_ptr()))]
 
     def check(self):
         if self.timed_out():

@@ -155,6 +155,11 @@ class GradSync:
         if self.active and self._cuda:  # the arenas every collective of this strategy moves
             e = engine
             comm.prepare([e.grads.flat, e.params.flat, e.mom.flat, e.buffers.flat, e.nbt])
+            # device error words of the communicator (peer-collective timeouts) join the engine's
+            # per-step health snapshot
+            if hasattr(engine, "add_health_word"):
+                for nm, addr in getattr(comm, "health_words", lambda: [])():
+                    engine.add_health_word(nm, addr)
         if broadcast_init and self.active:
             self.broadcast_state()
 

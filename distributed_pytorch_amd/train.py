@@ -70,6 +70,23 @@ def _fault_point(rank: int, it: int):
     os._exit(13)
 
 
+def agreed_health_check(engine: VGGEngine, ctx: DistContext):
+    """Before anything is saved: this rank's device error words (engine.check_signals: the per-step
+    health snapshots, the wgrad-stream / BN-rendezvous timeouts, the fp16-pair overflow words) and
+    its communicator's (ctx.comm.check: RCCL async errors, peer-collective timeouts), agreed over
+    every rank -- a peer whose collectives timed out may have fed this rank a corrupted reduction
+    while this rank's own words are clear, so every rank raises together or none does."""
+    err = None
+    try:
+        engine.check_signals()
+        ctx.comm.check()
+    except RuntimeError as e:
+        err = e
+    if ctx.all_max(1.0 if err is not None else 0.0) > 0:
+        raise err if err is not None else RuntimeError(
+            f"[rank {ctx.rank}] a peer rank failed its health check; not saving results built on its collectives")
+
+
 def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: DistContext, args,
                 start_batch: int = 0, stats: Optional[dict] = None, budget: Optional[int] = None) -> Optional[int]:
     """One epoch (main.py:19-49).  ``budget`` caps the iterations run in this call (the remainder of
@@ -114,7 +131,7 @@ def train_model(engine: VGGEngine, loader: DeviceLoader, sync, epoch: int, ctx: 
             t_win = now
             ctx.comm.check()
         if ck_every and args.checkpoint_dir and (batch_idx + 1) % ck_every == 0:
-            engine.check_signals()  # never save weights built from a step whose cross-stream wait gave up
+            agreed_health_check(engine, ctx)  # never save weights built from a failed step, on any rank
             sync.prepare_checkpoint()
             checkpoint.save(args.checkpoint_dir, ctx.rank, engine, epoch, batch_idx + 1, args.sampler_seed, ctx.world,
                             sync.mode, ddp_prefix=sync.mode == "ddp")
@@ -248,7 +265,7 @@ def run(ctx: DistContext, mode: str, args):
         stopped = train_model(engine, train_loader, sync, epoch, ctx, args, start_batch=start_batch, stats=stats,
                               budget=budget)
         start_batch = 0
-        engine.check_signals()  # the epoch's cross-stream waits all saw their producers
+        agreed_health_check(engine, ctx)  # the epoch's waits, collectives and splits were all valid
         if budget is not None:
             budget -= stats.get("iters_run", 0)
         if stopped is not None:  # preempted mid-epoch: checkpoint the position, no eval
