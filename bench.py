@@ -79,6 +79,9 @@ def parse(argv=None):
                          "tail bucket, per-bucket update inside backward) on the real fabric and keep the fastest "
                          "(max over ranks, so every rank picks the same plan); off = --bucket-mb / defaults")
     ap.add_argument("--comm-tune-steps", type=int, default=8, help="timed steps per plan and repetition")
+    ap.add_argument("--comm-tune-budget", type=float, default=60.0,
+                    help="wall-clock seconds the comm tuner may take in all (agreed over ranks; plans not reached "
+                         "are skipped, the default plan stays the fallback)")
     ap.add_argument("--ipc", default="off", choices=["auto", "on", "off"],
                     help="N>1 on one node: collectives on the peer-memory kernels (parallel/ipc.py). auto = "
                          "extra comm-tuner plans; on = always (any --comm; several ranks may share a GPU); off "
@@ -236,6 +239,15 @@ def ipc_live_checks(ipc, engine, checks: list):
     checks.append(ipc.verify_all_reduce(engine.grads.flat))
 
 
+def _test_drop(rank: int, idx: int) -> bool:
+    """Test hook: DPA_TEST_TUNE_DROP=rank:plan makes that rank fail to set up that plan."""
+    spec = os.environ.get("DPA_TEST_TUNE_DROP")
+    if not spec:
+        return False
+    r, i = (int(v) for v in spec.split(":"))
+    return r == rank and i == idx
+
+
 def tune_comm(a, engine, sync, ctx, dev, batches):
     """Warmup-phase choice among ``comm_plans``: each plan runs ``--comm-tune-steps`` steps per
     repetition (2 repetitions, interleaved); the score of a plan is its best repetition's time,
@@ -243,7 +255,15 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     (sync, report).  Gradient-sync plans change only where and when collectives and the update
     run: the numerics of every plan are identical (bitwise, tests/test_multirank_gpu.py).  The
     tuning steps draw their own batches and the training state is restored afterwards, so the
-    run that follows is the same as without tuning."""
+    run that follows is the same as without tuning.
+
+    First-contact safety on a real multi-GPU node: a plan's communicator is
+    created only when that plan is first timed (its init time, max over ranks, is reported); the
+    whole tuner runs under ``--comm-tune-budget`` seconds of wall clock, agreed over the ranks
+    (``all_max``) before every plan, so every rank stops at the same plan -- plans not timed are
+    not candidates and the default plan (always timed first) stays the fallback; a plan that
+    fails to set up on ANY rank is dropped on every rank; the communicators of the plans not
+    chosen are destroyed on every rank in the same order after a barrier."""
     from distributed_pytorch_amd.parallel.comm import RcclComm
 
     if isinstance(ctx.comm, IpcComm):  # --ipc on: the transport is fixed
@@ -257,28 +277,53 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     snap = [t.clone() for t in (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt,
                                 engine.loss_accum)]
     steps_taken = engine.steps_taken
-    syncs, comms = {}, {}
-    for p in list(plans):
-        err = None
+    syncs, comms, init_s = {}, {}, {}
+    all_plans = list(plans)
+    dropped = []
+
+    def setup(p) -> bool:
+        """Create plan p's communicator and sync (lazily); False (on every rank) if it failed anywhere."""
+        if p in syncs:
+            return True
+        err, t0 = None, time.perf_counter()
+        key = "ipc" if p[4] else p[3]
         try:
+            if _test_drop(ctx.rank, all_plans.index(p)):
+                raise RuntimeError("injected set-up failure (DPA_TEST_TUNE_DROP)")
             comm = ipc_comm(ctx, dev, engine, comms) if p[4] else comm_for_channels(ctx, dev, p[3], comms)
         except RuntimeError as e:
             err = e
+        dt = ctx.all_max(time.perf_counter() - t0)
+        name = "ipc" if p[4] else f"ch{p[3]}"
+        if key != 0 and name not in init_s:
+            init_s[name] = round(dt, 3)
         # a plan is dropped on EVERY rank if its communicator failed on ANY rank (a rank-local
         # failure must not leave the ranks with different plan lists: mismatched collectives hang)
         if ctx.all_max(1.0 if err is not None else 0.0) > 0:
             print(f"[rank {ctx.rank}] comm tuner: no communicator for plan {p} ({err or 'failed on a peer'})",
                   flush=True)
-            plans.remove(p)
-            comms.pop("ipc" if p[4] else p[3], None)
-            continue
+            dropped.append(p)
+            if key != 0:
+                comms.pop(key, None)
+            return False
         s = make_sync(a.mode, engine, comm, bucket_mb=p[0], overlap=True, broadcast_init=False, tail_mb=p[1])
         s.fuse_step = p[2] and s.fusable_step
         syncs[p] = s
+        return True
+
     n = max(1, a.comm_tune_steps)
     score = {}
+    budget_hit = False
     for _rep in range(2):
-        for p in plans:
+        for p in list(plans):
+            # the budget check is agreed (max over ranks): every rank stops before the same plan;
+            # the default plan's first repetition always runs
+            if score and ctx.all_max(time.perf_counter() - t_tune) > a.comm_tune_budget:
+                budget_hit = True
+                break
+            if not setup(p):
+                plans.remove(p)
+                continue
             if p[4]:
                 comms["ipc"].blocks = p[4]
             step = make_step(engine, syncs[p], it)
@@ -291,6 +336,9 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
             benchlib.device_barrier(ctx, dev)
             el = ctx.all_max(time.perf_counter() - t0) / n * 1e3
             score[p] = min(score.get(p, el), el)
+        if budget_hit:
+            break
+    plans = [p for p in plans if p in score]
     # a plan whose peer-memory waits timed out (any rank), or whose all-reduce of the real gradient
     # arena fails the store-side agreement check (IpcComm.verify_all_reduce: same verdict on every
     # rank), is disqualified
@@ -307,8 +355,8 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     # the first plan is the default: another one must beat it by 1 % (run-to-run noise of a few
     # steps), so the choice does not flap between equivalent plans
     best = min(plans, key=lambda p: score[p])
-    if score[best] > 0.99 * score[plans[0]]:
-        best = plans[0]
+    if all_plans[0] in score and score[best] > 0.99 * score[all_plans[0]]:
+        best = all_plans[0]
     benchlib.device_barrier(ctx, dev)
     for dst, src in zip((engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt, engine.loss_accum),
                         snap):
@@ -322,8 +370,10 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
     report = {"chosen": {"bucket_mb": best[0], "tail_mb": best[1], "per_bucket_update": best[2],
                          "rccl_channels": best[3] or None, "ipc_blocks": best[4] or None},
               "ipc_check": ipc_check,
-              # the whole tuner (communicator creation, every plan, the agreement check), max over ranks
-              "tune_seconds": round(ctx.all_max(time.perf_counter() - t_tune), 3),
+              "budget_s": a.comm_tune_budget, "budget_hit": budget_hit,
+              "untimed_plans": len(all_plans) - len(score) - len(dropped), "dropped_plans": len(dropped),
+              # communicators the tuner created (max over ranks), the run's main one excluded
+              "comm_init_s": init_s,
               "ms_per_step": {f"b{p[0]}_t{p[1]}_{'fused' if p[2] else 'after'}" + (f"_ch{p[3]}" if p[3] else "")
                               + (f"_ipc{p[4]}" if p[4] else ""): round(score[p], 4) for p in plans}}
     if best[4]:  # the peer-memory communicator carries the run from here on
@@ -331,9 +381,24 @@ def tune_comm(a, engine, sync, ctx, dev, batches):
         ctx.comm.blocks = best[4]
     elif best[3]:  # the bounded communicator carries the run from here on (and the replica check)
         ctx.comm = comms.pop(best[3])
-    for c in comms.values():  # the other bounded communicators are drained and left idle
+    chosen = syncs[best]
+    # the unchosen communicators: drained, then destroyed on every rank in the same order
+    for c in comms.values():
         c.synchronize()
-    return syncs[best], report
+    benchlib.device_barrier(ctx, dev)
+    for k in sorted(comms, key=str):
+        c = comms[k]
+        if hasattr(c, "close"):
+            c.close()
+    syncs.clear()
+    comms.clear()
+    gc.collect()
+    # the whole tuner (communicator creation, every plan, the agreement check), max over ranks
+    report["tune_seconds"] = round(ctx.all_max(time.perf_counter() - t_tune), 3)
+    if ctx.rank == 0:
+        print(f"[bench] comm tuner: {report['tune_seconds']} s, chosen {report['chosen']}, "
+              f"communicator init {init_s or '-'}, budget hit {budget_hit}", file=sys.stderr, flush=True)
+    return chosen, report
 
 
 def solo_phase(a, dev, steps, warmup):
@@ -454,6 +519,8 @@ def main(argv=None):
             "solo_img_s": round(solo_img_s, 1) if solo_img_s else None,
             "scaling_efficiency": round(per_gpu / solo_img_s, 4) if solo_img_s else None,
             "rccl_world": cw,
+            # seconds this rank spent creating the main RCCL communicator (ncclCommInitRankConfig)
+            "rccl_init_s": round(ctx.comm.init_s, 3) if getattr(ctx.comm, "init_s", None) is not None else None,
             "ipc_allreduce_ops": getattr(ctx.comm, "ipc_ops", None),
             # peer-memory collectives by kind, and collectives the IPC communicator handed to the
             # communicator it wraps (0 with --comm ipc: no tensor byte through gloo / the host)

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -161,7 +162,9 @@ def _make_comm(kind: str, rank: int, world: int, device: torch.device, store=Non
     if torch_store:
         store = dist.distributed_c10d._get_default_store()
     try:
+        t0 = time.perf_counter()
         comm = RcclComm(rank, world, device, store=store)
+        comm.init_s = time.perf_counter() - t0  # (reported by bench.py: first-contact diagnostics)
     except Exception as e:  # noqa: BLE001 — keep the job alive on torch's own RCCL group
         if not torch_store or os.environ.get("DPA_COMM_FALLBACK", "0") != "1":
             raise

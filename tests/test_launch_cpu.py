@@ -332,3 +332,39 @@ def test_ipc_collective_pieces_cover_the_tensor():
         if reg and op != AR:
             assert len(ps) == 1
     assert C.ipc_pieces(AR, 0, 4, 1 << 20, 1 << 20, True) == []
+
+def _bench8(extra_env, args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", spawn.SPAWNED_ENV)}
+    env.update(OMP_NUM_THREADS="1", **extra_env)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--batch", "2",
+                        "--steps", "1", "--warmup", "1", "--solo-steps", "0", "--diag-steps", "0",
+                        "--comm-tune-steps", "1"] + args, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_comm_tuner_eight_ranks_plan_dropped_on_one_rank():
+    """VERDICT r5 item 6 (first 8-GPU contact): the warmup comm tuner at W = 8 (gloo ranks on CPU,
+    the same bench.py code path).  A plan whose set-up fails on ONE rank (injected on rank 5) is
+    dropped on EVERY rank -- the ranks keep identical plan lists, nothing hangs -- every other plan
+    is timed, one is chosen, and the replicas end identical."""
+    rec = _bench8({"DPA_TEST_TUNE_DROP": "5:1"}, [])
+    tune = rec["config"]["comm_tune"]
+    assert rec["n_gpus"] == 8 and rec["replicas_identical"] is True, rec
+    assert tune["dropped_plans"] == 1 and tune["untimed_plans"] == 0 and not tune["budget_hit"], tune
+    assert len(tune["ms_per_step"]) == 4 and "b25.0_t2.0_after" not in tune["ms_per_step"], tune
+    assert tune["tune_seconds"] > 0 and tune["tune_seconds"] < tune["budget_s"], tune
+
+
+def test_comm_tuner_eight_ranks_budget():
+    """A spent wall-clock budget (agreed over the ranks) stops the tuner at the same plan on every
+    rank; the default plan, always timed first, carries the run."""
+    rec = _bench8({}, ["--comm-tune-budget", "0"])
+    tune = rec["config"]["comm_tune"]
+    assert rec["replicas_identical"] is True, rec
+    assert tune["budget_hit"] is True and list(tune["ms_per_step"]) == ["b10.0_t2.0_after"], tune
+    assert tune["chosen"] == {"bucket_mb": 10.0, "tail_mb": 2.0, "per_bucket_update": False, "rccl_channels": None,
+                              "ipc_blocks": None}, tune
+    assert tune["untimed_plans"] == 4, tune

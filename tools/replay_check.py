@@ -98,22 +98,35 @@ def child(a) -> dict:
         step()
     names = [n for n, _ in _bufs(engine)]
     state = (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt, engine.loss_accum)
-    hashes = []
+    hashes, pre, zdiff = [], [], []
+    w0 = engine.params["layers.0.weight"]
+    z0 = engine.z[0]
+    nblk = z0.shape[0] * 4  # conv0 blocks: (image, 8-row band)
+    blk_hits = torch.zeros(nblk, dtype=torch.int64, device=dev)
     t0 = time.time()
     pairs = 0
     while pairs < a.pairs and time.time() - t0 < a.seconds:
         snap = [s.clone() for s in state]
         taken = engine.steps_taken
-        pair = []
+        pair, pp = [], []
         for rep in range(2):
             if rep:
                 for d, s in zip(state, snap):
                     d.copy_(s)
                 engine.steps_taken = taken
                 engine.refresh_weight_planes()
+            pp.append(torch.stack([_hash(x), _hash(w0)]))  # conv0's inputs, right before the step
             step()
+            if rep == 0:
+                z0a = z0.clone()
+            else:
+                d = (z0 != z0a)
+                blk_hits += d.view(nblk, -1).any(dim=1).long()
+                zdiff.append(torch.stack([d.sum().double(), (z0 - z0a).abs().max().double(),
+                                          z0a.abs().max().double()]))
             pair.append(torch.stack([_hash(b) for _, b in _bufs(engine)]))
         hashes.append(torch.stack(pair))
+        pre.append(torch.stack(pp))
         pairs += 1
         if pairs % 25 == 0 and dev.type == "cuda":
             torch.cuda.synchronize()
@@ -121,14 +134,23 @@ def child(a) -> dict:
         torch.cuda.synchronize()
         engine.check_signals()
     H = torch.stack(hashes).cpu()  # [pairs, 2, nbuf]
+    P = torch.stack(pre).cpu()  # [pairs, 2 reps, (x, w0)]
+    Z = torch.stack(zdiff).cpu()  # [pairs, (elements differing, max |diff|, max |z0|)]
     diff = (H[:, 0] != H[:, 1])
     bad_pairs = diff.any(dim=1).nonzero().flatten().tolist()
     first = {}
     for p in bad_pairs:
         idx = diff[p].nonzero().flatten().tolist()
-        first[p] = [names[j] for j in idx[:6]]
+        first[p] = [names[j] for j in idx[:3]]
+    hits = blk_hits.cpu()
+    by_xcd = [int(hits[x::8].sum()) for x in range(8)]  # round-robin dispatch: block b on XCD b % 8
     return {"rank": a.rank, "pairs": pairs, "bad_pairs": len(bad_pairs),
-            "first_diffs": {str(k): v for k, v in list(first.items())[:10]}}
+            "inputs_differ": int((P[:, 0] != P[:, 1]).any(dim=1).sum()),
+            "z0_bad_pairs": int((Z[:, 0] > 0).sum()),
+            "z0_elems_differing": [int(v) for v in Z[Z[:, 0] > 0][:6, 0].tolist()],
+            "z0_maxdiff_vs_max": [[float(f"{u:.3g}"), float(f"{v:.3g}")] for u, v in Z[Z[:, 0] > 0][:4, 1:].tolist()],
+            "z0_block_hits_by_xcd": by_xcd, "z0_blocks_hit": int((hits > 0).sum()), "z0_blocks": nblk,
+            "first_diffs": {str(k): v for k, v in list(first.items())[:4]}}
 
 
 def main(argv=None):
