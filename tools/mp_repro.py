@@ -44,6 +44,30 @@ def child(mode: str, seconds: float, rank: int) -> dict:
                 bad += (X != v).sum()
                 Y.mul_(0.5)
                 iters += 1
+    elif mode in ("big", "bigev"):
+        # torch only: a 64 MiB producer (the size of the first VGG layer's output at batch 256), a
+        # second stream, events and small pinned-memory copies around it -- the host-visible
+        # traffic of a training step -- then the check of every element
+        X = torch.empty(1 << 24, device=dev)
+        Y = torch.empty(1 << 22, device=dev)
+        side = torch.cuda.Stream(dev)
+        ev = torch.cuda.Event()
+        host = torch.zeros(64, dtype=torch.int32).pin_memory()
+        small = torch.zeros(64, dtype=torch.int32, device=dev)
+        t0 = time.time()
+        while time.time() - t0 < seconds:
+            for _ in range(20):
+                v = float(iters % 1000)
+                X.fill_(v)
+                if mode == "bigev":
+                    ev.record()
+                    side.wait_event(ev)
+                    with torch.cuda.stream(side):
+                        Y.mul_(0.5)
+                    host.copy_(small, non_blocking=True)
+                bad += (X != v).sum()
+                iters += 1
+            torch.cuda.synchronize()
     elif mode in ("conv0", "conv0alt"):
         from distributed_pytorch_amd import _ext
 

@@ -70,6 +70,29 @@ def _hash(t):
     return (v.to(torch.int64) * w).sum()
 
 
+def _diag_conv0(x, w0, za, zb) -> dict:
+    """Which of the two first-layer outputs is wrong (vs an fp64 conv of the same inputs), and where:
+    conv0_fwd_kernel's block = (image, 8-row band), thread = (channel quad c // 4, pixel lane p % 16)."""
+    import torch.nn.functional as F
+
+    xd = x[..., :3].double().permute(0, 3, 1, 2)
+    wd = w0[..., :3].double().permute(0, 3, 1, 2)
+    ref = F.conv2d(xd, wd, padding=1).permute(0, 2, 3, 1)
+    out = {}
+    for nm, z in (("rep0", za), ("rep1", zb)):
+        err = (z.double() - ref).abs()
+        bad = (err > 1e-4 * ref.abs().max()).nonzero().cpu()
+        rows = []
+        for n, h, w, c in bad[:24].tolist():
+            p = (h % 8) * 32 + w
+            rows.append({"n": n, "h": h, "w": w, "c": c, "blk": n * 4 + h // 8, "c4": c // 4, "k": c % 4,
+                         "pl": p % 16, "j": p // 16, "got": round(float(z[n, h, w, c]), 4),
+                         "ref": round(float(ref[n, h, w, c]), 4)})
+        out[nm] = {"wrong": int(bad.shape[0]), "blocks": sorted({n * 4 + h // 8 for n, h, w, c in bad.tolist()})[:16],
+                   "channels": sorted({c for n, h, w, c in bad.tolist()})[:64], "rows": rows[:12]}
+    return out
+
+
 def child(a) -> dict:
     import bench
     from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_cifar
@@ -99,6 +122,7 @@ def child(a) -> dict:
     names = [n for n, _ in _bufs(engine)]
     state = (engine.params.flat, engine.mom.flat, engine.buffers.flat, engine.nbt, engine.loss_accum)
     hashes, pre, zdiff = [], [], []
+    diag_out = []
     w0 = engine.params["layers.0.weight"]
     z0 = engine.z[0]
     nblk = z0.shape[0] * 4  # conv0 blocks: (image, 8-row band)
@@ -121,6 +145,8 @@ def child(a) -> dict:
                 z0a = z0.clone()
             else:
                 d = (z0 != z0a)
+                if a.diag and len(diag_out) < 3 and bool(d.any()):  # (synchronises: diagnostic runs only)
+                    diag_out.append(_diag_conv0(x, w0, z0a, z0.clone()))
                 blk_hits += d.view(nblk, -1).any(dim=1).long()
                 zdiff.append(torch.stack([d.sum().double(), (z0 - z0a).abs().max().double(),
                                           z0a.abs().max().double()]))
@@ -150,7 +176,7 @@ def child(a) -> dict:
             "z0_elems_differing": [int(v) for v in Z[Z[:, 0] > 0][:6, 0].tolist()],
             "z0_maxdiff_vs_max": [[float(f"{u:.3g}"), float(f"{v:.3g}")] for u, v in Z[Z[:, 0] > 0][:4, 1:].tolist()],
             "z0_block_hits_by_xcd": by_xcd, "z0_blocks_hit": int((hits > 0).sum()), "z0_blocks": nblk,
-            "first_diffs": {str(k): v for k, v in list(first.items())[:4]}}
+            "first_diffs": {str(k): v for k, v in list(first.items())[:4]}, "diag": diag_out}
 
 
 def main(argv=None):
@@ -162,6 +188,7 @@ def main(argv=None):
     ap.add_argument("--impl", default="h2")
     ap.add_argument("--env", default="", help="comma list K=V for the children (A/B of engine switches)")
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--diag", action="store_true", help="locate the wrong first-layer outputs of bad pairs")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args(argv)
@@ -173,7 +200,8 @@ def main(argv=None):
         k, v = kv.split("=", 1)
         env[k] = v
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", "--rank", str(r), "--pairs",
-                               str(a.pairs), "--seconds", str(a.seconds), "--batch", str(a.batch), "--impl", a.impl, "--device", a.device],
+                               str(a.pairs), "--seconds", str(a.seconds), "--batch", str(a.batch), "--impl", a.impl, "--device", a.device]
+                              + (["--diag"] if a.diag else []),
                               stdout=subprocess.PIPE, env=env, text=True) for r in range(a.procs)]
     rows, rc = [], 0
     for p in procs:
