@@ -4,7 +4,9 @@
         [gpurun_out/pmcB/run_counter_collection.csv] [--step -1] [--marker sgd_flat]
 
 Columns: duration, MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), kernel
-cycles = GRBM_GUI_ACTIVE / 8 XCDs from the second pass, else duration x 2.1 GHz), and the wave-state
+cycles = GRBM_GUI_ACTIVE / 8 XCDs from the second pass, else duration x 2.1 GHz; never more than
+duration x 2.4 GHz, MI355X's peak engine clock -- GRBM_GUI_ACTIVE of a short dispatch also counts the
+busy cycles around it, and such rows are marked '*' in the GHz column), and the wave-state
 split of SQ_WAVE_CYCLES: parked (SQ_WAIT_ANY: s_waitcnt / barrier), issue-stalled
 (SQ_WAIT_INST_ANY), issuing (SQ_ACTIVE_INST_ANY); LDS-issue stalls and bank-conflict cycles per wave
 cycle.  Passes are matched by dispatch id (the step's launch sequence is deterministic).
@@ -12,6 +14,8 @@ cycle.  Passes are matched by dispatch id (the step's launch sequence is determi
 import argparse
 import collections
 import csv
+
+PEAK_GHZ = 2.4  # MI355X peak engine clock: no dispatch runs more cycles than duration x this
 
 
 def load(path):
@@ -53,6 +57,9 @@ def main():
         dur = (r["t1"] - r["t0"]) / 1e3
         rb = B.get(d, {})
         cyc = rb.get("GRBM_GUI_ACTIVE", 0.0) / 8 if rb else dur * 1e3 * 2.1
+        clamped = cyc > dur * 1e3 * PEAK_GHZ
+        if clamped:
+            cyc = dur * 1e3 * PEAK_GHZ
         ghz = cyc / (dur * 1e3) if dur > 0 else 0.0
         mf = r.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024 * cyc) * 100 if cyc else 0.0
         wc = r.get("SQ_WAVE_CYCLES", 0.0) or 1.0
@@ -62,7 +69,7 @@ def main():
         ls = r.get("SQ_WAIT_INST_LDS", 0.0) / wc * 100
         bc = r.get("SQ_LDS_BANK_CONFLICT", 0.0) / wc * 100
         nwg = r["grid"] // max(r["wg"], 1)
-        print(f"{dur:7.1f} {mf:6.1f} {pk:6.1f} {st:6.1f} {iss:6.1f} {ls:6.1f} {bc:6.1f} {ghz:5.2f} {r['vgpr']:>4} "
+        print(f"{dur:7.1f} {mf:6.1f} {pk:6.1f} {st:6.1f} {iss:6.1f} {ls:6.1f} {bc:6.1f} {ghz:4.2f}{'*' if clamped else ' '} {r['vgpr']:>4} "
               f"{r['agpr']:>4} {r['lds']:>6} {nwg:6d}  {short(r['name'])}")
         tot["dur"] += dur
         tot["mfma_cyc"] += r.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
