@@ -56,8 +56,14 @@ __device__ __forceinline__ void conv0_px(const float4 (*xs)[XC], int r, int c, c
     }
 }
 
+// Built without gfx950's packed fp32 instructions (v_pk_fma_f32): see docs/PERF_NOTES.md round 6 --
+// under multi-process load, this kernel's packed FMAs produced wrong values for one 16-lane pass
+// (one component, one pixel) now and then; the scalar v_fma_f32 form does not.
+// (the host compilation pass ignores the attribute: -Wignored-attributes is silenced there)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wignored-attributes"
 template <bool STATS>
-__global__ __launch_bounds__(256) void conv0_fwd_kernel(const float4* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256) __attribute__((target("no-packed-fp32-ops"))) void conv0_fwd_kernel(const float4* __restrict__ x, const float* __restrict__ w,
                                                         int CP, float4* __restrict__ z, float2* __restrict__ part) {
   __shared__ float4 xs[C0_ROWS + 2][C0_W + 2];
   __shared__ float4 ws[16][27];   // [channel quad][tap * 3 + ci] -> the quad's 4 output channels
@@ -141,6 +147,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const float4* __restrict
     }
   }
 }
+#pragma clang diagnostic pop
 
 }  // namespace
 

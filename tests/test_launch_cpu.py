@@ -85,7 +85,7 @@ def test_bench_self_launch_two_ranks_cpu():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", spawn.SPAWNED_ENV)}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
                         "--batch", "4", "--steps", "2", "--warmup", "1", "--solo-steps", "1",
-                        "--comm-tune-steps", "1"],
+                        "--comm-tune-steps", "1", "--comm-tune-budget", "500"],  # (a loaded CPU: every plan timed)
                        capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

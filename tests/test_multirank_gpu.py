@@ -10,15 +10,12 @@ the reference's correctness oracle (the three modes give bit-identi
 the same seed) — every mode with the same parameters as every other: with two ranks a sum of two
 gradients and its halving are exact in any order.
 
-The oracle runs set AMD_SERIALIZE_KERNEL=3 (every process waits for each of its kernels): without
-it, runs of several processes sharing ONE GPU are not run-to-run reproducible on this pool (about
-1 run in 3-6 takes a step on stale data, gloo and peer kernels alike, while one process always is:
-docs/PERF_NOTES.md round 5, tracked by test_four_rank_training_run_to_run).  Serialised, 22 of 23
-runs of the four modes at W=2 (gloo and peer kernels) and W=4 (peer kernels) were bitwise identical
-and the 23rd differed by 2e-6 of the checksum (unserialised misses move it by ~1-2 %), so the
-cross-mode checks allow 1e-4 of the checksum (RTOL); serialised misses still occur now and then (one
-W=2 gloo run 0.3 % off in a later suite), so a run off the majority is re-run once and must then
-agree (_agree): a wrong sync mode reproduces its error, the platform's misses do not."""
+The oracle is strict: no kernel serialisation, bitwise equality, no re-runs.  Until round 6 it was
+not (runs of several processes sharing one GPU were not run-to-run reproducible, so the checks ran
+serialised, to 1e-4, with one re-run).  The cause was found by differential replay
+(tools/replay_check.py, docs/PERF_NOTES.md round 6): the first-layer conv kernel's packed fp32 FMAs
+(v_pk_fma_f32) produced a wrong value for one 16-lane pass now and then under multi-process load;
+built without packed fp32 that kernel replays bit-exactly, and so do the runs."""
 import json
 import os
 import subprocess
@@ -30,27 +27,12 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODES = ["ddp", "allreduce", "gather", "zero1"]
-SERIAL = {"AMD_SERIALIZE_KERNEL": "3"}  # the oracle runs (module docstring)
-RTOL = 1e-4
+SERIAL: dict = {}  # (the oracle runs unserialised since round 6, module docstring)
 
 
-def _same(a, b):
-    return abs(a - b) <= RTOL * abs(b)
-
-
-def _agree(sums, rerun):
-    """The cross-mode oracle over {label: checksum}: every run within RTOL of the majority value.
-    A run off the majority is re-run ONCE and must then agree: the engine is deterministic, so a
-    wrong sync mode reproduces its error, while the platform's multi-process misses (module
-    docstring) do not repeat on the same run.  Returns the labels that needed the re-run."""
-    vals = list(sums.values())
-    best = max(vals, key=lambda v: sum(_same(u, v) for u in vals))
-    assert sum(_same(u, best) for u in vals) >= 2, sums
-    redo = [k for k, v in sums.items() if not _same(v, best)]
-    for k in redo:
-        v = rerun(k)
-        assert _same(v, best), (k, sums[k], v, best, sums)
-    return redo
+def _agree(sums):
+    """The cross-mode oracle over {label: checksum}: bitwise one value (no tolerance, no re-run)."""
+    assert len(set(sums.values())) == 1, sums
 
 
 def _run(mode):
@@ -82,11 +64,10 @@ def test_two_ranks_share_one_gpu(runs, mode):
 
 def test_modes_agree(runs):
     """The reference oracle (same seed, same parameters in every mode), two ranks
-    sharing one GPU through gloo (to RTOL, module docstring)."""
+    sharing one GPU through gloo: bitwise (a sum of two gradients and its halving are exact)."""
     if len(runs) < len(MODES):
         pytest.skip("needs every mode's run")
-    sums = {m: runs[m]["param_checksum"] for m in MODES}
-    _agree(sums, lambda m: _run(m)["param_checksum"])
+    _agree({m: runs[m]["param_checksum"] for m in MODES})
 
 
 def test_four_ranks_ddp_share_one_gpu():
@@ -222,17 +203,16 @@ def test_modes_on_peer_kernels(ipc_runs, mode, world):
 
 def test_peer_kernel_modes_agree(ipc_runs, runs):
     """The reference oracle (same seed, same parameters in every mode) on the peer
-    kernels (to RTOL, module docstring): every mode at W=2 lands on the parameters of the gloo
-    (host-staged) runs (a sum of two is exact in any order), and at W=4 (rank-order sums in every
-    mode) every mode on the parameters of every other."""
+    kernels, bitwise: every mode at W=2 lands on the parameters of the gloo (host-staged) runs (a
+    sum of two is exact in any order), and at W=4 (rank-order sums in every mode) every mode on the
+    parameters of every other."""
     need = [(m, w) for m in MODES for w in (2, 4)]
     if not all(k in ipc_runs for k in need) or not runs:
         pytest.skip("needs every mode's run")
     w2 = {("ipc", m): ipc_runs[(m, 2)]["param_checksum"] for m in MODES}
     w2.update({("gloo", m): d["param_checksum"] for m, d in runs.items()})
-    _agree(w2, lambda k: (_ipc_run(k[1], 2) if k[0] == "ipc" else _run(k[1]))["param_checksum"])
-    w4 = {m: ipc_runs[(m, 4)]["param_checksum"] for m in MODES}
-    _agree(w4, lambda m: _ipc_run(m, 4)["param_checksum"])
+    _agree(w2)
+    _agree({m: ipc_runs[(m, 4)]["param_checksum"] for m in MODES})
 
 
 def test_ddp_eight_ranks_share_one_gpu():
@@ -254,16 +234,13 @@ def test_resnet_generic_ddp_on_peer_kernels():
 def test_ipc_ddp_matches_gloo(runs):
     """Bucketed DDP with the collectives on the peer-memory kernels wrapped around the gloo
     communicator (--ipc on, 2 ranks on one GPU): replicas identical and -- a sum of two is exact in
-    any order -- the parameters of the gloo run of the same mode (to RTOL, module docstring)."""
+    any order -- bitwise the parameters of the gloo run of the same mode."""
     args = ["--gpus", "2", "--comm", "gloo", "--mode", "ddp", "--ipc", "on", "--steps", "3", "--warmup", "2",
             "--solo-steps", "0", "--diag-steps", "1"]
     d = _bench(args, env_extra=SERIAL)
     assert d["replicas_identical"] is True and d["ipc_allreduce_ops"] and d["ipc_allreduce_ops"] > 0, d
-    if "ddp" in runs and not _same(d["param_checksum"], runs["ddp"]["param_checksum"]):
-        # one re-run of each side (see _agree): a real difference reproduces
-        again = _bench(args, env_extra=SERIAL)["param_checksum"]
-        ref = _run("ddp")["param_checksum"]
-        assert _same(again, ref), (d["param_checksum"], again, runs["ddp"]["param_checksum"], ref)
+    if "ddp" in runs:
+        assert d["param_checksum"] == runs["ddp"]["param_checksum"], (d["param_checksum"], runs["ddp"])
 
 
 def test_ipc_live_agreement_checks():
@@ -321,10 +298,9 @@ def _w4_checksums(comm, runs=3):
     return sums
 
 
-@pytest.mark.xfail(strict=False, reason="open issue (docs/PERF_NOTES.md round 5): several processes sharing "
-                   "one GPU are not run-to-run reproducible unless every kernel is serialised (gloo and peer "
-                   "kernels alike; one process is)")
 @pytest.mark.parametrize("comm", ["gloo", "ipc"])
 def test_four_rank_training_run_to_run(comm):
+    """Four processes on one GPU, three runs of the same seed: bitwise the same parameters (the
+    round-5 open issue, fixed in round 6 -- module docstring)."""
     sums = _w4_checksums(comm)
     assert len(set(sums)) == 1, sums

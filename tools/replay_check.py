@@ -70,26 +70,42 @@ def _hash(t):
     return (v.to(torch.int64) * w).sum()
 
 
-def _diag_conv0(x, w0, za, zb) -> dict:
-    """Which of the two first-layer outputs is wrong (vs an fp64 conv of the same inputs), and where:
-    conv0_fwd_kernel's block = (image, 8-row band), thread = (channel quad c // 4, pixel lane p % 16)."""
+def _conv0_ref(x, w):
     import torch.nn.functional as F
 
     xd = x[..., :3].double().permute(0, 3, 1, 2)
-    wd = w0[..., :3].double().permute(0, 3, 1, 2)
-    ref = F.conv2d(xd, wd, padding=1).permute(0, 2, 3, 1)
-    out = {}
-    for nm, z in (("rep0", za), ("rep1", zb)):
-        err = (z.double() - ref).abs()
-        bad = (err > 1e-4 * ref.abs().max()).nonzero().cpu()
-        rows = []
-        for n, h, w, c in bad[:24].tolist():
-            p = (h % 8) * 32 + w
-            rows.append({"n": n, "h": h, "w": w, "c": c, "blk": n * 4 + h // 8, "c4": c // 4, "k": c % 4,
-                         "pl": p % 16, "j": p // 16, "got": round(float(z[n, h, w, c]), 4),
-                         "ref": round(float(ref[n, h, w, c]), 4)})
-        out[nm] = {"wrong": int(bad.shape[0]), "blocks": sorted({n * 4 + h // 8 for n, h, w, c in bad.tolist()})[:16],
-                   "channels": sorted({c for n, h, w, c in bad.tolist()})[:64], "rows": rows[:12]}
+    wd = w[..., :3].double().permute(0, 3, 1, 2)
+    return F.conv2d(xd, wd, padding=1).permute(0, 2, 3, 1)
+
+
+def _diag_conv0(x, w_snap, z, cands) -> dict:
+    """Where a first-layer output z (computed from x and the pre-step weights w_snap) is wrong, and
+    whether the wrong values are those of an OLDER weight tensor (cands: name -> weights), i.e. a
+    stale read of w.  conv0_fwd_kernel's block = (image, 8-row band), thread = (channel quad, pixel
+    lane)."""
+    ref = _conv0_ref(x, w_snap)
+    tol = 1e-4 * float(ref.abs().max())
+    bad = (z.double() - ref).abs() > tol
+    idx = bad.nonzero().cpu()
+    out = {"wrong": int(idx.shape[0])}
+    if not idx.shape[0]:
+        return out
+    zb = z.double()[bad]
+    for nm, w in cands.items():  # wrong values explained by another weight tensor
+        r2 = _conv0_ref(x, w)[bad]
+        out[f"match_{nm}"] = int(((zb - r2).abs() <= tol).sum())
+    blk = idx[:, 0] * 4 + idx[:, 1] // 8
+    out["blocks"] = sorted(set(blk.tolist()))[:24]
+    out["n_blocks"] = len(set(blk.tolist()))
+    out["channels"] = sorted(set(idx[:, 3].tolist()))[:64]
+    out["pixels"] = len(set((idx[:, 0] * 1024 + idx[:, 1] * 32 + idx[:, 2]).tolist()))
+    per = {}
+    for b, c, h, w_ in zip(blk.tolist(), idx[:, 3].tolist(), idx[:, 1].tolist(), idx[:, 2].tolist()):
+        e = per.setdefault(b, [set(), set()])
+        e[0].add(c)
+        e[1].add((h % 8) * 32 + w_)
+    out["per_block"] = {str(b): {"ch": sorted(v[0])[:16], "nch": len(v[0]), "npix": len(v[1]),
+                                 "pix": sorted(v[1])[:12]} for b, v in list(per.items())[:6]}
     return out
 
 
@@ -129,8 +145,10 @@ def child(a) -> dict:
     blk_hits = torch.zeros(nblk, dtype=torch.int64, device=dev)
     t0 = time.time()
     pairs = 0
+    w_prev = w0.clone()
     while pairs < a.pairs and time.time() - t0 < a.seconds:
         snap = [s.clone() for s in state]
+        w_snap = w0.clone() if a.diag else None
         taken = engine.steps_taken
         pair, pp = [], []
         for rep in range(2):
@@ -143,16 +161,21 @@ def child(a) -> dict:
             step()
             if rep == 0:
                 z0a = z0.clone()
+                w_after0 = w0.clone() if a.diag else None
             else:
                 d = (z0 != z0a)
-                if a.diag and len(diag_out) < 3 and bool(d.any()):  # (synchronises: diagnostic runs only)
-                    diag_out.append(_diag_conv0(x, w0, z0a, z0.clone()))
+                if a.diag and len(diag_out) < 4 and bool(d.any()):  # (synchronises: diagnostic runs only)
+                    diag_out.append({"pair": pairs,
+                                     "rep0": _diag_conv0(x, w_snap, z0a, {"prev_snap": w_prev}),
+                                     "rep1": _diag_conv0(x, w_snap, z0, {"after_rep0": w_after0})})
                 blk_hits += d.view(nblk, -1).any(dim=1).long()
                 zdiff.append(torch.stack([d.sum().double(), (z0 - z0a).abs().max().double(),
                                           z0a.abs().max().double()]))
             pair.append(torch.stack([_hash(b) for _, b in _bufs(engine)]))
         hashes.append(torch.stack(pair))
         pre.append(torch.stack(pp))
+        if a.diag:
+            w_prev = w_snap
         pairs += 1
         if pairs % 25 == 0 and dev.type == "cuda":
             torch.cuda.synchronize()
