@@ -34,7 +34,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, unsigned short* dz3, int np, int N, int H, int W, int C,
                int pool, int act, const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val,
-               const void* g2, const unsigned char* mask, unsigned* bound, unsigned* tcnt);
+               const void* g2, const unsigned char* mask, unsigned* bound);
 long dpa_wgrad0_part_floats(int N);
 int dpa_gap(const void* x, float* feat, int N, int HW, int C, int xbf, hipStream_t st);
 int dpa_ce(const float* logits, const long long* target, float* loss_row, float* dlogits, int* correct_row,
@@ -50,7 +50,7 @@ int dpa_conv0_fwd(const float* x, const float* w, int CP, float* z, float* part,
 int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
-                      float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val, unsigned* tcnt);
+                      float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val);
 int dpa_fc_ce_train(const float* x, const float* w, const float* b, const long long* target, float* loss_row,
                     float* dlogits, float* dx, float* dw, float* db, float* loss_out, float* loss_accum, int B,
                     int Cin, int J, hipStream_t st, const float* bn_z, const float* bn_scale,
@@ -199,15 +199,6 @@ int* signal_ptr(const Tensor& t, const char* what) {
 
 int* opt_signal(const OptT& t, const char* what) {
   return (t.has_value() && t->defined()) ? signal_ptr(*t, what) : nullptr;
-}
-
-// the BN-backward finalize-tail counters (bn.hip BwdTail): a zeroed CUDA int32 tensor of >= 64 words,
-// or nullptr (separate finalize kernel)
-unsigned* opt_tail_cnt(const OptT& t, const char* what) {
-  if (!(t.has_value() && t->defined())) return nullptr;
-  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt32 && t->numel() >= 64 && t->is_contiguous(), what,
-              ": tail counters must be a contiguous CUDA int32 tensor of >= 64 words");
-  return reinterpret_cast<unsigned*>(t->data_ptr<int>());
 }
 
 // the current stream waits (one polling wave) until sig[0] >= val; tmo[0] = 1 after timeout_us
@@ -650,7 +641,7 @@ void bn_apply(Tensor z, Tensor a, Tensor scale, Tensor shift, bool pool, int64_t
 // x [N,32,32,4], dw [64,3,3,CP], wpart >= wgrad0_part_floats(N).
 void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean,
                    Tensor invstd, Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias,
-                   Tensor x, Tensor wpart, Tensor dw, OptT sig, int64_t sig_val, OptT cnt) {
+                   Tensor x, Tensor wpart, Tensor dw, OptT sig, int64_t sig_val) {
   for (auto* t : {&gsrc, &g, &z, &scale, &shift, &mean, &invstd, &gamma, &part, &coef, &dgamma, &dbeta, &x, &wpart, &dw})
     need(*t, "bn_bwd_wgrad0 operand");
   const int N = z.size(0);
@@ -666,8 +657,7 @@ void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale
   TORCH_CHECK(coef.numel() >= 3 * 64 && scale.numel() == 64 && gamma.numel() == 64, "bn_bwd_wgrad0: channel vectors");
   chk(dpa_bn_bwd_wgrad0(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma),
                         fp(part), fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), fp(x), fp(wpart), fp(dw),
-                        (int)dw.size(3), N, cur_stream(), opt_signal(sig, "bn_bwd_wgrad0"), (int)sig_val,
-                        opt_tail_cnt(cnt, "bn_bwd_wgrad0")),
+                        (int)dw.size(3), N, cur_stream(), opt_signal(sig, "bn_bwd_wgrad0"), (int)sig_val),
       "bn_bwd_wgrad0");
 }
 
@@ -776,8 +766,7 @@ void gap_bwd(Tensor dfeat, Tensor dx) {
 
 void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tensor shift, Tensor mean, Tensor invstd,
             Tensor gamma, Tensor part, Tensor coef, Tensor dgamma, Tensor dbeta, OptT dbias, Tensor dz, bool pool,
-            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask, OptT bound,
-            OptT cnt) {
+            int64_t act, OptT res, OptT dres, OptT sig, int64_t sig_val, OptT g2, OptT mask, OptT bound) {
   const bool bf = z.scalar_type() == at::kBFloat16;
   const void* zp = act_ptr(z, "z", bf);
   const void* gsp = act_ptr(gsrc, "gsrc", bf);
@@ -828,7 +817,7 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   chk(dpa_bn_bwd(gsp, (int)nsplit, gp, zp, fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma), fp(part), fp(coef),
                  fp(dgamma), fp(dbeta), ofp(dbias), dzf, dz3, np, N, H, W, C, pool ? 1 : 0, (int)act, rp, drp,
                  bf ? 1 : 0, cur_stream(), opt_signal(sig, "bn_bwd"), (int)sig_val, g2p, mp,
-                 const_cast<unsigned*>(bound_ptr(bound, "bn_bwd")), opt_tail_cnt(cnt, "bn_bwd")),
+                 const_cast<unsigned*>(bound_ptr(bound, "bn_bwd"))),
       "bn_bwd");
 }
 
@@ -1249,7 +1238,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("dz"), py::arg("pool"), py::arg("act") = 0,
         py::arg("res") = py::none(), py::arg("dres") = py::none(), py::arg("sig") = py::none(),
         py::arg("sig_val") = 0, py::arg("g2") = py::none(), py::arg("mask") = py::none(),
-        py::arg("bound") = py::none(), py::arg("cnt") = py::none());
+        py::arg("bound") = py::none());
   m.def("bn_fused_geo", &bn_fused_geo, py::arg("Mo"), py::arg("C"), py::arg("pool"), py::arg("bwd"),
         py::arg("rmax"));
   m.def("bn_fused_fwd", &bn_fused_fwd, py::arg("src"), py::arg("nsplit"), py::arg("z"), py::arg("pool"),
@@ -1264,7 +1253,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_wgrad0", &bn_bwd_wgrad0, py::arg("gsrc"), py::arg("nsplit"), py::arg("g"), py::arg("z"),
         py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("part"),
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("x"), py::arg("wpart"),
-        py::arg("dw"), py::arg("sig") = py::none(), py::arg("sig_val") = 0, py::arg("cnt") = py::none());
+        py::arg("dw"), py::arg("sig") = py::none(), py::arg("sig_val") = 0);
   m.def("gap", &gap);
   m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("trans_a") = false,
         py::arg("trans_b") = false, py::arg("bias") = py::none(), py::arg("splits") = 1, py::arg("slab") = py::none());

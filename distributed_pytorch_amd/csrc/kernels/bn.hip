@@ -62,9 +62,6 @@ constexpr int BWD_BLOCKS = 512;
 // ResNet-50 +0.6 % over one / two rows).
 constexpr bool g_bn_unr = true;
 constexpr long WIDE_MIN_F4 = 3L << 20;
-// finalize tail of the backward reduce (BwdTail): blocks per first-level group, most groups
-constexpr int BWD_TAIL_TG = 32;
-constexpr int BWD_TAIL_MAXG = 63;
 constexpr int BWD_WIDE_BLOCKS = 256;
 // bf: bf16 tensors (the generic path, its 16-byte-lane reduce): the 1024-thread geometry at every
 // size (ResNet-50 A/B: 9,240 -> 9,330 img/s); fp32 (the VGG engine) by size as above.
@@ -474,9 +471,8 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
   d11 = (arg == 3 && y11 > 0.f) ? g : 0.f;
 }
 
-// Per-channel backward finalize from the complete sums (bn_bwd_finalize_kernel and the reduce
-// kernel's tail use this one function, so both paths round alike): dgamma, dbeta, dbias and the dz
-// coefficients dz = k1*dy + c2*z + c3.  Returns the channel's dz bound |k1| max|dy| + |c2| max|z| + |c3|.
+// Per-channel backward finalize from the complete sums: dgamma, dbeta, dbias and the dz coefficients
+// dz = k1*dy + c2*z + c3.  Returns the channel's dz bound |k1| max|dy| + |c2| max|z| + |c3|.
 __device__ __forceinline__ float bwd_coef(int c, int C, float sdy, float sdx, float sx, float mdy, float mz,
                                           float Mfull, const float* __restrict__ gamma,
                                           const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -495,63 +491,6 @@ __device__ __forceinline__ float bwd_coef(int c, int C, float sdy, float sdx, fl
   coef[2 * C + c] = c3;  // constant
   // (rounding of the fma chain stays far inside the 2^14 -> 65504 headroom of the scale)
   return fabsf(k1) * mdy + fabsf(c2) * mz + fabsf(c3);
-}
-
-// The reduce kernel's finalize tail (VGG engine, DPA_BN_TAIL): instead of a separate finalize launch
-// -- 7-16 us in the step for microseconds of work, because its blocks wait for CU slots held by the
-// weight-gradient convs of the other stream -- the blocks that are already resident finish the job.
-// Two levels of "last block in" tickets: the last of each group of `tg` blocks sums the group's
-// partial rows into gpart[group]; the last group to finish sums the group rows and writes the
-// coefficients, the parameter gradients and the dz bound.  Every sum runs in one fixed order
-// (rows in lane order, then the LDS tree), whichever block arrives last: deterministic.
-// Hand-off without cache maintenance: every word that crosses blocks (partial rows, group rows) is
-// stored and loaded as a relaxed AGENT-scope atomic (global_store / global_load with sc1: coherent
-// across the 8 XCDs' L2s by themselves); the storing waves drain (vmcnt 0), barrier, one lane takes
-// a relaxed agent-scope ticket.  No agent-scope release/acquire fence: on gfx950 those are
-// buffer_wbl2 / buffer_inv of the whole XCD L2, and one per block of a 512-block reduce -- beside
-// the weight-gradient convs writing their split-K slabs -- measured +40 us per layer (1.455 vs
-// 1.132 ms/step).  The winner zeroes the counter for the next launch (stream-ordered).
-struct BwdTail {
-  unsigned* cnt;  // [>= ngroups + 1] zeroed once; self-resetting
-  float* gpart;   // [ngroups][5][C]
-  int tg;         // blocks per group
-  float Mfull;
-  const float* gamma;
-  float* dgamma;
-  float* dbeta;
-  float* dbias;
-  float* coef;
-};
-
-// one lane publishes the block's (already drained) stores and takes a ticket; true in every thread of
-// the block that arrived last of `n`
-__device__ __forceinline__ bool last_block_in(unsigned* cnt, unsigned n, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's agent-coherent stores are complete
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    typedef __attribute__((address_space(1))) unsigned gu32;
-    const unsigned k = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = k == n - 1;
-    if (last) __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-// float4 through relaxed agent-scope atomics (sc1: bypasses a stale or dirty line of this XCD's L2)
-typedef __attribute__((address_space(1))) float gf32;
-__device__ __forceinline__ void st4_agent(float* p, float4 v) {
-  __hip_atomic_store((gf32*)p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gf32*)(p + 1), v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gf32*)(p + 2), v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gf32*)(p + 3), v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float4 ld4_agent(const float* p) {
-  return make_float4(__hip_atomic_load((gf32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     __hip_atomic_load((gf32*)(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     __hip_atomic_load((gf32*)(p + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     __hip_atomic_load((gf32*)(p + 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat and maxima of |dy|, |z| (the
@@ -576,10 +515,9 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
                                                             int rpb, int* sig, int sig_val,
                                                             const TZ* __restrict__ g2,
                                                             const unsigned char* __restrict__ mask,
-                                                            TZ* __restrict__ dyout, unsigned* __restrict__ bound,
-                                                            BwdTail tl) {
+                                                            TZ* __restrict__ dyout, unsigned* __restrict__ bound) {
   start_signal(sig, sig_val);
-  if (bound != nullptr && tl.cnt == nullptr && blockIdx.x == 0 && threadIdx.x == 0) *bound = 0u;  // re-armed for this layer's
+  if (bound != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *bound = 0u;  // re-armed for this layer's
                                                                                // finalize (the next kernel)
   const RedGeom gg = red_geom(C, RTB);
   const int t = threadIdx.x;
@@ -710,82 +648,8 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
         tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
       else
         tree_rows_max<RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-      if (cval && lane_r == 0) {
-        if (tl.cnt != nullptr)
-          st4_agent(o + q * C, sh[0][t]);  // read by another block (finalize tail)
-        else
-          *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
-      }
+      if (cval && lane_r == 0) *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
       __syncthreads();
-    }
-  }
-  if (tl.cnt == nullptr) return;  // (uniform) the separate finalize kernel follows
-  // ---- finalize tail (host guarantees CG == 1: every channel lane is one thread column) ----
-  __shared__ int s_last;
-  const int nblk = gridDim.x;
-  const int ngrp = (nblk + tl.tg - 1) / tl.tg;
-  const int grp = blockIdx.x / tl.tg, g0 = grp * tl.tg, gn = min(tl.tg, nblk - g0);
-  if (!last_block_in(tl.cnt + grp, (unsigned)gn, &s_last)) return;
-  const int c4 = lane_c;
-  const bool cval = active && c4 < gg.C4;
-  const long rowf = 5L * C;
-  // level 1: the group's rows -> gpart[grp]
-#pragma unroll 1
-  for (int q = 0; q < 5; ++q) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (cval)
-      for (int r = lane_r; r < gn; r += gg.RPI) {
-        const float4 v = ld4_agent(part + (g0 + r) * rowf + q * C + c4 * 4);
-        acc = q < 3 ? f4add(acc, v)
-                    : make_float4(fmaxf(acc.x, v.x), fmaxf(acc.y, v.y), fmaxf(acc.z, v.z), fmaxf(acc.w, v.w));
-      }
-    sh[0][t] = acc;
-    __syncthreads();
-    if (q < 3)
-      tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-    else
-      tree_rows_max<RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-    if (cval && lane_r == 0) st4_agent(tl.gpart + grp * rowf + q * C + c4 * 4, sh[0][t]);
-    __syncthreads();
-  }
-  if (!last_block_in(tl.cnt + ngrp, (unsigned)ngrp, &s_last)) return;
-  // level 2: the group rows -> the channel sums, then the coefficients
-  float4 fin[5];  // (fully unrolled: a runtime index would put fin in scratch, and a kernel with scratch
-                  // costs the queue a scratch-setup stall at every launch: +40 us per layer measured)
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (cval)
-      for (int r = lane_r; r < ngrp; r += gg.RPI) {
-        const float4 v = ld4_agent(tl.gpart + r * rowf + q * C + c4 * 4);
-        acc = q < 3 ? f4add(acc, v)
-                    : make_float4(fmaxf(acc.x, v.x), fmaxf(acc.y, v.y), fmaxf(acc.z, v.z), fmaxf(acc.w, v.w));
-      }
-    sh[0][t] = acc;
-    __syncthreads();
-    if (q < 3)
-      tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-    else
-      tree_rows_max<RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-    fin[q] = sh[0][t];
-    __syncthreads();
-  }
-  float B = 0.f;
-  if (cval && lane_r == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      B = fmaxf(B, bwd_coef(c4 * 4 + k, C, F4GET(fin[0], k), F4GET(fin[1], k), F4GET(fin[2], k), F4GET(fin[3], k),
-                            F4GET(fin[4], k), tl.Mfull, tl.gamma, mean, invstd, tl.dgamma, tl.dbeta, tl.dbias,
-                            tl.coef));
-  }
-  if (bound != nullptr) {  // the largest channel bound (one block: a plain store)
-    sh[0][t] = make_float4(B, 0.f, 0.f, 0.f);
-    __syncthreads();
-    if (t == 0) {
-      float m = 0.f;
-      for (int i = 0; i < gg.TPR; ++i) m = fmaxf(m, sh[0][i].x);
-      if (!(m < 3.0e38f)) m = 3.0e38f;  // inf / NaN gradients: the largest finite bound (scale 2^-114)
-      *bound = __float_as_uint(m);
     }
   }
 }
@@ -1083,20 +947,13 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
                  const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                  float* dbeta, float* dbias, int N, int H, int W, int C, int pool, int act, const TZ* res,
                  hipStream_t st, int* sig = nullptr, int sig_val = 0, const TZ* g2 = nullptr,
-                 const unsigned char* mask = nullptr, TZ* dyout = nullptr, unsigned* bound = nullptr,
-                 unsigned* tcnt = nullptr) {
+                 const unsigned char* mask = nullptr, TZ* dyout = nullptr, unsigned* bound = nullptr) {
   const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
   const int Mo = N * Ho * Wo;
   constexpr bool bf = sizeof(TZ) == 2;
   const int rpb = bwd_rows_per_block(Mo, C, bf);
   int nblk = (Mo + rpb - 1) / rpb;
   const bool wide = bwd_wide(Mo, C, bf);
-  // finalize in the reduce kernel's tail (tcnt given): the 256-thread geometry with one channel
-  // lane per thread column, and at most BWD_TAIL_MAXG groups
-  BwdTail tl{};
-  if (tcnt != nullptr && !wide && red_geom(C, RTB).CG == 1 && cdiv(nblk, BWD_TAIL_TG) <= BWD_TAIL_MAXG) {
-    tl = BwdTail{tcnt, part + (long)nblk * 5 * C, BWD_TAIL_TG, (float)N * H * W, gamma, dgamma, dbeta, dbias, coef};
-  }
   int nw = 0;  // bf16 in the 1024-thread geometry: 16-byte lanes (bn_wide.hip); 0 = not applicable
   if constexpr (sizeof(TZ) == 2) {
     if (wide && !pool && nsplit == 1) {
@@ -1108,12 +965,10 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
 #define RED(P, A)                                                                                               \
   if (wide)                                                                                                       \
     bn_bwd_reduce_kernel<P, A, TZ, RT><<<nblk, RT, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd, part, \
-                                                            N, H, W, C, rpb, sig, sig_val, g2, mask, dyout, bound,     \
-                                                            BwdTail{});                                                 \
+                                                            N, H, W, C, rpb, sig, sig_val, g2, mask, dyout, bound);     \
   else                                                                                                            \
     bn_bwd_reduce_kernel<P, A, TZ, RTB><<<nblk, RTB, 0, st>>>(gsrc, g, nsplit, z, res, scale, shift, mean, invstd,  \
-                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout, bound, \
-                                                              tl)
+                                                              part, N, H, W, C, rpb, sig, sig_val, g2, mask, dyout, bound)
   if (nw > 0) {
     nblk = nw;
   } else if (pool) {
@@ -1126,7 +981,6 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
     RED(false, 2);
   }
 #undef RED
-  if (nw == 0 && tl.cnt != nullptr) return (int)hipGetLastError();  // finalized in the reduce kernel's tail
   if (nw > 0)  // (bn_wide.hip's rows: the three sums)
     bn_bwd_finalize_kernel<8, 3><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
                                                              dgamma, dbeta, dbias, coef, nullptr);
@@ -1282,7 +1136,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
                 const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                 float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                 const TZ* res, TZ* dres, hipStream_t st, int* sig, int sig_val, const TZ* g2,
-                const unsigned char* mask, unsigned* bound, unsigned* tcnt) {
+                const unsigned char* mask, unsigned* bound) {
   if (nsplit < 1) nsplit = 1;
   if (np == 2 && (sizeof(TZ) != 4 || bound == nullptr || act != 0)) return -2;  // fp16 pairs: the VGG engine
   // add+ReLU: the reduce pass stores dy (= dres) and the apply pass reads it alone as an identity
@@ -1290,7 +1144,7 @@ int bn_bwd_host(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sca
   const bool dyp = act == 2 && nsplit == 1 && !pool && dres != nullptr;
   const int rc0 = bn_bwd_stats<TZ>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta,
                                    dbias, N, H, W, C, pool, act, res, st, sig, sig_val, g2, mask, dyp ? dres : nullptr,
-                                   np == 2 ? bound : nullptr, tcnt);
+                                   np == 2 ? bound : nullptr);
   if (rc0) return rc0;
   if (dyp) {
     act = 1;
@@ -1351,8 +1205,7 @@ long dpa_bn_part_floats(int M, int C, int bwd) {
   }
   const int r32 = bwd_rows_per_block(M, C, false), r16 = bwd_rows_per_block(M, C, true);
   const long nblk = std::max((M + r32 - 1) / r32, (M + r16 - 1) / r16);
-  // [block][5][C]: the three sums and the two maxima, then the finalize tail's group rows
-  return (nblk + cdiv((int)nblk, BWD_TAIL_TG)) * C * 5;
+  return nblk * C * 5;  // [block][5][C]: the three sums and the two maxima
 }
 
 // z [M][C] (or nsplit fp32 slabs of it in src; then z is written) -> partials -> finalize.
@@ -1414,7 +1267,7 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
                const float* mean, const float* invstd, const float* gamma, float* part, float* coef, float* dgamma,
                float* dbeta, float* dbias, float* dz, u16* dz3, int np, int N, int H, int W, int C, int pool, int act,
                const void* res, void* dres, int zbf, hipStream_t st, int* sig, int sig_val, const void* g2,
-               const unsigned char* mask, unsigned* bound, unsigned* tcnt) {
+               const unsigned char* mask, unsigned* bound) {
   if (C % 4 || act < 0 || act > 2 || (act != 0 && pool) || (act == 2 && ((!res && !mask) || !dres))) return -2;
   if (mask && act != 2) return -2;
   if (zbf && nsplit > 1) return -2;
@@ -1422,10 +1275,10 @@ int dpa_bn_bwd(const void* gsrc, int nsplit, void* g, const void* z, const float
   if (zbf)
     return bn_bwd_host<u16>((const u16*)gsrc, nsplit, (u16*)g, (const u16*)z, scale, shift, mean, invstd, gamma, part,
                             coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const u16*)res,
-                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask, bound, tcnt);
+                            (u16*)dres, st, sig, sig_val, (const u16*)g2, mask, bound);
   return bn_bwd_host<float>((const float*)gsrc, nsplit, (float*)g, (const float*)z, scale, shift, mean, invstd, gamma,
                             part, coef, dgamma, dbeta, dbias, dz, dz3, np, N, H, W, C, pool, act, (const float*)res,
-                            (float*)dres, st, sig, sig_val, (const float*)g2, mask, bound, tcnt);
+                            (float*)dres, st, sig, sig_val, (const float*)g2, mask, bound);
 }
 
 // Layer-0 backward (see bn_bwd_wgrad0_kernel): BN statistics, then the fused apply + weight gradient.
@@ -1435,12 +1288,11 @@ long dpa_wgrad0_part_floats(int N) { return (long)N * (16 / WB0_RPB) * 64 * 27; 
 int dpa_bn_bwd_wgrad0(const float* gsrc, int nsplit, float* g, const float* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                       float* coef, float* dgamma, float* dbeta, float* dbias, const float* x, float* wpart,
-                      float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val, unsigned* tcnt) {
+                      float* dw, int CP, int N, hipStream_t st, int* sig, int sig_val) {
   if (nsplit < 1) nsplit = 1;
   if (CP < 3) return -2;
   const int rc = bn_bwd_stats<float>(gsrc, nsplit, g, z, scale, shift, mean, invstd, gamma, part, coef, dgamma, dbeta,
-                                     dbias, N, 32, 32, 64, 1, 0, nullptr, st, sig, sig_val, nullptr, nullptr, nullptr,
-                                     nullptr, tcnt);
+                                     dbias, N, 32, 32, 64, 1, 0, nullptr, st, sig, sig_val);
   if (rc) return rc;
   const float* gg = nsplit > 1 ? g : gsrc;
   const int nblk = N * (16 / WB0_RPB);

@@ -319,12 +319,6 @@ class VGGEngine:
         self.fpart = torch.zeros(max(fpart, 1), **f32)
         self.fcnt = torch.zeros(max(fcnt, 32), dtype=torch.int32, device=dev)
         self.bn_tmo = torch.zeros(1, dtype=torch.int32, device=dev)
-        # BN backward finalize in the reduce kernel's tail (bn.hip BwdTail: two levels of last-block
-        # tickets; self-resetting counters, zeroed once here).  Off by default (measured slower, round 6):
-        # DPA_BN_TAIL=1 turns it on; otherwise the separate finalize
-        # kernel (A/B).
-        self.bn_tcnt = (torch.zeros(64, dtype=torch.int32, device=dev)
-                        if dev.type == "cuda" and os.environ.get("DPA_BN_TAIL", "0") == "1" else None)
         # BN statistics from the forward conv's epilogue (conv_x3.hip epi_col_stats) for layers whose
         # conv runs one split and whose BN is not the one-launch kernel: the statistics pass's read
         # of z goes; DPA_EPI_STATS=0 keeps bn_stats_kernel
@@ -848,12 +842,11 @@ class VGGEngine:
             dzbuf = self.dz3[i][:, :n] if self.planes[i] else self.dz[i][:n]
             names = [f"{l.conv_key}.weight", f"{l.conv_key}.bias", f"{l.bn_key}.weight", f"{l.bn_key}.bias"]
             bsig = dict(sig=self.bsig[i:i + 1], sig_val=epoch) if epoch else {}
-            tail = {"cnt": self.bn_tcnt} if self.bn_tcnt is not None else {}
             if i == 0 and self.fused_wgrad0:
                 K.bn_bwd_wgrad0(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                                 st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
                                 G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], x, self.wpart,
-                                G[f"{l.conv_key}.weight"], **bsig, **tail)
+                                G[f"{l.conv_key}.weight"], **bsig)
                 after_bn(i)
                 drain_side()
                 if grad_ready is not None:
@@ -870,7 +863,7 @@ class VGGEngine:
                 bnd = {"bound": self.dzb[i:i + 1]} if self.np == 2 and self.planes[i] else {}
                 K.bn_bwd(self.slab if gsplit > 1 else g, gsplit, g, z, st["scale"], st["shift"], st["mean"],
                          st["invstd"], P[f"{l.bn_key}.weight"], self.part, self.coef, G[f"{l.bn_key}.weight"],
-                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig, **bnd, **tail)
+                         G[f"{l.bn_key}.bias"], G[f"{l.conv_key}.bias"], dzbuf, l.pool, **bsig, **bnd)
             after_bn(i)
             if not self._wgrad_on_side(i):
                 # wgrad first: it needs no slab that bn_bwd(i-1) reads, and its bucket becomes ready early.
