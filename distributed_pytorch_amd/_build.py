@@ -27,8 +27,11 @@ import sysconfig
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
-BUILD_DIR = os.path.join(os.path.dirname(PKG_DIR), "build", "native")
-OUT_SO = os.path.join(PKG_DIR, "_C.so")
+# DPA_NO_PACKED_FP32=1: every kernel built without gfx950's packed fp32 instructions (A/B build,
+# written to build/native_nopk/_C.so; load it with DPA_EXT_SO=<path>, _ext.py)
+NOPK = os.environ.get("DPA_NO_PACKED_FP32", "0") == "1"
+BUILD_DIR = os.path.join(os.path.dirname(PKG_DIR), "build", "native_nopk" if NOPK else "native")
+OUT_SO = os.path.join(BUILD_DIR, "_C.so") if NOPK else os.path.join(PKG_DIR, "_C.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -83,8 +86,9 @@ def _compile_cmd(src, obj, torch_inc):
     common = ["-O3", "-fPIC", "-std=c++17", "-I" + CSRC, "-I" + os.path.join(ROCM, "include"),
               "-D__HIP_PLATFORM_AMD__=1", "-Wno-unused-result"]
     if src.endswith(".hip"):
+        nopk = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"] if NOPK else []
         return [os.path.join(ROCM, "bin", "hipcc"), "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-                "-c", src, "-o", obj] + common
+                "-c", src, "-o", obj] + common + nopk
     py_inc = sysconfig.get_paths()["include"]
     incs = ["-I" + p for p in torch_inc] + ["-I" + py_inc]
     return ["g++", "-c", src, "-o", obj, "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",

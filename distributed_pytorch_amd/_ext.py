@@ -7,7 +7,9 @@ callers (tests, the gloo oracle) never touch it.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 
 _mod = None
 _err: Exception | None = None
@@ -20,7 +22,14 @@ def _load():
     import torch  # noqa: F401  (loads torch's vendored libamdhip64 / librccl first)
 
     try:
-        _mod = importlib.import_module("distributed_pytorch_amd._C")
+        alt = os.environ.get("DPA_EXT_SO")  # an A/B build of the same sources (_build.py)
+        if alt:
+            spec = importlib.util.spec_from_file_location("distributed_pytorch_amd._C", alt)
+            _mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+            sys.modules["distributed_pytorch_amd._C"] = _mod
+        else:
+            _mod = importlib.import_module("distributed_pytorch_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
 

@@ -18,6 +18,15 @@ distributed_pytorch_amd/tuning/mi355x.json ([tile, splits, posmajor, isolated_ms
 count instead of the ``--top`` fastest overall.  The isolated ranking favours many splits (short
 conv, long slab reduction); on the weight-gradient stream, which shares the chip with the critical
 path, a configuration with fewer splits can win in the step although it loses alone.
+
+Precision gate (default on; ``--no-precision`` skips it): a plan changes the
+order and split of a conv's reduction, and with fp16-pair (h2) operands that moves the step's
+gradient errors (round 5: two faster candidate sets failed the parity suite afterwards).  So every
+candidate that wins on time is also scored BEFORE it is accepted: one batch-256 training step with
+the candidate plan installed, from the random init and from a trained state (200 x3 steps), each
+against fp64 autograd of the same step (tests/test_parity256_gpu.py's fixture).  It is accepted
+only if every gradient tensor stays within 4x of the step's error floor and the median tensor
+within ``--gate-median`` (default 1.3, the suite's bound being 1.5) of torch fp32's own error.
 """
 import argparse
 import json
@@ -81,6 +90,55 @@ def isolated(e, i, kind, n, iters=3):
     return sorted(res)
 
 
+class PrecisionGate:
+    """Scores a plan table (the tuning engine's ``_cfg_cache``) against fp64 autograd at batch 256,
+    from the random init and from a trained state, with the parity suite's own fixture."""
+
+    def __init__(self, impl, gate_median=1.3, trained_steps=200):
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import test_parity256_gpu as P  # noqa: E402  (the suite's fixture, not a copy of it)
+
+        self.P, self.impl, self.gate_median = P, impl, gate_median
+        self.refs = [P._reference()]
+        if trained_steps:
+            self.refs.append(P._reference(P._trained_state(trained_steps), data_seed=512))
+        self.floor, self.tref = [], []
+        for ref in self.refs:
+            tg, _ = P._torch_fp32_errors(ref)
+            pert = ([P._perturbed_errors(ref, sd, torch.float64) for sd in (1, 2)]
+                    + [P._perturbed_errors(ref, sd, torch.float32) for sd in (3, 4)])
+            self.tref.append(tg)
+            self.floor.append({n: (None if e is None else max([e] + [p[n] for p in pert])) for n, e in tg.items()})
+
+    def score(self, cfg_cache):
+        """{"median": worst median ratio vs torch fp32, "worst_floor": worst ratio to the floor, "ok": bool}"""
+        from distributed_pytorch_amd.engine import VGGEngine
+
+        med, worst, per = 0.0, 0.0, []
+        for ref, floor, tref in zip(self.refs, self.floor, self.tref):
+            e = VGGEngine("VGG11", "cuda", max_batch=self.P.N, impl=self.impl)
+            e._cfg_cache.update({k: v for k, v in cfg_cache.items() if k[2] == self.P.N})
+            e.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref["sd0"].items()})
+            x4 = torch.zeros(self.P.N, 32, 32, 4)
+            x4[..., :3] = ref["x"].float().permute(0, 2, 3, 1)
+            e.forward_backward(x4.cuda(), ref["t"].cuda())
+            torch.cuda.synchronize()
+            e.check_signals()
+            ratios = []
+            for n, gref in ref["grads"].items():
+                if gref.abs().max() < 1e-7:
+                    continue
+                err = self.P._rel(e._to_torch_layout(n, e.grads[n]).cpu(), gref)
+                worst = max(worst, err / (floor[n] + 1e-5 / 4.0))
+                ratios.append(err / max(tref[n], 1e-12))
+            ratios.sort()
+            med = max(med, ratios[len(ratios) // 2])
+            per.append(round(ratios[len(ratios) // 2], 3))
+            del e
+        return {"median": round(med, 3), "worst_floor": round(worst, 3), "per_ref_median": per,
+                "ok": med <= self.gate_median and worst <= 4.0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -94,6 +152,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="report, do not write the table")
     ap.add_argument("--per-split", action="store_true",
                     help="candidates: the fastest isolated config of every split count (not the --top overall)")
+    ap.add_argument("--no-precision", action="store_true", help="skip the precision gate (timing only)")
+    ap.add_argument("--gate-median", type=float, default=1.3)
     a = ap.parse_args()
     args = bench.parse(["--batch", str(a.batch), "--impl", a.impl])
     dev = torch.device("cuda", 0)
@@ -104,6 +164,11 @@ def main():
     n = a.batch
     base = step_ms(step, a.steps, a.reps)
     print(json.dumps({"start_step_ms": round(base, 4)}), flush=True)
+    gate = None if a.no_precision else PrecisionGate(a.impl, a.gate_median)
+    if gate is not None:
+        g0 = gate.score(engine._cfg_cache)
+        print(json.dumps({"start_precision": g0}), flush=True)
+    rejected = {}
     # group layers by table key (layers of identical shape share one entry)
     groups = {}
     for kind in a.kinds.split(","):
@@ -138,6 +203,12 @@ def main():
             ms = step_ms(step, a.steps, a.reps)
             print(f"  {k} {c} iso={iso.get(c, 0):.4f} step={ms:.4f} (cur {cur} {cur_ms:.4f})", flush=True)
             if ms < best_ms * (1 - a.min_gain):
+                if gate is not None:  # faster: is it still fp32-grade?
+                    sc = gate.score(engine._cfg_cache)
+                    print(f"    precision {sc}", flush=True)
+                    if not sc["ok"]:
+                        rejected.setdefault(k, []).append([list(c), round(ms, 4), sc])
+                        continue
                 best, best_ms = c, ms
         for i in layers:
             engine._cfg_cache[(engine._layer_impl(i), kind, n, i)] = best
@@ -148,8 +219,11 @@ def main():
         print(json.dumps({"key": k, "layers": layers, "choice": list(best), "was": list(cur),
                           "step_ms": round(best_ms, 4), "was_ms": round(cur_ms, 4)}), flush=True)
     final = step_ms(step, a.steps, a.reps * 2)
-    print(json.dumps({"start_step_ms": round(base, 4), "final_step_ms": round(final, 4),
-                      "changed": changed}), flush=True)
+    out = {"start_step_ms": round(base, 4), "final_step_ms": round(final, 4), "changed": changed,
+           "rejected_on_precision": rejected}
+    if gate is not None:
+        out["final_precision"] = gate.score(engine._cfg_cache)
+    print(json.dumps(out), flush=True)
     if changed and not a.dry_run:
         table.update(changed)
         with open(a.out, "w") as f:
