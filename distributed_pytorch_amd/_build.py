@@ -29,9 +29,11 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 # DPA_NO_PACKED_FP32=1: every kernel built without gfx950's packed fp32 instructions (A/B build,
 # written to build/native_nopk/_C.so; load it with DPA_EXT_SO=<path>, _ext.py)
+# DPA_BUILD_TAG=<tag>: any A/B build of the working tree, to build/native_<tag>/_C.so likewise
 NOPK = os.environ.get("DPA_NO_PACKED_FP32", "0") == "1"
-BUILD_DIR = os.path.join(os.path.dirname(PKG_DIR), "build", "native_nopk" if NOPK else "native")
-OUT_SO = os.path.join(BUILD_DIR, "_C.so") if NOPK else os.path.join(PKG_DIR, "_C.so")
+TAG = os.environ.get("DPA_BUILD_TAG") or ("nopk" if NOPK else "")
+BUILD_DIR = os.path.join(os.path.dirname(PKG_DIR), "build", "native_" + TAG if TAG else "native")
+OUT_SO = os.path.join(BUILD_DIR, "_C.so") if TAG else os.path.join(PKG_DIR, "_C.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 

@@ -654,7 +654,7 @@ void bn_bwd_wgrad0(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale
               "bn_bwd_wgrad0: dw [64,3,3,CP]");
   TORCH_CHECK(wpart.numel() >= dpa_wgrad0_part_floats(N), "bn_bwd_wgrad0: wpart too small");
   TORCH_CHECK(part.numel() >= dpa_bn_part_floats(N * 256, 64, 1), "bn_bwd_wgrad0: part too small");
-  TORCH_CHECK(coef.numel() >= 3 * 64 && scale.numel() == 64 && gamma.numel() == 64, "bn_bwd_wgrad0: channel vectors");
+  TORCH_CHECK(coef.numel() >= 4 * 64 && scale.numel() == 64 && gamma.numel() == 64, "bn_bwd_wgrad0: channel vectors");
   chk(dpa_bn_bwd_wgrad0(fp(gsrc), (int)nsplit, fp(g), fp(z), fp(scale), fp(shift), fp(mean), fp(invstd), fp(gamma),
                         fp(part), fp(coef), fp(dgamma), fp(dbeta), ofp(dbias), fp(x), fp(wpart), fp(dw),
                         (int)dw.size(3), N, cur_stream(), opt_signal(sig, "bn_bwd_wgrad0"), (int)sig_val),
@@ -807,7 +807,7 @@ void bn_bwd(Tensor gsrc, int64_t nsplit, Tensor g, Tensor z, Tensor scale, Tenso
   TORCH_CHECK(g.numel() == (int64_t)Mo * C, "bn_bwd: g shape");
   TORCH_CHECK(gsrc.numel() >= nsplit * (int64_t)Mo * C, "bn_bwd: gsrc too small");
   TORCH_CHECK(part.numel() >= dpa_bn_part_floats(Mo, C, 1), "bn_bwd: part too small");
-  TORCH_CHECK(coef.numel() >= 3L * C, "bn_bwd: coef too small");
+  TORCH_CHECK(coef.numel() >= 4L * C, "bn_bwd: coef too small (4 rows: k1, c2, k3, mean)");
   const void* g2p = nullptr;
   if (g2.has_value() && g2->defined()) {
     TORCH_CHECK(g2->numel() == g.numel() && g2->scalar_type() == g.scalar_type() && nsplit == 1,

@@ -141,6 +141,23 @@ __device__ __forceinline__ void tree_rows_max(float4 (*sh)[T], int t, int lane_r
 
 #define F4GET(v, k) ((k) == 0 ? (v).x : (k) == 1 ? (v).y : (k) == 2 ? (v).z : (v).w)
 
+// fp64 lanes of the backward sums (bn_bwd_reduce_kernel)
+struct __attribute__((aligned(16))) dbl4 {
+  double x, y, z, w;
+};
+template <int T>
+__device__ __forceinline__ void tree_rows_d(dbl4* sh, int t, int lane_r, int TPR, int RPI) {
+  int p2 = 1;
+  while (p2 < RPI) p2 <<= 1;
+  for (int o = p2 >> 1; o >= 1; o >>= 1) {
+    if (lane_r < o && lane_r + o < RPI) {
+      const dbl4 a = sh[t], b = sh[t + o * TPR];
+      sh[t] = dbl4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+    }
+    __syncthreads();
+  }
+}
+
 
 // ---- output writer: NP == 0 -> fp32 float4 store; NP in {1,3} -> bf16 planes x = x0 (+ x1 + x2);
 // NP 2 -> the fp16 pair of x * s (common.h split_val) -- the next conv reads MFMA-ready operands.
@@ -472,7 +489,11 @@ __device__ __forceinline__ void route1(float z00, float z01, float z10, float z1
 }
 
 // Per-channel backward finalize from the complete sums: dgamma, dbeta, dbias and the dz coefficients
-// dz = k1*dy + c2*z + c3.  Returns the channel's dz bound |k1| max|dy| + |c2| max|z| + |c3|.
+// of the CENTRED form dz = k1*dy + c2*(z - mean) + k3 (coef rows: k1, c2, k3, mean).  The centred form
+// keeps the x-hat term's rounding relative to |z - mean| instead of |z|: the expanded
+// c2*z + (k3 - c2*mean) cancels when |mean| >> sigma, which trained layers reach, and its rounding
+// then grew every lower layer's gradients (docs/PERF_NOTES.md round 6; torch's CPU backward also
+// forms (z - mean)).  Returns the channel's dz bound |k1| max|dy| + |c2| max|z - mean| + |k3|.
 __device__ __forceinline__ float bwd_coef(int c, int C, float sdy, float sdx, float sx, float mdy, float mz,
                                           float Mfull, const float* __restrict__ gamma,
                                           const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -482,20 +503,50 @@ __device__ __forceinline__ float bwd_coef(int c, int C, float sdy, float sdx, fl
   const float k1 = gm * iv;
   const float k2x = -k1 * sdx / Mfull;  // coefficient of xhat
   const float k3 = -k1 * sdy / Mfull;
-  const float c2 = k2x * iv, c3 = k3 - k2x * iv * mean[c];
+  const float c2 = k2x * iv;
   dgamma[c] = sdx;
   dbeta[c] = sdy;
   if (dbias) dbias[c] = k2x * sx;  // = sum over rows of dz (analytically 0)
   coef[c] = k1;
-  coef[C + c] = c2;      // coefficient of z
-  coef[2 * C + c] = c3;  // constant
+  coef[C + c] = c2;      // coefficient of z - mean
+  coef[2 * C + c] = k3;  // constant
+  coef[3 * C + c] = mean[c];
   // (rounding of the fma chain stays far inside the 2^14 -> 65504 headroom of the scale)
-  return fabsf(k1) * mdy + fabsf(c2) * mz + fabsf(c3);
+  return fabsf(k1) * mdy + fabsf(c2) * mz + fabsf(k3);
 }
 
-// Backward reduce: per (row-block, channel) sums of dy, dy*xhat, xhat and maxima of |dy|, |z| (the
-// data-gradient bound of fp16-pair planes, bn_bwd_finalize_kernel).  Rows are OUTPUT rows of
-// the layer (pooled positions when POOL).  part: [block][5][C].  If nsplit > 1, gsrc holds the split-K slabs of g and
+// The same from fp64 sums of dy, dy (z - mean) and (z - mean) (bn_bwd_reduce_kernel): the arithmetic in
+// double, the outputs rounded once.
+__device__ __forceinline__ float bwd_coef_d(int c, int C, double sdy, double sdc, double sxc, float mdy, float mz,
+                                            double Mfull, const float* __restrict__ gamma,
+                                            const float* __restrict__ mean, const float* __restrict__ invstd,
+                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                            float* __restrict__ dbias, float* __restrict__ coef) {
+  const double iv = invstd[c], gm = gamma[c];
+  const double sdx = sdc * iv;  // sum dy * xhat
+  const double k1 = gm * iv;
+  const double k2x = -k1 * sdx / Mfull;
+  const double k3 = -k1 * sdy / Mfull;
+  const double c2 = k2x * iv;
+  dgamma[c] = (float)sdx;
+  dbeta[c] = (float)sdy;
+  if (dbias) dbias[c] = (float)(k2x * sxc * iv);
+  coef[c] = (float)k1;
+  coef[C + c] = (float)c2;
+  coef[2 * C + c] = (float)k3;
+  coef[3 * C + c] = mean[c];
+  return (float)(fabs(k1) * mdy + fabs(c2) * mz + fabs(k3));
+}
+
+// Backward reduce: per (row-block, channel) sums of dy, dy*(z - mean), (z - mean) and maxima of |dy|,
+// |z| (the data-gradient bound of fp16-pair planes, bn_bwd_finalize_kernel).  Rows are OUTPUT rows of
+// the layer (pooled positions when POOL).  The three sums leave each thread's short run of rows
+// (2-8 rows in the VGG geometry) in FP64: the block tree, the partials and the finalize sum in
+// double (torch's CPU batch norm accumulates in double too): the BN parameter gradients are sums
+// over up to 262,144 rows that cancel heavily once the network trains, and fp32 accumulation left
+// dgamma / dbeta several times further from fp64 than stock torch fp32 at a trained state
+// (docs/PERF_NOTES.md round 6; fp64 arithmetic per element measured 1.5 % slower in the step).  part: [block][3][C] doubles, then [block][2][C]
+// floats (the maxima) at float offset gridDim.x * 6 * C.  If nsplit > 1, gsrc holds the split-K slabs of g and
 // the summed g is written to gout (consumed by the apply pass).  g2 (optional, nsplit == 1): a second
 // contribution to the same gradient, summed on load here and in the apply pass instead of by a
 // separate add pass (ResNet: a block input's two gradient contributions, ops/functional.GradJoin).
@@ -528,11 +579,13 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(Mo, r0 + rpb);
   const long slab4 = (long)Mo * gg.C4;
-  __shared__ float4 sh[1][RTB];  // one tree buffer, used for the three sums in turn
+  __shared__ dbl4 shd[RTB];  // one tree buffer, used for the three sums in turn (and the maxima,
+                             // as float4 in its first half)
+  float4(*sh)[RTB] = reinterpret_cast<float4(*)[RTB]>(shd);
   for (int cg = 0; cg < gg.CG; ++cg) {
     const int c4 = lane_c + cg * gg.TPR;
     const bool cval = active && c4 < gg.C4;
-    float sdy[4] = {0, 0, 0, 0}, sdx[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
+    float sdy[4] = {0, 0, 0, 0}, sdx[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};  // dy, dy (z - mu), z - mu
     float mdy[4] = {0, 0, 0, 0}, mz[4] = {0, 0, 0, 0};  // max |dy|, max |z|
     if (cval) {
       const float4 sc = reinterpret_cast<const float4*>(scale)[c4];
@@ -568,12 +621,12 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
               const float dy = mk ? (((mv[u] >> k) & 1u) ? F4GET(gv[u], k) : 0.f)
                                   : act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv[u], k),
                                                   F4GET(gv[u], k));
-              const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
+              const float zc = zz - F4GET(mu, k);
               sdy[k] += dy;
-              sdx[k] = fmaf(dy, xh, sdx[k]);
-              sx[k] += xh;
+              sdx[k] = fmaf(dy, zc, sdx[k]);
+              sx[k] += zc;
               mdy[k] = fmaxf(mdy[k], fabsf(dy));
-              mz[k] = fmaxf(mz[k], fabsf(zz));
+              mz[k] = fmaxf(mz[k], fabsf(zz - F4GET(mu, k)));
               dyu[k] = dy;
             }
             if (ACT == 2 && dyout) st4(dyout, gi[u], make_float4(dyu[0], dyu[1], dyu[2], dyu[3]));
@@ -601,12 +654,12 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             const float zz = F4GET(zv, k);
             const float dy = mk ? (((m >> k) & 1u) ? F4GET(gv, k) : 0.f)
                                 : act_grad<ACT>(fmaf(zz, F4GET(sc, k), F4GET(sh, k)), F4GET(rv, k), F4GET(gv, k));
-            const float xh = (zz - F4GET(mu, k)) * F4GET(is, k);
+            const float zc = zz - F4GET(mu, k);
             sdy[k] += dy;
-            sdx[k] = fmaf(dy, xh, sdx[k]);
-            sx[k] += xh;
+            sdx[k] = fmaf(dy, zc, sdx[k]);
+            sx[k] += zc;
             mdy[k] = fmaxf(mdy[k], fabsf(dy));
-            mz[k] = fmaxf(mz[k], fabsf(zz));
+            mz[k] = fmaxf(mz[k], fabsf(zz - F4GET(mu, k)));
             dyv[k] = dy;
           }
           if (ACT == 2 && dyout) st4(dyout, gi, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
@@ -623,31 +676,39 @@ __global__ __launch_bounds__(RTB) void bn_bwd_reduce_kernel(const TZ* __restrict
             float d00, d01, d10, d11;
             route1(F4GET(z00, k), F4GET(z01, k), F4GET(z10, k), F4GET(z11, k), F4GET(sc, k), F4GET(sh, k),
                    F4GET(gv, k), d00, d01, d10, d11);
-            const float m = F4GET(mu, k), iv = F4GET(is, k);
-            const float x00 = (F4GET(z00, k) - m) * iv, x01 = (F4GET(z01, k) - m) * iv;
-            const float x10 = (F4GET(z10, k) - m) * iv, x11 = (F4GET(z11, k) - m) * iv;
-            sdy[k] += (d00 + d01) + (d10 + d11);
-            sdx[k] += (d00 * x00 + d01 * x01) + (d10 * x10 + d11 * x11);
+            const float m = F4GET(mu, k);
+            const float x00 = F4GET(z00, k) - m, x01 = F4GET(z01, k) - m;
+            const float x10 = F4GET(z10, k) - m, x11 = F4GET(z11, k) - m;
+            sdy[k] += (d00 + d01) + (d10 + d11);  // (at most one routed term is non-zero)
+            sdx[k] = fmaf(d00, x00, fmaf(d01, x01, fmaf(d10, x10, fmaf(d11, x11, sdx[k]))));
             sx[k] += (x00 + x01) + (x10 + x11);
             mdy[k] = fmaxf(mdy[k], fmaxf(fmaxf(fabsf(d00), fabsf(d01)), fmaxf(fabsf(d10), fabsf(d11))));
-            mz[k] = fmaxf(mz[k], fmaxf(fmaxf(fabsf(F4GET(z00, k)), fabsf(F4GET(z01, k))),
-                                       fmaxf(fabsf(F4GET(z10, k)), fabsf(F4GET(z11, k)))));
+            const float mf = F4GET(mu, k);
+            mz[k] = fmaxf(mz[k], fmaxf(fmaxf(fabsf(F4GET(z00, k) - mf), fabsf(F4GET(z01, k) - mf)),
+                                       fmaxf(fabsf(F4GET(z10, k) - mf), fabsf(F4GET(z11, k) - mf))));
           }
         }
       }
     }
-    const float4 vals[5] = {make_float4(sdy[0], sdy[1], sdy[2], sdy[3]), make_float4(sdx[0], sdx[1], sdx[2], sdx[3]),
-                            make_float4(sx[0], sx[1], sx[2], sx[3]), make_float4(mdy[0], mdy[1], mdy[2], mdy[3]),
-                            make_float4(mz[0], mz[1], mz[2], mz[3])};
-    float* o = part + (long)blockIdx.x * 5 * C + c4 * 4;
+    const dbl4 dv[3] = {dbl4{(double)sdy[0], (double)sdy[1], (double)sdy[2], (double)sdy[3]},
+                        dbl4{(double)sdx[0], (double)sdx[1], (double)sdx[2], (double)sdx[3]},
+                        dbl4{(double)sx[0], (double)sx[1], (double)sx[2], (double)sx[3]}};
+    double* od = reinterpret_cast<double*>(part) + (long)blockIdx.x * 3 * C + c4 * 4;
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < 3; ++q) {
+      shd[t] = dv[q];
+      __syncthreads();
+      tree_rows_d<RTB>(shd, t, lane_r, gg.TPR, gg.RPI);
+      if (cval && lane_r == 0) *reinterpret_cast<dbl4*>(od + q * C) = shd[t];
+      __syncthreads();
+    }
+    const float4 vals[2] = {make_float4(mdy[0], mdy[1], mdy[2], mdy[3]), make_float4(mz[0], mz[1], mz[2], mz[3])};
+    float* o = part + (long)gridDim.x * 6 * C + (long)blockIdx.x * 2 * C + c4 * 4;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
       sh[0][t] = vals[q];
       __syncthreads();
-      if (q < 3)
-        tree_rows<1, RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
-      else
-        tree_rows_max<RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
+      tree_rows_max<RTB>(sh, t, lane_r, gg.TPR, gg.RPI);
       if (cval && lane_r == 0) *reinterpret_cast<float4*>(o + q * C) = sh[0][t];
       __syncthreads();
     }
@@ -747,6 +808,88 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
+// The finalize of bn_bwd_reduce_kernel's partials: fp64 sums [block][3][C] (dy, dy (z - mean),
+// z - mean) and fp32 maxima [block][2][C] at float offset nblk * 6 * C.  Same geometry and fixed order
+// as bn_bwd_finalize_kernel, the sums and the coefficient arithmetic in double (bwd_coef_d).
+template <int BF_CPB>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_d_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                float Mfull, const float* __restrict__ gamma,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                float* __restrict__ dbias, float* __restrict__ coef,
+                                                                unsigned* __restrict__ bound) {
+  constexpr int G = 256 / BF_CPB;  // partial-row groups per channel
+  const int cl = threadIdx.x % BF_CPB, grp = threadIdx.x / BF_CPB;
+  const int c = blockIdx.x * BF_CPB + cl;
+  const bool mx = bound != nullptr;
+  const double* pd = reinterpret_cast<const double*>(part);
+  const float* pf = part + (long)nblk * 6 * C;
+  double a = 0.0, b = 0.0, x = 0.0;
+  float mdy = 0.f, mz = 0.f;
+  if (c < C) {
+    for (int k = grp; k < nblk; k += 16 * G) {  // 16 rows per thread in flight, branch-free masking
+      double pa[16], pb[16], px[16];
+      float pm[16], pz[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const bool v = k + G * u < nblk;
+        const long row = v ? k + G * u : 0;
+        const double* p = pd + row * 3 * C + c;
+        const float* q = pf + row * 2 * C + c;
+        const double l0 = p[0], l1 = p[C], l2 = p[2 * C];
+        const float l3 = q[0], l4 = q[C];
+        pa[u] = v ? l0 : 0.0;
+        pb[u] = v ? l1 : 0.0;
+        px[u] = v ? l2 : 0.0;
+        pm[u] = v ? l3 : 0.f;
+        pz[u] = v ? l4 : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        a += pa[u];
+        b += pb[u];
+        x += px[u];
+        mdy = fmaxf(mdy, pm[u]);
+        mz = fmaxf(mz, pz[u]);
+      }
+    }
+  }
+  __shared__ double shd[3][256];
+  __shared__ float shf[2][256];
+  shd[0][threadIdx.x] = a;
+  shd[1][threadIdx.x] = b;
+  shd[2][threadIdx.x] = x;
+  shf[0][threadIdx.x] = mdy;
+  shf[1][threadIdx.x] = mz;
+  __syncthreads();
+  for (int o = 128; o >= BF_CPB; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      shd[0][threadIdx.x] += shd[0][threadIdx.x + o];
+      shd[1][threadIdx.x] += shd[1][threadIdx.x + o];
+      shd[2][threadIdx.x] += shd[2][threadIdx.x + o];
+      shf[0][threadIdx.x] = fmaxf(shf[0][threadIdx.x], shf[0][threadIdx.x + o]);
+      shf[1][threadIdx.x] = fmaxf(shf[1][threadIdx.x], shf[1][threadIdx.x + o]);
+    }
+    __syncthreads();
+  }
+  float B = 0.f;
+  if (grp == 0 && c < C)
+    B = bwd_coef_d(c, C, shd[0][cl], shd[1][cl], shd[2][cl], shf[0][cl], shf[1][cl], Mfull, gamma, mean, invstd,
+                   dgamma, dbeta, dbias, coef);
+  if (mx) {  // the block's channels' largest bound, one atomic per block
+    __syncthreads();
+    if (grp == 0) shf[0][cl] = B;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = 0.f;
+      for (int q = 0; q < BF_CPB; ++q) m = fmaxf(m, shf[0][q]);
+      if (!(m < 3.0e38f)) m = 3.0e38f;  // inf / NaN gradients: the largest finite bound (scale 2^-114)
+      atomicMax(bound, __float_as_uint(m));
+    }
+  }
+}
+
 template <bool POOL, int NP, int ACT, typename TZ>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict__ g, const TZ* __restrict__ z,
                                                            const float* __restrict__ scale,
@@ -764,12 +907,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
   // fp16-pair planes (NP 2): the scale of the bound the finalize wrote
   const float dsc = NP == 2 ? h2_scale_of_bound(__uint_as_float(*bound)) : 1.f;
   struct Co {
-    float4 sc, sh, k1, k2, k3;
+    float4 sc, sh, k1, k2, k3, mu;
   };
-  auto coefs = [&](int c4) {
+  auto coefs = [&](int c4) {  // (centred form: dz = k1 dy + k2 (z - mu) + k3, bwd_coef)
     return Co{reinterpret_cast<const float4*>(scale)[c4], reinterpret_cast<const float4*>(shift)[c4],
               reinterpret_cast<const float4*>(coef)[c4], reinterpret_cast<const float4*>(coef + C)[c4],
-              reinterpret_cast<const float4*>(coef + 2 * C)[c4]};
+              reinterpret_cast<const float4*>(coef + 2 * C)[c4], reinterpret_cast<const float4*>(coef + 3 * C)[c4]};
   };
   auto body = [&](long i, int c4, const Co& q) {
     float4 gv = ld4(g, i);
@@ -788,7 +931,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
         dyv[k] = dy;
         // explicit fma order: every ACT instantiation rounds alike (the dy pass's ACT 1 apply is
         // bitwise the ACT 2 one it replaces)
-        r[k] = fmaf(F4GET(q.k1, k), dy, fmaf(F4GET(q.k2, k), zz, F4GET(q.k3, k)));
+        r[k] = fmaf(F4GET(q.k1, k), dy, fmaf(F4GET(q.k2, k), zz - F4GET(q.mu, k), F4GET(q.k3, k)));
       }
       store4<NP>(dz, dz3, ps, i, make_float4(r[0], r[1], r[2], r[3]), dsc);
       if constexpr (ACT == 2) st4(dres, i, make_float4(dyv[0], dyv[1], dyv[2], dyv[3]));
@@ -809,7 +952,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const TZ* __restrict_
                F4GET(gv, k), d[0], d[1], d[2], d[3]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          out[u][k] = fmaf(F4GET(q.k1, k), d[u], fmaf(F4GET(q.k2, k), F4GET(zq[u], k), F4GET(q.k3, k)));
+          out[u][k] = fmaf(F4GET(q.k1, k), d[u], fmaf(F4GET(q.k2, k), F4GET(zq[u], k) - F4GET(q.mu, k), F4GET(q.k3, k)));
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -985,8 +1128,8 @@ int bn_bwd_stats(const TZ* gsrc, int nsplit, TZ* g, const TZ* z, const float* sc
     bn_bwd_finalize_kernel<8, 3><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
                                                              dgamma, dbeta, dbias, coef, nullptr);
   else
-    bn_bwd_finalize_kernel<8, 5><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
-                                                             dgamma, dbeta, dbias, coef, bound);
+    bn_bwd_finalize_d_kernel<8><<<cdiv(C, 8), 256, 0, st>>>(part, nblk, C, (float)N * H * W, gamma, mean, invstd,
+                                                            dgamma, dbeta, dbias, coef, bound);
   return (int)hipGetLastError();
 }
 
@@ -1033,6 +1176,7 @@ __global__ __launch_bounds__(256) void bn_bwd_wgrad0_kernel(const float* __restr
   const float4 k1 = reinterpret_cast<const float4*>(coef)[c4];
   const float4 k2 = reinterpret_cast<const float4*>(coef + C)[c4];
   const float4 k3 = reinterpret_cast<const float4*>(coef + 2 * C)[c4];
+  const float4 mu = reinterpret_cast<const float4*>(coef + 3 * C)[c4];  // (centred form, bwd_coef)
   float acc[4][27];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -1053,7 +1197,8 @@ __global__ __launch_bounds__(256) void bn_bwd_wgrad0_kernel(const float* __restr
       route1(F4GET(zq[0], k), F4GET(zq[1], k), F4GET(zq[2], k), F4GET(zq[3], k), F4GET(sc, k), F4GET(sh, k),
              F4GET(gv, k), r[0], r[1], r[2], r[3]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[q][k] = F4GET(k1, k) * r[q] + F4GET(k2, k) * F4GET(zq[q], k) + F4GET(k3, k);
+      for (int q = 0; q < 4; ++q)
+        d[q][k] = F4GET(k1, k) * r[q] + F4GET(k2, k) * (F4GET(zq[q], k) - F4GET(mu, k)) + F4GET(k3, k);
     }
     // the 4x4 input neighbourhood of the 2x2 window: rows 2oh-1 .. 2oh+2, columns 2ow-1 .. 2ow+2
     const int xr = 2 * oh - 1 - h_lo;  // staged row of input row 2oh-1
@@ -1204,8 +1349,9 @@ long dpa_bn_part_floats(int M, int C, int bwd) {
     return (long)((M + rpb - 1) / rpb) * C * 2;
   }
   const int r32 = bwd_rows_per_block(M, C, false), r16 = bwd_rows_per_block(M, C, true);
-  const long nblk = std::max((M + r32 - 1) / r32, (M + r16 - 1) / r16);
-  return nblk * C * 5;  // [block][5][C]: the three sums and the two maxima
+  // fp32 geometry: [block][3][C] fp64 sums + [block][2][C] maxima (8 floats per (block, channel));
+  // bf16 wide reduce (bn_wide.hip): [block][3][C] fp32
+  return std::max((long)((M + r32 - 1) / r32) * 8, (long)((M + r16 - 1) / r16) * 5) * C;
 }
 
 // z [M][C] (or nsplit fp32 slabs of it in src; then z is written) -> partials -> finalize.

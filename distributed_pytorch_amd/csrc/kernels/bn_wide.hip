@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void bn_apply_wide_kernel(const uint4* __restr
 }
 
 // backward apply: dy = g (+ g2) through the ReLU mask recomputed from z (ACT 0) or as is (ACT 1);
-// dz = fma(k1, dy, fma(k2, z, k3))
+// dz = fma(k1, dy, fma(k2, z - mu, k3)) (the centred coefficients of bn.hip bwd_coef)
 template <int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_wide_kernel(const uint4* __restrict__ g, const uint4* __restrict__ g2,
                                                                 const uint4* __restrict__ z, uint4* __restrict__ dz,
@@ -108,12 +108,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_wide_kernel(const uint4* __r
   const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c8 = (int)(i0 % C8);
   const int C = 8 * C8;
-  float sc[8], sh[8], k1[8], k2[8], k3[8];
+  float sc[8], sh[8], k1[8], k2[8], k3[8], mu[8];
   coef8(scale, c8, sc);
   coef8(shift, c8, sh);
   coef8(coef, c8, k1);
   coef8(coef + C, c8, k2);
   coef8(coef + 2 * C, c8, k3);
+  coef8(coef + 3 * C, c8, mu);
   auto body = [&](uint4 gv, uint4 g2v, uint4 zv, long i) {
     float gf[8], zf[8], o[8];
     unpack8(gv, gf);
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_wide_kernel(const uint4* __r
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float dy = ACT == 0 ? (fmaf(zf[e], sc[e], sh[e]) > 0.f ? gf[e] : 0.f) : gf[e];
-      o[e] = fmaf(k1[e], dy, fmaf(k2[e], zf[e], k3[e]));
+      o[e] = fmaf(k1[e], dy, fmaf(k2[e], zf[e] - mu[e], k3[e]));
     }
     dz[i] = pack8(o);
   };

@@ -332,7 +332,7 @@ class VGGEngine:
         self.epart = torch.empty(max(epart, 1), **f32)
         # BN reduction workspace
         self.part = torch.zeros(part_need, **f32)
-        self.coef = torch.empty(3 * max(l.cout for l in L), **f32)
+        self.coef = torch.empty(4 * max(l.cout for l in L), **f32)  # [k1, c2, k3, mean] (bn.hip bwd_coef)
         self.loss_row = torch.zeros(N, **f32)
         self.dlogits = torch.zeros(N, num_classes, **f32)
         self.loss = torch.zeros(1, **f32)

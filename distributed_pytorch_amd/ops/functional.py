@@ -580,7 +580,7 @@ class BnActNHWC(torch.autograd.Function):
         dgamma, dbeta = _bn_grad_bufs(ctx.params[:2], C, f32)
         dres = torch.empty_like(z) if ctx.act == 2 else None
         part = WS.get("bn_part", K.bn_part_floats(N * H * W, C, True), z.device, zero=True) if native else None
-        coef = torch.empty(3 * C, **f32)
+        coef = torch.empty(4 * C, **f32)
         g2 = None  # ... summed on load by the kernels
         if ent is not None:
             if native and ent[1].dtype == da.dtype and ent[1].numel() == da.numel():

@@ -148,7 +148,7 @@ def test_bn_three_kernel_backward(shape, nsplit):
     d = lambda t: t.cuda()
     Ho, Wo = gout.shape[1:3]
     part = torch.zeros(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
-    coef = torch.empty(3 * C, device="cuda")
+    coef = torch.empty(4 * C, device="cuda")
     out = [torch.zeros(C, device="cuda") for _ in range(3)]
     dz = torch.empty(z.shape, device="cuda")
     if nsplit == 1:
@@ -187,7 +187,7 @@ def test_bn_backward_fp16_pair_planes(shape, nsplit):
     part = torch.zeros(C_.bn_part_floats(N * Ho * Wo, C, True), device="cuda")
     outs = []
     for kind in ("fp32", "h2"):
-        coef = torch.empty(3 * C, device="cuda")
+        coef = torch.empty(4 * C, device="cuda")
         o = [torch.zeros(C, device="cuda") for _ in range(3)]
         dz = (torch.empty(z.shape, device="cuda") if kind == "fp32"
               else torch.empty((2,) + tuple(z.shape), device="cuda", dtype=torch.float16))

@@ -84,7 +84,7 @@ def _bwd_compare(monkeypatch, shape, act, with_g2, use_mask, exact):
         dz = torch.empty_like(d["z"])
         dres = torch.empty_like(d["z"]) if act == 2 else None
         part = torch.zeros(K.bn_part_floats(N * H * W, C, True), device="cuda")
-        coef = torch.empty(3 * C, device="cuda")
+        coef = torch.empty(4 * C, device="cuda")
         dgamma, dbeta = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
         K.bn_bwd(d["gz"], 1, d["gz"], d["z"], d["scale"], d["shift"], d["mean"], d["invstd"], d["gamma"], part, coef,
                  dgamma, dbeta, None, dz, False, act, d["res"] if act == 2 and mask is None else None, dres,

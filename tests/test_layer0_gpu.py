@@ -87,7 +87,7 @@ def test_layer0_fused_forward_and_backward(N, CP):
     C.bn_apply(z, a32, scale, shift, True)
     g = ops["gout"].clone()
     bpart = torch.zeros(C.bn_part_floats(N * 256, 64, True), device=dev)
-    coef = torch.empty(3 * 64, device=dev)
+    coef = torch.empty(4 * 64, device=dev)
     wpart = torch.empty(C.wgrad0_part_floats(N), device=dev)
     dg, db, dbias = (torch.zeros(64, device=dev) for _ in range(3))
     dw = torch.empty_like(ops["w"])

@@ -44,7 +44,7 @@ def test_bn_backward_wide_geometry(act):
                    False, act, res, dres_ref)
     d = lambda t: t.cuda()
     part = torch.zeros(C_.bn_part_floats(N * H * W, C, True), device="cuda")
-    coef = torch.empty(3 * C, device="cuda")
+    coef = torch.empty(4 * C, device="cuda")
     out = [torch.zeros(C, device="cuda") for _ in range(3)]
     dz = torch.empty(z.shape, device="cuda")
     dres = torch.empty(z.shape, device="cuda") if act == 2 else None
@@ -82,7 +82,7 @@ def test_bn_backward_matches_torch_autograd():
     out = [torch.zeros(C, device="cuda") for _ in range(3)]
     dz = torch.empty(z.shape, device="cuda")
     part = torch.zeros(C_.bn_part_floats(N * H * W // 4, C, True), device="cuda")
-    coef = torch.empty(3 * C, device="cuda")
+    coef = torch.empty(4 * C, device="cuda")
     gg = d(gy.float().permute(0, 2, 3, 1))
     C_.bn_bwd(gg, 1, gg, d(z), d(scale), d(shift), d(mean), d(invstd), d(gamma), part, coef,
               out[0], out[1], out[2], dz, True)

@@ -182,29 +182,29 @@ def test_all_gradients_fp32_grade(errors, impl):
 
 
 def _trained_state(steps=200):
-    """The reference-layout state after ``steps`` x3 (fp32-grade) training steps of the bench's own
-    loop on its synthetic data (lr 0.1): weights and BN statistics far from the random init, where
-    activations, gradient magnitudes and the fp16-pair bounds are those of real training."""
-    from distributed_pytorch_amd.data import DeviceLoader, ShardSampler, synthetic_cifar
-    from distributed_pytorch_amd.engine import VGGEngine
+    """The reference-layout state after ``steps`` training steps (lr 0.1, momentum 0.9, wd 1e-4,
+    batch 256) on the bench's synthetic data: weights and BN statistics far from the random init,
+    where activations, gradient magnitudes and the fp16-pair bounds are those of real training.
+    Trained with stock torch on the GPU (deterministic MIOpen algorithms), so the state -- and every
+    error measured from it -- does not move when the framework's own kernels change."""
+    from distributed_pytorch_amd.data import synthetic_cifar
+    from distributed_pytorch_amd.models import VGG11
 
-    train = synthetic_cifar(50000, 0)
-    loader = DeviceLoader(train, N, "cuda", sampler=ShardSampler(len(train), 1, 0, shuffle=True, seed=0),
-                          train=True, seed=7919, drop_last=True)
-    e = VGGEngine("VGG11", "cuda", max_batch=N, impl="x3")
-    e.init_parameters(seed=1)
-    done = 0
-    while done < steps:
-        for x, t in loader:
-            e.forward_backward(x, t)
-            e.sgd_step()
-            e.finish_step()
-            done += 1
-            if done == steps:
-                break
-    e.check_signals()
-    assert float(e.loss.item()) == float(e.loss.item())
-    return e.state_dict()
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+    torch.manual_seed(1)
+    m = VGG11().cuda()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    train = synthetic_cifar(N * 50, 0)
+    imgs = train.images.cuda().permute(0, 3, 1, 2).float().div_(255.0).sub_(0.5).div_(0.25)
+    labels = train.labels.cuda()
+    for i in range(steps):
+        j = (i % 50) * N
+        opt.zero_grad(set_to_none=True)
+        F.cross_entropy(m(imgs[j:j + N]), labels[j:j + N]).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    return {k: v.detach().cpu() for k, v in m.state_dict().items()}
 
 
 @pytest.fixture(scope="module")
@@ -216,7 +216,7 @@ def trained_errors():
 @pytest.mark.parametrize("impl", ["x3", "h2"])
 def test_parity_at_trained_state(trained_errors, impl):
     """the same whole-step fp64 comparison from a TRAINED state (200 steps of
-    the bench's training on its synthetic data), where the fixed fp16-pair scales and the
+    training on the bench's synthetic data, _trained_state), where the fixed fp16-pair scales and the
     data-gradient bounds meet the magnitudes of real training rather than of the random init:
     loss, every gradient tensor within 4x of the step's error floor, median no worse than torch
     fp32, updates to fp32 rounding."""
