@@ -24,7 +24,12 @@ def _taps(model, x, t):
     output, from one forward + backward of ``model`` on (x, t)."""
     convs = [m for m in model.modules() if isinstance(m, nn.Conv2d)]
     outs = []
-    hs = [c.register_forward_hook(lambda m, i, o: (o.retain_grad(), outs.append(o))) for c in convs]
+
+    def hook(m, i, o):
+        o.retain_grad()
+        outs.append(o)
+
+    hs = [c.register_forward_hook(hook) for c in convs]
     loss = F.cross_entropy(model(x), t)
     loss.backward()
     for h in hs:
