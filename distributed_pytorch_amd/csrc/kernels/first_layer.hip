@@ -58,7 +58,8 @@ __device__ __forceinline__ void conv0_px(const float4 (*xs)[XC], int r, int c, c
 
 // Built without gfx950's packed fp32 instructions (v_pk_fma_f32): see docs/PERF_NOTES.md round 6 --
 // under multi-process load, this kernel's packed FMAs produced wrong values for one 16-lane pass
-// (one component, one pixel) now and then; the scalar v_fma_f32 form does not.
+// (one component, one pixel) now and then; the scalar v_fma_f32 form does not (+8.8 us: the doubled
+// VALU instruction count only partly hides under the output store).
 // (the host compilation pass ignores the attribute: -Wignored-attributes is silenced there)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wignored-attributes"

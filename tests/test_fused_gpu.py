@@ -42,7 +42,7 @@ def test_bn_bwd_wgrad0_matches_reference(N, nsplit, cp):
     cu = lambda t: t.contiguous().cuda()
     out = {k: torch.zeros(C_, device="cuda") for k in ("dgamma", "dbeta", "dbias")}
     part = torch.zeros(C.bn_part_floats(N * 256, C_, True), device="cuda")
-    coef = torch.zeros(3 * C_, device="cuda")
+    coef = torch.zeros(4 * C_, device="cuda")  # [k1, c2, k3, mean]
     wpart = torch.empty(C.wgrad0_part_floats(N), device="cuda")
     dw = torch.full((C_, 3, 3, cp), 7.0, device="cuda")  # padded channels must come back as 0
     g = torch.empty(N, 16, 16, C_, device="cuda")
