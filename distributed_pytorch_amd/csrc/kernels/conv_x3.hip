@@ -1030,8 +1030,11 @@ struct HArgs {
   const unsigned* obound;
 };
 
-// staged slots per block: BM + 2W + 2 pixels (W <= BM/4 - 1) and the zero slot (the last one)
-__host__ __device__ constexpr int halo_slots(int BM) { return BM + BM / 2 + 1; }
+// staged slots per block: BM + 2W + 2 pixels and the zero slot (the last one).  Chunks of up to 32
+// channels size the image for rows of up to BM/4 - 1 pixels.  64-channel chunks (tiles 22, 23: twice
+// the reduction per barrier, bf16 / fp16-pair planes) size it for rows of at most 16 pixels, so that
+// with NP 2 the image (74.5 KB) and the double-buffered weight tiles (64 KB) fit the 160 KB of LDS.
+__host__ __device__ constexpr int halo_slots(int BM, int BC) { return BC >= 64 ? BM + 2 * 16 + 3 : BM + BM / 2 + 1; }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, bool OB>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs a) {
@@ -1042,7 +1045,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
   constexpr int CPR = BC / 8;    // 16-B chunks per staged row
   constexpr int RPB = 16 / CPR;  // staged rows per 256-B bank row
-  constexpr int SLOTS = halo_slots(BM), ZS = SLOTS - 1;
+  constexpr int SLOTS = halo_slots(BM, BC), ZS = SLOTS - 1;
   constexpr int A_PLANE = SLOTS * BC;
   constexpr bool BSWZ = DG && BN >= 128;
   constexpr int BPITCH = DG ? (BSWZ ? BN : BN + 32) : BC;
@@ -1937,11 +1940,13 @@ int xsplits(int Kred, int splits) {
 //                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32,
 //                  20 = 256x64 / 32 (8 waves of 64x32), 21 = 128x64 / 32 (4 waves of 64x32) for
 //                  64-channel outputs (e.g. the data gradient into a 64-channel layer),
+//                  22 = 256x128 / 64, 23 = 256x64 / 64 (8 waves; rows <= 16 pixels, NP 1 or 2):
+//                  four k-steps of MFMAs per barrier instead of two,
 //   WGRAD:         16 = 64-pixel chunks, 17 = 32-pixel chunks
-bool is_halo(int tile) { return tile >= 16 && tile <= 21; }
-int halo_bm(int tile) { return (tile <= 17 || tile == 20) ? 256 : 128; }
-int halo_bn(int tile) { return tile == 20 || tile == 21 ? 64 : 128; }
-int halo_bc(int tile) { return (tile & 1) || tile == 20 ? 32 : 16; }
+bool is_halo(int tile) { return tile >= 16 && tile <= 23; }
+int halo_bm(int tile) { return (tile <= 17 || tile == 20 || tile >= 22) ? 256 : 128; }
+int halo_bn(int tile) { return tile == 20 || tile == 21 || tile == 23 ? 64 : 128; }
+int halo_bc(int tile) { return tile >= 22 ? 64 : ((tile & 1) || tile == 20 ? 32 : 16); }
 
 template <int BM, int BN, int WM, int WN, bool DG, int NP, int BC, bool OB>
 int launch_halo(const HArgs& a, int splits, hipStream_t st) {
@@ -1958,16 +1963,26 @@ int launch_halo_tile(const HArgs& a, int tile, int splits, hipStream_t st) {
     case 18: return launch_halo<128, 128, 2, 2, DG, NP, 16, OB>(a, splits, st);
     case 20: return launch_halo<256, 64, 4, 2, DG, NP, 32, OB>(a, splits, st);
     case 21: return launch_halo<128, 64, 2, 2, DG, NP, 32, OB>(a, splits, st);
+    case 22:
+    case 23:
+      if constexpr (NP == 3) {  // three planes of a 64-channel chunk do not fit the LDS
+        return -6;
+      } else {
+        return tile == 22 ? launch_halo<256, 128, 4, 2, DG, NP, 64, OB>(a, splits, st)
+                          : launch_halo<256, 64, 4, 2, DG, NP, 64, OB>(a, splits, st);
+      }
     default: return launch_halo<128, 128, 2, 2, DG, NP, 32, OB>(a, splits, st);
   }
 }
 
-// -6: the conv does not fit the halo tile (channels, or rows wider than BM/4 - 1 pixels)
+// -6: the conv does not fit the halo tile (channels, rows wider than the staged image allows, or
+// three planes of a 64-channel chunk)
 template <bool DG>
 int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st,
              const void* add = nullptr) {
   const int BM = halo_bm(tile), BC = halo_bc(tile);
-  if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM) - 1) return -6;
+  if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM, BC) - 1) return -6;
+  if (BC >= 64 && np == 3) return -6;
   if (obf && np != 1) return -4;  // bf16 output from one-plane operands (unreduced slabs stay fp32)
   a.M = a.N * a.H * a.W;
   a.gm = cdiv(a.M, BM);

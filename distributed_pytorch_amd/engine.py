@@ -98,24 +98,32 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
 
 # Halo-staged 3x3/s1/p1 tiles of conv_x3.hip (ids after the 16 implicit-GEMM tiles): the block's
 # input pixels are staged once per channel chunk and the 9 taps read shifted views of them.
-HALO_TILES = (16, 17, 18, 19, 20, 21)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19) or 64 (20, 21)
-                                       # output channels, 16 or 32-channel chunks
+HALO_TILES = (16, 17, 18, 19, 20, 21, 22, 23)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19, 22) or 64
+                                               # (20, 21, 23) output channels, 16-, 32- or 64-channel
+                                               # chunks (22, 23: rows <= 16 pixels, not with x3's 3 planes)
+# tile -> (rows BM, channel chunk BC, staged image slots) of conv_x3.hip's halo_bm / halo_bc / halo_slots
+HALO_GEOM = {16: (256, 16), 17: (256, 32), 18: (128, 16), 19: (128, 32), 20: (256, 32), 21: (128, 32),
+             22: (256, 64), 23: (256, 64)}
 HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
 POS_TILES = (24, 25, 26, 27, 28, 29)  # fprop / dgrad of small images: position-major rows, padding taps
                                       # skipped (conv_x3.hip conv_pos_kernel)
 
 
-def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8) -> bool:
+def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8, np_: int = 2) -> bool:
     """Whether halo tile `tile` runs conv call `kind` of a 3x3/s1/p1 conv whose rows are w pixels
     wide.  cred: channels reduced (fprop C_in, dgrad C_out; wgrad C_in), cout: output channels
-    (wgrad C_out).  Mirrors run_halo / run_halo_wgrad in conv_x3.hip (-6 otherwise)."""
+    (wgrad C_out), np_: operand planes (1 bf16, 2 h2, 3 x3).  Mirrors run_halo / run_halo_wgrad in
+    conv_x3.hip (-6 otherwise)."""
     if kind == "wgrad":
         p = {16: 64, 17: 32}.get(tile)
         return p is not None and cred % 8 == 0 and cout % 8 == 0 and p + 2 * w + 2 <= 2 * p + 3
     if tile not in HALO_TILES:
         return False
-    bm, bc = (256 if tile in (16, 17, 20) else 128), (32 if tile & 1 or tile == 20 else 16)
-    return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= bm + bm // 2
+    bm, bc = HALO_GEOM[tile]
+    slots = bm + 35 if bc >= 64 else bm + bm // 2 + 1
+    if bc >= 64 and np_ == 3:
+        return False
+    return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= slots - 1
 
 
 def pos_ok(kind: str, tile: int, h: int, w: int, cred: int, cout: int) -> bool:
@@ -547,7 +555,8 @@ class VGGEngine:
                 ok = [t for t in HALO_WGRAD_TILES if halo_ok(kind, t, l.hw, l.cin_pad, l.cout)]
             else:
                 cred, cout = (l.cin_pad, l.cout) if kind == "fprop" else (l.cout, l.cin_pad)
-                ok = [t for t in HALO_TILES if halo_ok(kind, t, l.hw, cred, cout)]
+                np_ = {"x3": 3, "h2": 2}.get(impl, 1)
+                ok = [t for t in HALO_TILES if halo_ok(kind, t, l.hw, cred, cout, np_)]
                 ok += [t for t in POS_TILES if pos_ok(kind, t, l.hw, l.hw, cred, cout)]
             out += [(t, s, False) for t in ok for s in splits]
         return out

@@ -139,9 +139,9 @@ def save_tuning_table(path: Optional[str] = None):
     _AUTOTUNE["dirty"] = False
 
 
-def halo_candidates(kind: str, geom: tuple) -> Tuple[int, ...]:
+def halo_candidates(kind: str, geom: tuple, np_: int = 1) -> Tuple[int, ...]:
     """Halo-staged tiles (conv_x3.hip, ids >= 16) that can run this conv call: 3x3, stride 1,
-    pad 1 only, channel / row-width limits as in engine.halo_ok."""
+    pad 1 only, channel / row-width / plane-count limits as in engine.halo_ok."""
     from ..engine import HALO_TILES, HALO_WGRAD_TILES, halo_ok
 
     N, H, W, C, K, R, S, stride, pad = geom
@@ -150,7 +150,7 @@ def halo_candidates(kind: str, geom: tuple) -> Tuple[int, ...]:
     if kind == "wgrad":
         return tuple(t for t in HALO_WGRAD_TILES if halo_ok("wgrad", t, W, C, K))
     cred, cout = (C, K) if kind == "fprop" else (K, C)
-    return tuple(t for t in HALO_TILES if halo_ok(kind, t, W, cred, cout))
+    return tuple(t for t in HALO_TILES if halo_ok(kind, t, W, cred, cout, np_))
 
 
 STREAM_TILES = (30,)  # conv_x3.hip gemm_stream_kernel: 1x1 / stride 1 / pad 0 fprop + dgrad, bf16, one split
@@ -209,7 +209,7 @@ def choose_config(impl: str, kind: str, geom: tuple, M: int, Ngemm: int, Kred: i
         c = (int(t[0]), int(t[1]), bool(t[2]))
     elif _AUTOTUNE["on"] and run is not None:
         c = _autotune(key, kind, M if kind == "wgrad" else Kred, run, slab_bytes,
-                      halo_candidates(kind, geom) + stream_candidates(impl, kind, geom))
+                      halo_candidates(kind, geom, {"x3": 3, "h2": 2}.get(impl, 1)) + stream_candidates(impl, kind, geom))
     else:
         c = conv_config(kind, M, Ngemm, Kred, hw_small)
     _chosen[key] = c

@@ -379,28 +379,29 @@ HALO_SHAPES = [
     (1, 56, 56, 16, 16),    # rows of 56 pixels (fits the 256-pixel tiles only)
     (3, 16, 16, 128, 64),   # VGG layer-1-like data gradient into 64 channels (tiles 20/21)
     (2, 8, 8, 64, 96),      # 96 output channels: one full and one partial 64-column tile
+    (2, 12, 12, 192, 128),  # three 64-channel chunks (tiles 22/23), partial 256-pixel block
 ]
 
 
-def _halo_ok(kind, tile, w, cred, cout):
+def _halo_ok(kind, tile, w, cred, cout, np_=2):
     from distributed_pytorch_amd.engine import halo_ok
 
-    return halo_ok(kind, tile, w, cred, cout)
+    return halo_ok(kind, tile, w, cred, cout, np_)
 
 
 @pytest.mark.parametrize("shape", HALO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
-@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21, 22, 23])
 @pytest.mark.parametrize("np_", [3, 2, 1])
 @pytest.mark.parametrize("dgrad", [False, True])
 def test_conv_halo(shape, splits, tile, np_, dgrad):
-    """Halo-staged 3x3 fprop / data gradient (tiles 16-21) against fp64: partial blocks, blocks
-    across image boundaries, bands of rows, partial column tiles (128- and 64-column tiles) and
-    split-K."""
+    """Halo-staged 3x3 fprop / data gradient (tiles 16-23) against fp64: partial blocks, blocks
+    across image boundaries, bands of rows, partial column tiles (128- and 64-column tiles),
+    32- and 64-channel chunks and split-K."""
     C = _C()
     N, H, W, Cin, K = shape
     cred, cout = (K, Cin) if dgrad else (Cin, K)
-    if not _halo_ok("dgrad" if dgrad else "fprop", tile, W, cred, cout):
+    if not _halo_ok("dgrad" if dgrad else "fprop", tile, W, cred, cout, np_):
         pytest.skip("shape outside this halo tile")
     g = torch.Generator().manual_seed(17)
     x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).requires_grad_(dgrad)
@@ -569,11 +570,12 @@ EPI_SHAPES = [
     (3, 9, 9, 32, 48, 3, 1, 1),      # partial row tile, partial column tile
     (2, 14, 14, 64, 128, 1, 1, 0),   # 1x1 (ResNet bottleneck)
     (4, 8, 8, 16, 64, 3, 2, 1),      # strided
+    (3, 9, 9, 64, 48, 3, 1, 1),      # 64-channel chunks (halo tiles 22/23)
 ]
 
 
 @pytest.mark.parametrize("shape", EPI_SHAPES)
-@pytest.mark.parametrize("tile", [0, 1, 5, 7, 11, 14, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("tile", [0, 1, 5, 7, 11, 14, 16, 17, 18, 19, 20, 21, 22, 23])
 @pytest.mark.parametrize("np_", [1, 2, 3])
 @pytest.mark.parametrize("posmajor", [0, 1])
 def test_conv_epilogue_bn_stats(shape, tile, np_, posmajor):
@@ -583,7 +585,7 @@ def test_conv_epilogue_bn_stats(shape, tile, np_, posmajor):
     rounding of the stored values' statistics)."""
     C_ = _C()
     N, H, W, Cin, K, R, st, pd = shape
-    if tile >= 16 and (R != 3 or st != 1 or not _halo_ok("fprop", tile, W, Cin, K)):
+    if tile >= 16 and (R != 3 or st != 1 or not _halo_ok("fprop", tile, W, Cin, K, np_)):
         pytest.skip("halo tiles are 3x3/s1 only")
     if tile >= 16 and posmajor:
         pytest.skip("halo tiles ignore the row order")
