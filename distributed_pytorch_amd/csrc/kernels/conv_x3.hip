@@ -1030,11 +1030,13 @@ struct HArgs {
   const unsigned* obound;
 };
 
-// staged slots per block: BM + 2W + 2 pixels and the zero slot (the last one).  Chunks of up to 32
-// channels size the image for rows of up to BM/4 - 1 pixels.  64-channel chunks (tiles 22, 23: twice
-// the reduction per barrier, bf16 / fp16-pair planes) size it for rows of at most 16 pixels, so that
-// with NP 2 the image (74.5 KB) and the double-buffered weight tiles (64 KB) fit the 160 KB of LDS.
-__host__ __device__ constexpr int halo_slots(int BM, int BC) { return BC >= 64 ? BM + 2 * 16 + 3 : BM + BM / 2 + 1; }
+// staged slots per block: BM + 2W + 2 pixels and the zero slot (the last one), sized for rows of up
+// to BM/4 - 1 pixels -- except fp16-pair planes of 64-channel chunks (tiles 22, 23: twice the
+// reduction per barrier), whose image is sized for rows of at most 16 pixels so that it (74.5 KB)
+// and the double-buffered weight tiles (64 KB) fit the 160 KB of LDS.
+__host__ __device__ constexpr int halo_slots(int BM, int BC, int NP) {
+  return BC >= 64 && NP >= 2 ? BM + 2 * 16 + 3 : BM + BM / 2 + 1;
+}
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool DG, int NP, int BC, bool OB>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs a) {
@@ -1045,7 +1047,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
   constexpr int CPR = BC / 8;    // 16-B chunks per staged row
   constexpr int RPB = 16 / CPR;  // staged rows per 256-B bank row
-  constexpr int SLOTS = halo_slots(BM, BC), ZS = SLOTS - 1;
+  constexpr int SLOTS = halo_slots(BM, BC, NP), ZS = SLOTS - 1;
   constexpr int A_PLANE = SLOTS * BC;
   constexpr bool BSWZ = DG && BN >= 128;
   constexpr int BPITCH = DG ? (BSWZ ? BN : BN + 32) : BC;
@@ -1940,7 +1942,7 @@ int xsplits(int Kred, int splits) {
 //                  18 = 128x128 / 16 (4 waves), 19 = 128x128 / 32,
 //                  20 = 256x64 / 32 (8 waves of 64x32), 21 = 128x64 / 32 (4 waves of 64x32) for
 //                  64-channel outputs (e.g. the data gradient into a 64-channel layer),
-//                  22 = 256x128 / 64, 23 = 256x64 / 64 (8 waves; rows <= 16 pixels, NP 1 or 2):
+//                  22 = 256x128 / 64, 23 = 256x64 / 64 (8 waves; NP 1, or NP 2 with rows <= 16 px):
 //                  four k-steps of MFMAs per barrier instead of two,
 //   WGRAD:         16 = 64-pixel chunks, 17 = 32-pixel chunks
 bool is_halo(int tile) { return tile >= 16 && tile <= 23; }
@@ -1981,7 +1983,7 @@ template <bool DG>
 int run_halo(HArgs& a, int tile, int splits, int np, int obf, float* slab, void* out, int reduce, hipStream_t st,
              const void* add = nullptr) {
   const int BM = halo_bm(tile), BC = halo_bc(tile);
-  if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM, BC) - 1) return -6;
+  if (a.C % BC || a.Nout % 8 || BM + 2 * a.W + 2 > halo_slots(BM, BC, np) - 1) return -6;
   if (BC >= 64 && np == 3) return -6;
   if (obf && np != 1) return -4;  // bf16 output from one-plane operands (unreduced slabs stay fp32)
   a.M = a.N * a.H * a.W;

@@ -100,8 +100,8 @@ def conv_key(impl: str, kind: str, n: int, hw: int, cin: int, cout: int) -> str:
 # input pixels are staged once per channel chunk and the 9 taps read shifted views of them.
 HALO_TILES = (16, 17, 18, 19, 20, 21, 22, 23)  # fprop / dgrad: 256 or 128 pixels x 128 (16-19, 22) or 64
                                                # (20, 21, 23) output channels, 16-, 32- or 64-channel
-                                               # chunks (22, 23: rows <= 16 pixels, not with x3's 3 planes)
-# tile -> (rows BM, channel chunk BC, staged image slots) of conv_x3.hip's halo_bm / halo_bc / halo_slots
+                                               # chunks (22, 23: not x3's 3 planes; h2 rows <= 16 pixels)
+# tile -> (rows BM, channel chunk BC) of conv_x3.hip's halo_bm / halo_bc (image slots: halo_slots)
 HALO_GEOM = {16: (256, 16), 17: (256, 32), 18: (128, 16), 19: (128, 32), 20: (256, 32), 21: (128, 32),
              22: (256, 64), 23: (256, 64)}
 HALO_WGRAD_TILES = (16, 17)          # wgrad: 64- or 32-pixel chunks, 128 x 32 x 9 taps per block
@@ -120,7 +120,7 @@ def halo_ok(kind: str, tile: int, w: int, cred: int, cout: int = 8, np_: int = 2
     if tile not in HALO_TILES:
         return False
     bm, bc = HALO_GEOM[tile]
-    slots = bm + 35 if bc >= 64 else bm + bm // 2 + 1
+    slots = bm + 35 if bc >= 64 and np_ >= 2 else bm + bm // 2 + 1
     if bc >= 64 and np_ == 3:
         return False
     return cred % bc == 0 and cout % 8 == 0 and bm + 2 * w + 2 <= slots - 1

@@ -380,6 +380,7 @@ HALO_SHAPES = [
     (3, 16, 16, 128, 64),   # VGG layer-1-like data gradient into 64 channels (tiles 20/21)
     (2, 8, 8, 64, 96),      # 96 output channels: one full and one partial 64-column tile
     (2, 12, 12, 192, 128),  # three 64-channel chunks (tiles 22/23), partial 256-pixel block
+    (1, 28, 28, 64, 64),    # rows of 28 pixels: 64-channel chunks with one plane only (NP 2 needs <= 16)
 ]
 
 

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "halo64_ab.json"))
+    ap.add_argument("--all", action="store_true", help="also calls whose current plan is not a halo tile")
+    ap.add_argument("--only", default="", help="comma-separated conv_key substrings")
     a = ap.parse_args()
     n = a.batch
     e = VGGEngine("VGG11", "cuda", max_batch=n, impl=a.impl)
@@ -46,10 +48,12 @@ def main():
                 continue
             impl = e._layer_impl(i)
             key = (impl, kind, n, i)
-            cur = e.conv_config(i, kind, n)
-            if not (16 <= cur[0] <= 23):
+            if a.only and not any(o in conv_key(impl, kind, n, l.hw, l.cin_pad, l.cout) for o in a.only.split(",")):
                 continue
+            cur = e.conv_config(i, kind, n)
             cred, cout = (l.cin_pad, l.cout) if kind == "fprop" else (l.cout, l.cin_pad)
+            if not (16 <= cur[0] <= 23 or (a.all and halo_ok(kind, 22, l.hw, cred, cout, np_))):
+                continue
             cands = [cur]
             for tile in (22, 23):
                 if not halo_ok(kind, tile, l.hw, cred, cout, np_):
