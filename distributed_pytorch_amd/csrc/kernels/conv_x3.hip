@@ -1228,6 +1228,19 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
   // ---- main loop: step = (chunk, tap).  The weight tile of step st+1 is written to the other
   // buffer after step st's MFMAs (its loads were issued a step earlier); the next chunk's pixels
   // sit in registers during the 9 taps and replace the staged image at the chunk boundary.
+  // fp16-pair 64-channel chunks: each chunk's 9 x 64 products per output go to a fresh accumulator
+  // that is then added to the running total -- the fp32 rounding of a long reduction grows with
+  // the chain, and this cuts the chain to one chunk plus one add per chunk (64 adds per wave)
+  constexpr bool CACC = BC >= 64 && NP == 2;
+  f32x16 tot[CACC ? TM : 1][CACC ? TN : 1];
+  if constexpr (CACC) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tot[i][j][r] = 0.f;
+  }
   const int nch = a.C / BC;
   const int cb = blockIdx.y * a.cps, ce = min(nch, cb + a.cps);
   const int nsteps = max(0, ce - cb) * 9;
@@ -1243,6 +1256,19 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
     for (int st = 0; st < nsteps; ++st) {
       compute(tap, st & 1);
       const bool last_tap = tap == 8;
+      if constexpr (CACC) {
+        if (last_tap) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                tot[i][j][r] += acc[i][j][r];
+                acc[i][j][r] = 0.f;
+              }
+        }
+      }
       const int tap1 = last_tap ? 0 : tap + 1, ch1 = last_tap ? ch + 1 : ch;  // step st + 1
       if (st + 1 < nsteps) {
         store_b((st + 1) & 1);
@@ -1257,6 +1283,14 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_halo_kernel(HArgs 
       tap = tap1;
       ch = ch1;
     }
+  }
+  if constexpr (CACC) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r];
   }
 
   // ---------------- epilogue (rows are NHWC pixels) ----------------
