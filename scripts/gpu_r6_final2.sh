@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-O=gpurun_out/val7
+O=${OUT:-gpurun_out/val7}
 mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
 tail -3 $O/gpu_tests.log; grep -E "^FAILED|^ERROR" $O/gpu_tests.log | head -10
