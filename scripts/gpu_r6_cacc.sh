@@ -12,7 +12,7 @@ timeout -k 10 600 python -u -m pytest tests/test_parity256_gpu.py -q --timeout 3
   -k "fp32_grade or trained_state or loss_matches" > gpurun_out/cacc_parity.log 2>&1
 cp gpurun_out/parity256_errors.json gpurun_out/parity256_trained_errors.json gpurun_out/cacc/
 tail -1 gpurun_out/cacc_parity.log
-DPA_TUNING_EXTRA=$PWD/distributed_pytorch_amd/tuning/ab_l3_epi.json timeout -k 10 600 python -u -m pytest tests/test_parity256_gpu.py -q \
+DPA_TUNING_EXTRA=$PWD/distributed_pytorch_amd/tuning/ab/ab_l3_epi.json timeout -k 10 600 python -u -m pytest tests/test_parity256_gpu.py -q \
   --timeout 300 --timeout-method thread -k "fp32_grade or trained_state or loss_matches" > gpurun_out/cacc_l3_parity.log 2>&1
 cp gpurun_out/parity256_errors.json gpurun_out/parity256_trained_errors.json gpurun_out/cacc_l3/
 tail -1 gpurun_out/cacc_l3_parity.log

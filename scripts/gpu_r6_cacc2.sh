@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-T=distributed_pytorch_amd/tuning
+T=distributed_pytorch_amd/tuning/ab
 mkdir -p gpurun_out/cacc_l345
 AB_ENVS="|DPA_TUNING_EXTRA=$T/ab_l3_epi.json|DPA_TUNING_EXTRA=$T/ab_l345.json" REPS=4 bash scripts/gpu_ab.sh 2>&1 | tee gpurun_out/cacc_step_ab.log || exit 1
 DPA_TUNING_EXTRA=$PWD/$T/ab_l345.json timeout -k 10 600 python -u -m pytest tests/test_parity256_gpu.py -q \

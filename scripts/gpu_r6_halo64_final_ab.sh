@@ -3,4 +3,4 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-AB_ENVS="DPA_TUNING_EXTRA=distributed_pytorch_amd/tuning/ab_old_r6.json|DPA_AB_NEW=1" REPS=4 bash scripts/gpu_ab.sh 2>&1 | tee gpurun_out/halo64_final_ab.log
+AB_ENVS="DPA_TUNING_EXTRA=distributed_pytorch_amd/tuning/ab/ab_old_r6.json|DPA_AB_NEW=1" REPS=4 bash scripts/gpu_ab.sh 2>&1 | tee gpurun_out/halo64_final_ab.log
