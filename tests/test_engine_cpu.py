@@ -270,3 +270,20 @@ def test_fused_step_matches_single_update(mode, monkeypatch):
             assert all(stepped)
         out.append((e.params.flat.clone(), e.mom.flat.clone()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def test_halo_tile_geometry_rules():
+    """engine.halo_ok mirrors conv_x3.hip run_halo: 64-channel-chunk tiles (22, 23) need C % 64,
+    never run x3's three planes, and with fp16 pairs stage rows of at most 16 pixels (one bf16 plane
+    keeps the BM/4 - 1 limit of the other tiles)."""
+    from distributed_pytorch_amd.engine import HALO_GEOM, halo_ok
+
+    for t in (22, 23):
+        assert HALO_GEOM[t] == (256, 64)
+        assert halo_ok("fprop", t, 16, 64, 128, 2) and not halo_ok("fprop", t, 17, 64, 128, 2)
+        assert halo_ok("fprop", t, 56, 64, 64, 1) and not halo_ok("fprop", t, 64, 64, 64, 1)
+        assert not halo_ok("fprop", t, 8, 64, 128, 3)
+        assert not halo_ok("dgrad", t, 8, 96, 128, 2)
+    # the 32-channel tiles are unchanged: rows up to BM/4 - 1 for every plane count
+    assert halo_ok("fprop", 17, 63, 32, 64, 3) and not halo_ok("fprop", 17, 64, 32, 64, 3)
+    assert halo_ok("dgrad", 21, 31, 32, 64, 2) and not halo_ok("dgrad", 21, 32, 32, 64, 2)
